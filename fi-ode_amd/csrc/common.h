@@ -1,0 +1,184 @@
+// Device helpers shared by the FI-ODE gfx950 kernels.
+//
+// Numerics: this file is compiled with -ffp-contract=off, so every a*b+c below rounds twice
+// exactly like the reference's eager float32 torch ops; fused multiply-adds appear only where
+// written (the MFMA contractions, which are a k-ordered fmaf chain).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FIODE_C 10
+#define FIODE_M 128
+#define FIODE_X 10
+#define FIODE_TILE 32          // rows (samples) per wave tile = MFMA 32x32 N dimension
+#define FIODE_WAVES 4          // waves per workgroup
+#define FIODE_LDQ 132          // padded LDS row stride (floats) of 128-wide weight images
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f32_32x32x2_f32: lane l supplies A[i=l&31][k=l>>5], B[k=l>>5][j=l&31];
+// accumulator register r of lane l holds D[row=(r&3)+8*(r>>2)+4*(l>>5)][col=l&31].
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+__device__ __forceinline__ f32x16 f16_zero() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// ---- Philox4x32-10 counter-based RNG (stateless; key = seed, counter = (index, stream, offset)) ---
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0;
+    k.y += W1;
+  }
+  return c;
+}
+
+struct Rng {
+  uint2 key;
+  uint32_t off_lo, off_hi;
+  __device__ __forceinline__ uint4 draw(uint32_t index, uint32_t stream) const {
+    return philox4x32_10(make_uint4(index, stream, off_lo, off_hi), key);
+  }
+};
+
+// Philox streams (second counter word).  Sampler draws: 3 calls per row (12 words >= 10).
+#define RNG_STREAM_UNIFORM 0x100u     // + call, index = s (shared across the batch)
+#define RNG_STREAM_CONE 0x200u        // + call, index = row
+#define RNG_STREAM_DB 0x300u          // + call, index = row
+#define RNG_STREAM_DROP 0x1000u       // + (mask_set << 4) + call, index = row
+
+// Exp(1) variate from 24 random bits: -log(u), u in (0, 1].
+__device__ __forceinline__ float exp1_from_bits(uint32_t x) {
+  const float u = (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);
+  return -logf(u);
+}
+
+// ---- wave helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ float shfl_xor32(float v) { return __shfl_xor(v, 32, 64); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_and(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v &= (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
+// ---- row-level math shared by every kernel (one lane = one row of C=10) ---------------------
+
+// F.normalize(x, p=1): x / max(sum |x|, 1e-12), sequential sum.
+__device__ __forceinline__ void l1_normalize(float (&x)[FIODE_C]) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < FIODE_C; ++j) s = s + fabsf(x[j]);
+  s = fmaxf(s, 1e-12f);
+#pragma unroll
+  for (int j = 0; j < FIODE_C; ++j) x[j] = x[j] / s;
+}
+
+struct DynScalars {
+  float alpha_1, alpha_2, sigma_1, tol;
+  int scale_nominal, max_iter;
+};
+
+// lower = -alpha_1*(exp(sigma_1*h) - 1); upper = alpha_2*(1-h); nominal = scale ? (upper-lower)*sig + lower : ft
+__device__ __forceinline__ void barrier_nominal(const DynScalars& d, const float (&h)[FIODE_C],
+                                                const float (&ft)[FIODE_C], float (&lower)[FIODE_C],
+                                                float (&nominal)[FIODE_C], float (&sig)[FIODE_C],
+                                                float (&span)[FIODE_C]) {
+#pragma unroll
+  for (int j = 0; j < FIODE_C; ++j) {
+    lower[j] = -d.alpha_1 * (expf(d.sigma_1 * h[j]) - 1.0f);
+    const float upper = d.alpha_2 * (1.0f - h[j]);
+    span[j] = upper - lower[j];
+    if (d.scale_nominal) {
+      sig[j] = 1.0f / (1.0f + expf(-ft[j]));
+      nominal[j] = span[j] * sig[j] + lower[j];
+    } else {
+      sig[j] = 0.f;
+      nominal[j] = ft[j];
+    }
+  }
+}
+
+// Bisection of FastBarrierProjectionNoUpper (barrier_projection.py:232-255) for one row.
+// Runs iterations 0..last (inclusive) and returns the per-iteration convergence bits of the
+// iterations run; v/mu hold the state of iteration `last`.
+__device__ __forceinline__ uint32_t qp_bisect(const float (&lower)[FIODE_C], const float (&nom)[FIODE_C],
+                                              int last, float tol, float (&v)[FIODE_C], float& mu) {
+  float hi = nom[0] - lower[0], lo = nom[0];
+#pragma unroll
+  for (int j = 1; j < FIODE_C; ++j) {
+    hi = fmaxf(hi, nom[j] - lower[j]);
+    lo = fminf(lo, nom[j]);
+  }
+  uint32_t conv = 0;
+  for (int it = 0; it <= last; ++it) {
+    mu = (hi - lo) / 2.0f + lo;
+    float eps = 0.f;
+#pragma unroll
+    for (int j = 0; j < FIODE_C; ++j) {
+      v[j] = fmaxf(nom[j] - mu, lower[j]);
+      eps = eps + v[j];
+    }
+    conv |= (fabsf(eps) < tol ? 1u : 0u) << it;
+    lo = eps > 0.f ? mu : lo;
+    hi = eps < 0.f ? mu : hi;
+  }
+  return conv;
+}
+
+// Global exit iteration from the AND of every row's convergence mask.
+__device__ __forceinline__ int qp_exit_iter(uint32_t and_mask, int max_iter) {
+  const uint32_t full = (max_iter >= 32) ? 0xFFFFFFFFu : ((1u << max_iter) - 1u);
+  const uint32_t m = and_mask & full;
+  return m ? (__ffs((int)m) - 1) : (max_iter - 1);
+}
+
+// QP backward (barrier_projection.py:288-311) closed form for one row.
+__device__ __forceinline__ void qp_backward_row(const float (&g)[FIODE_C], const float (&v)[FIODE_C], float mu,
+                                                const float (&nom)[FIODE_C], float (&g_nom)[FIODE_C],
+                                                float (&g_low)[FIODE_C]) {
+  bool act[FIODE_C];
+  int card = 0;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < FIODE_C; ++j) {
+    const float lam = (v[j] - nom[j]) + mu;
+    act[j] = lam > 0.f;
+    if (!act[j]) {
+      ++card;
+      s = s + g[j];
+    }
+  }
+  const float r = card > 0 ? 1.0f / (float)card : 0.f;
+  const float corr = r * s;
+#pragma unroll
+  for (int j = 0; j < FIODE_C; ++j) {
+    const float d = g[j] - corr;
+    g_nom[j] = act[j] ? 0.f : d;
+    g_low[j] = act[j] ? d : 0.f;
+  }
+}
+
+// Return code helpers for the C-ABI layer.
+#define FIODE_HIP_CHECK(expr)                       \
+  do {                                              \
+    hipError_t e_ = (expr);                         \
+    if (e_ != hipSuccess) return 100 + (int)e_;     \
+  } while (0)

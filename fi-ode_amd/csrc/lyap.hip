@@ -1,0 +1,618 @@
+// FI-ODE forward-invariance training step on gfx950 (MI355X).
+//
+// Replaces, below the Cayley maps, LyapunovLearning.compute_loss + loss.backward()
+// (pl_modules.py:390-502) and everything it calls on the per-sample path:
+//   sampler fan-out         sampling/sampler.py:34-38, 113-128, 139-153, 195-216
+//   dynamics f(h, x)        dynamics/classification.py:96-115
+//   QP projection fwd/bwd   barrier_projection/barrier_projection.py:217-313
+//   V, V-dot (jvp)          lya_cands.py:79-94, pl_modules.py:403-412
+//   hinge loss + logs       pl_modules.py:444-484
+//
+// Layout ("hidden on M, samples on N"): one wave owns a tile of 32 rows (samples).  Every layer
+// is computed transposed, Z^T[hidden x samples] = Q[hidden x in] * A^T[in x samples], with
+// v_mfma_f32_32x32x2_f32.  The accumulator of one layer (hidden index in registers, sample on
+// the lane) is directly the B operand of the next layer's MFMA (the K index of a k-step is the
+// register's row), so activations never leave registers between layers.  Weights live in LDS
+// (128x132-padded images read with ds_read_b128: 4 k-steps per read, conflict-free).
+//
+// Kernels of one step (stream-ordered, no host sync):
+//   k_static_proj  u[b] = U_x x_b + bx + b1, reset the QP exit words
+//   k_lyap_fwd     sampler, both eval_dot passes (loss pass + logging pass), per-row QP
+//                  convergence masks AND-reduced into one word per pass (batch-global exit,
+//                  barrier_projection.py:247-249), activations of the loss pass to HBM
+//   k_lyap_bwd     QP to the global exit, V / V-dot / hinge / logging stats, QP backward,
+//                  sigmoid backward, dL/da2 -> dL/dz2 -> dL/da1 -> dL/dz1 (MFMA)
+//   k_lyap_wgrad   weight gradients dQ2 = gz2^T a1, dQ3 = gft^T a2, dQ1 = gz1^T h (MFMA, K =
+//                  samples), split per image part into partial slabs (deterministic)
+//   k_lyap_reduce  slab sum, per-image g_u, scalars;  k_lyap_static_grads: dQx, dbx, dx
+#include "common.h"
+#include "tile.h"
+#include "../../include/fiode.h"
+
+namespace {
+using namespace fiode_tile;
+
+constexpr int SLAB = 16384 + 1280 + 1280 + 128 + 128 + 16;   // floats per wgrad partial slab
+constexpr int SLAB_Q2 = 0, SLAB_Q3 = 16384, SLAB_Q1 = 16384 + 1280, SLAB_B2 = 16384 + 2560,
+              SLAB_B1 = 16384 + 2560 + 128, SLAB_B3 = 16384 + 2560 + 256;
+
+struct LyapArgs {
+  int N, S, B, S1;
+  int sampler, dropout_mode, bit_mode;
+  uint32_t thr8;
+  float drop_scale;
+  Rng rng;
+  DynScalars d;
+  float kappa, invN;
+  int parts, chunk;
+  const float* x_feat;
+  const int64_t* y;
+  const float* h_in;
+  const uint8_t* masks;
+  const float *Q1, *b1, *Qx, *bx, *Q2, *b2, *Q3, *b3;
+  // workspace
+  uint32_t* conv;      // [2]
+  float* u;            // [B][M]
+  float* h_ws;         // [N][C]
+  float* ft_ws;        // [2][N][C]
+  float *a1, *a2, *gz2, *gz1;   // [N][M]
+  float* gft;          // [N][C]
+  uint4* kw;           // [4][N] dropout keep words (bit t of word mb = keep hidden 32mb+t)
+  float* tile_sc;      // [ntiles][4]
+  float* slabs;        // [B*parts][SLAB]
+  float* g_u;          // [B][M]
+  // outputs
+  float* scalars;
+  float *h_out, *V, *Vdot, *f, *f_log, *qp_lower, *qp_nominal, *g_ftilde;
+  fiode_lyap_grads grads;
+};
+
+// ---- sampler (one lane computes one row) ----------------------------------------------------
+__device__ __forceinline__ void draws10(const Rng& rng, uint32_t index, uint32_t stream, float (&e)[C]) {
+  const uint4 r0 = rng.draw(index, stream), r1 = rng.draw(index, stream + 1), r2 = rng.draw(index, stream + 2);
+  const uint32_t w[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
+#pragma unroll
+  for (int j = 0; j < C; ++j) e[j] = exp1_from_bits(w[j]);
+}
+
+__device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C]) {
+  if (a.sampler == FIODE_SAMPLER_GIVEN) {
+    load_row10(a.h_in + (size_t)row * C, h);
+    return;
+  }
+  const int b = row / a.S, s = row - b * a.S;
+  if (a.sampler == FIODE_SAMPLER_COMPOSITE) {
+    if (s < a.S1) {                      // UniformSimplexSampling, shared over the batch (sampler.py:209-210)
+      draws10(a.rng, (uint32_t)s, RNG_STREAM_UNIFORM, h);
+      l1_normalize(h);
+    } else {                             // CorrectConeSampling (sampler.py:113-128)
+      draws10(a.rng, (uint32_t)row, RNG_STREAM_CONE, h);
+      l1_normalize(h);
+      int am = 0;
+      float mx = h[0];
+#pragma unroll
+      for (int j = 1; j < C; ++j)
+        if (h[j] > mx) { mx = h[j]; am = j; }
+      float hl = 0.f;
+#pragma unroll
+      for (int j = 0; j < C; ++j) hl = (j == label) ? h[j] : hl;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const float o = h[j];
+        h[j] = (j == label) ? mx : ((j == am) ? hl : o);
+      }
+    }
+  } else {                               // DecisionBoundarySampling (sampler.py:139-153)
+    float z[C];
+    draws10(a.rng, (uint32_t)row, RNG_STREAM_DB, z);
+    float raw[C];
+    float zm = z[0];
+#pragma unroll
+    for (int j = 1; j < C - 1; ++j) zm = fmaxf(zm, z[j]);
+    raw[0] = zm;
+#pragma unroll
+    for (int j = 0; j < C - 1; ++j) raw[j + 1] = z[j];
+    l1_normalize(raw);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float below = raw[c + 1 < C ? c + 1 : C - 1];   // classes before the label keep raw[c+1]
+      const float above = raw[c];                          // classes after it take raw[c]
+      h[c] = (c == label) ? raw[0] : ((c < label) ? below : above);
+    }
+  }
+}
+
+// ---- dropout keep words: bit t of kw[mb] = keep hidden unit 32*mb + t --------------------------
+__device__ __forceinline__ void keep_words(const LyapArgs& a, int row, int set, uint32_t (&kw)[4]) {
+  if (a.dropout_mode == FIODE_DROPOUT_OFF) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) kw[mb] = 0xFFFFFFFFu;
+  } else if (a.dropout_mode == FIODE_DROPOUT_GIVEN) {
+    const uint8_t* m = a.masks + ((size_t)set * a.N + row) * M;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      uint32_t w = 0;
+      const uint4* q = reinterpret_cast<const uint4*>(m + 32 * mb);
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const uint4 t = q[v];
+        const uint32_t ww[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) ? 1u : 0u) << (16 * v + 4 * e + by);
+      }
+      kw[mb] = w;
+    }
+  } else if (a.bit_mode) {               // p = 0.5: one Philox bit per unit
+    const uint4 r = a.rng.draw((uint32_t)row, RNG_STREAM_DROP + ((uint32_t)set << 4));
+    kw[0] = r.x; kw[1] = r.y; kw[2] = r.z; kw[3] = r.w;
+  } else {                               // general p: keep iff random byte < round(256 (1-p))
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int call = 0; call < 2; ++call) {
+        const uint4 r = a.rng.draw((uint32_t)row, RNG_STREAM_DROP + ((uint32_t)set << 4) + 1 + 2 * mb + call);
+        const uint32_t ww[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) < a.thr8 ? 1u : 0u) << (16 * call + 4 * e + by);
+      }
+      kw[mb] = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
+  const int b = blockIdx.x, i = threadIdx.x;
+  if (b == 0 && i < 2) a.conv[i] = 0xFFFFFFFFu;
+  if (b >= a.B) return;
+  float s = 0.f;
+  const float* xb = a.x_feat + (size_t)b * FIODE_X;
+#pragma unroll
+  for (int c = 0; c < FIODE_X; ++c) s = __fmaf_rn(a.Qx[i * FIODE_X + c], xb[c], s);
+  a.u[(size_t)b * M + i] = (s + a.bx[i]) + a.b1[i];
+}
+
+// Per-row preparation: sampler fan-out (h -> h_ws) and the dropout keep words of the 4 mask sets.
+__global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= a.N) return;
+  if (a.sampler != FIODE_SAMPLER_GIVEN || a.h_out) {
+    const int label = (int)a.y[row / a.S];
+    float h[C];
+    sample_row(a, row, label, h);
+    if (a.sampler != FIODE_SAMPLER_GIVEN) store_row10(a.h_ws + (size_t)row * C, h);
+    if (a.h_out) store_row10(a.h_out + (size_t)row * C, h);
+  }
+  for (int set = 0; set < 4; ++set) {
+    uint32_t kw[4];
+    keep_words(a, row, set, kw);
+    a.kw[(size_t)set * a.N + row] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lyap_fwd(LyapArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Q2s = smem;
+  float* Q3s = smem + M * LDQ;
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
+  float q1[4][5];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
+  const int ntiles = (a.N + 31) / 32;
+  for (int tile = blockIdx.x * FIODE_WAVES + wave; tile < ntiles; tile += gridDim.x * FIODE_WAVES) {
+    const int row = tile * 32 + col;
+    const bool valid = row < a.N;
+    const int rr = valid ? row : a.N - 1;
+    const int b = rr / a.S;
+    float h[C];
+    load_row10(((a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws) + (size_t)rr * C, h);
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+      const uint4 k1 = a.kw[(size_t)(2 * pass) * a.N + rr], k2 = a.kw[(size_t)(2 * pass + 1) * a.N + rr];
+      const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w}, kw2[4] = {k2.x, k2.y, k2.z, k2.w};
+      f32x16 z1[4], z2[4];
+      const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
+                                 col, half, z1, z2);
+      if (pass == 0 && valid) {
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          store_acc_rows(a.a1 + (size_t)row * M, mb, half, z1[mb]);
+          store_acc_rows(a.a2 + (size_t)row * M, mb, half, z2[mb]);
+        }
+      }
+      float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
+      gather_ft(z3, half, ft);
+      barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+      uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
+      if (!valid) conv = 0xFFFFFFFFu;
+      conv = wave_and(conv);
+      if (lane == 0) atomicAnd(a.conv + pass, conv);
+      if (valid && half == 0) {
+        store_row10(a.ft_ws + ((size_t)pass * a.N + row) * C, ft);
+        if (a.qp_nominal) store_row10(a.qp_nominal + ((size_t)pass * a.N + row) * C, nominal);
+        if (pass == 0 && a.qp_lower) store_row10(a.qp_lower + (size_t)row * C, lower);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lyap_bwd(LyapArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Q2Ts = smem;      // Q2Ts[i][k] = Q2[k][i]
+  load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
+  float q3t[4][5];         // A operand of g_a2^T = Q3^T g_ft^T: Q3[2s+half][32mb+col]
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 5; ++s) q3t[mb][s] = a.Q3[(2 * s + half) * M + 32 * mb + col];
+  const int K0 = qp_exit_iter(a.conv[0], a.d.max_iter);
+  const int K1 = qp_exit_iter(a.conv[1], a.d.max_iter);
+  const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
+  const int ntiles = (a.N + 31) / 32;
+  for (int tile = blockIdx.x * FIODE_WAVES + wave; tile < ntiles; tile += gridDim.x * FIODE_WAVES) {
+    const int row = tile * 32 + col;
+    const bool valid = row < a.N;
+    const int rr = valid ? row : a.N - 1;
+    const int b = rr / a.S;
+    const int label = (int)a.y[b];
+    float h[C], ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
+    load_row10(hsrc + (size_t)rr * C, h);
+    // ---- loss pass: QP to the global exit K0
+    load_row10(a.ft_ws + (size_t)rr * C, ft);
+    barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+    qp_bisect(lower, nominal, K0, a.d.tol, v, mu);
+    // V = (1 + max_{j != y} h_j) - h_y ; j* first index (lya_cands.py:84-94)
+    int js = label == 0 ? 1 : 0;
+    float hm = h[js];
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      if (j != label && h[j] > hm) { hm = h[j]; js = j; }
+    float hy = 0.f, fy = 0.f, fj = 0.f;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      hy = (j == label) ? h[j] : hy;
+      fy = (j == label) ? v[j] : fy;
+      fj = (j == js) ? v[j] : fj;
+    }
+    const float Vv = (1.0f + hm) - hy;
+    const float Vd = fj - fy;                    // jvp of the piecewise-linear V along f
+    const float pre = Vd + a.kappa * Vv;         // vdot + kappa * V.detach() (pl_modules.py:455-457)
+    const float viol = pre > 0.f ? pre : 0.f;
+    const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
+    float g[C], g_nom[C], g_low[C], gft[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) g[j] = (j == js) ? gp : ((j == label) ? -gp : 0.f);
+    qp_backward_row(g, v, mu, nominal, g_nom, g_low);
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      gft[j] = a.d.scale_nominal ? ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j] : g_nom[j];
+    if (valid && half == 0) {
+      store_row10(a.gft + (size_t)row * C, gft);
+      if (a.V) a.V[row] = Vv;
+      if (a.Vdot) a.Vdot[row] = Vd;
+      if (a.f) store_row10(a.f + (size_t)row * C, v);
+      if (a.g_ftilde) store_row10(a.g_ftilde + (size_t)row * C, gft);
+    }
+    // ---- logging pass: QP to K1, active-constraint count (pl_modules.py:476-482)
+    float fl[C], nom1[C], mu1;
+    load_row10(a.ft_ws + ((size_t)a.N + rr) * C, ft);
+    barrier_nominal(a.d, h, ft, lower, nom1, sig, span);
+    qp_bisect(lower, nom1, K1, a.d.tol, fl, mu1);
+    float active = 0.f;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const float lin = -a.d.alpha_1 * h[j];
+      const float up = a.d.alpha_2 * (1.0f - h[j]);
+      active += (fabsf(fl[j] - lin) <= 1e-6f || fabsf(fl[j] - up) <= 1e-6f) ? 1.f : 0.f;
+    }
+    if (valid && half == 0 && a.f_log) store_row10(a.f_log + (size_t)row * C, fl);
+    {
+      const bool cnt = valid && half == 0;
+      const float s0 = wave_sum(cnt ? viol : 0.f);
+      const float s1 = wave_sum(cnt && viol > 0.f ? 1.f : 0.f);
+      const float s2 = wave_sum(cnt ? active : 0.f);
+      if (lane == 0) *reinterpret_cast<f32x4*>(a.tile_sc + 4 * tile) = f32x4{s0, s1, s2, 0.f};
+    }
+    // ---- g_a2^T = Q3^T g_ft^T ; g_z2 = g_a2 * [a2 > 0] * scale
+    f32x16 ga[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) ga[mb] = f16_zero();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const float bs = half ? gft[2 * s + 1] : gft[2 * s];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) ga[mb] = mfma32(q3t[mb][s], bs, ga[mb]);
+    }
+    const float* a2r = a.a2 + (size_t)rr * M;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      f32x16 act;
+      load_acc_rows(a2r, mb, half, act);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ga[mb][r] = act[r] > 0.f ? ga[mb][r] * a.drop_scale : 0.f;
+      if (valid) store_acc_rows(a.gz2 + (size_t)row * M, mb, half, ga[mb]);
+    }
+    // ---- g_a1^T = Q2^T g_z2^T ; g_z1 = g_a1 * [a1 > 0] * scale
+    f32x16 gb[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) gb[mb] = f16_zero();
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(Q2Ts + (32 * mb + col) * LDQ + 32 * kb + 8 * gg + 4 * half);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) gb[mb] = mfma32(q[t], ga[kb][4 * gg + t], gb[mb]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const float* a1r = a.a1 + (size_t)rr * M;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      f32x16 act;
+      load_acc_rows(a1r, mb, half, act);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb[mb][r] = act[r] > 0.f ? gb[mb][r] * a.drop_scale : 0.f;
+      if (valid) store_acc_rows(a.gz1 + (size_t)row * M, mb, half, gb[mb]);
+    }
+  }
+}
+
+// Weight gradients.  Workgroup (image b, part p) reduces rows [b*S + p*chunk, ...) of that image.
+// Wave w: dQ2[:, 32w:32w+32] (4 blocks), dQ3[:, 32w:32w+32], dQ1[32w:32w+32, :], db2/db1 slice w.
+__global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
+  const int b = blockIdx.x / a.parts, p = blockIdx.x - b * a.parts;
+  const int r0 = b * a.S + p * a.chunk;
+  const int r1 = min(r0 + a.chunk, (b + 1) * a.S);
+  const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
+  f32x16 acc2[4], acc3 = f16_zero(), acc1 = f16_zero();
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc2[mb] = f16_zero();
+  float db2 = 0.f, db1 = 0.f, db3 = 0.f;
+  for (int j = r0; j < r1; j += 2) {
+    const int jj = j + half;
+    const bool ok = jj < r1;
+    const int js = ok ? jj : r0;
+    float A2[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) A2[mb] = ok ? a.gz2[(size_t)js * M + 32 * mb + col] : 0.f;
+    const float B2 = a.a1[(size_t)js * M + 32 * w + col];
+    const float A3 = (ok && col < C) ? a.gft[(size_t)js * C + col] : 0.f;
+    const float B3 = a.a2[(size_t)js * M + 32 * w + col];
+    const float A1 = ok ? a.gz1[(size_t)js * M + 32 * w + col] : 0.f;
+    const float B1 = col < C ? hsrc[(size_t)js * C + col] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(A2[mb], B2, acc2[mb]);
+    acc3 = mfma32(A3, B3, acc3);
+    acc1 = mfma32(A1, B1, acc1);
+    db2 += (w == 0) ? A2[0] : (w == 1) ? A2[1] : (w == 2) ? A2[2] : A2[3];
+    db1 += A1;
+    db3 += A3;
+  }
+  float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) slab[SLAB_Q2 + (32 * mb + acc_row(r, half)) * M + 32 * w + col] = acc2[mb][r];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = acc_row(r, half);
+    if (i < C) slab[SLAB_Q3 + i * M + 32 * w + col] = acc3[r];
+    if (col < C) slab[SLAB_Q1 + (32 * w + i) * C + col] = acc1[r];
+  }
+  db2 += shfl_xor32(db2);
+  db1 += shfl_xor32(db1);
+  db3 += shfl_xor32(db3);
+  if (half == 0) {
+    slab[SLAB_B2 + 32 * w + col] = db2;
+    slab[SLAB_B1 + 32 * w + col] = db1;
+    if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
+  }
+}
+
+// Sum of the slabs (fixed order) -> dQ2, dQ3, dQ1, db2, db3; per-image g_u; scalars.
+__global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nwg = a.B * a.parts;
+  if (e < SLAB_B1) {
+    float s = 0.f;
+    for (int k = 0; k < nwg; ++k) s += a.slabs[(size_t)k * SLAB + e];
+    if (e < SLAB_Q3) a.grads.Q2[e] = s;
+    else if (e < SLAB_Q1) a.grads.Q3[e - SLAB_Q3] = s;
+    else if (e < SLAB_B2) a.grads.Q1[e - SLAB_Q1] = s;
+    else a.grads.b2[e - SLAB_B2] = s;
+  } else if (e >= SLAB_B3 && e < SLAB_B3 + C) {
+    float s = 0.f;
+    for (int k = 0; k < nwg; ++k) s += a.slabs[(size_t)k * SLAB + e];
+    a.grads.b3[e - SLAB_B3] = s;
+  } else if (e >= SLAB + 0 && e < SLAB + a.B * M) {       // g_u[b][i]
+    const int q = e - SLAB, b = q / M, i = q - b * M;
+    float s = 0.f;
+    for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
+    a.g_u[q] = s;
+  } else if (e == SLAB + a.B * M) {                      // scalars
+    const int ntiles = (a.N + 31) / 32;
+    double v = 0.0, ef = 0.0, ac = 0.0;
+    for (int t = 0; t < ntiles; ++t) {
+      v += a.tile_sc[4 * t];
+      ef += a.tile_sc[4 * t + 1];
+      ac += a.tile_sc[4 * t + 2];
+    }
+    a.scalars[0] = (float)(v / a.N);
+    a.scalars[1] = (float)ef;
+    a.scalars[2] = (float)(ac / ((double)a.N * C));
+    a.scalars[3] = (float)qp_exit_iter(a.conv[0], a.d.max_iter);
+    a.scalars[4] = (float)qp_exit_iter(a.conv[1], a.d.max_iter);
+    a.scalars[5] = (float)v;
+    a.scalars[6] = (float)ac;
+    a.scalars[7] = (float)a.N;
+  }
+}
+
+// dQx = g_u^T x ; dbx = db1 = sum_b g_u ; dx = g_u Qx   (expand backward, pl_modules.py:400)
+__global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < M * FIODE_X) {
+    const int i = e / FIODE_X, c = e - i * FIODE_X;
+    float s = 0.f;
+    for (int b = 0; b < a.B; ++b) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.x_feat[(size_t)b * FIODE_X + c], s);
+    a.grads.Qx[e] = s;
+  } else if (e < M * FIODE_X + M) {
+    const int i = e - M * FIODE_X;
+    float s = 0.f;
+    for (int b = 0; b < a.B; ++b) s += a.g_u[(size_t)b * M + i];
+    a.grads.bx[i] = s;
+    a.grads.b1[i] = s;
+  } else if (e < M * FIODE_X + M + a.B * FIODE_X) {
+    const int q = e - M * FIODE_X - M, b = q / FIODE_X, c = q - b * FIODE_X;
+    float s = 0.f;
+    for (int i = 0; i < M; ++i) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.Qx[i * FIODE_X + c], s);
+    a.grads.x_feat[q] = s;
+  }
+}
+
+// ---- workspace ----------------------------------------------------------------------------------
+struct WsLayout {
+  size_t conv, u, h, ft, a1, a2, gz2, gz1, gft, kw, tsc, slabs, gu, total;
+};
+inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+inline void parts_for(int B, int S, int& parts, int& chunk) {
+  parts = (256 + B - 1) / B;
+  const int maxp = S / 32 > 0 ? S / 32 : 1;
+  if (parts > maxp) parts = maxp;
+  if (parts < 1) parts = 1;
+  chunk = (S + parts - 1) / parts;
+  chunk = (chunk + 1) & ~1;
+}
+inline WsLayout ws_layout(int B, int S) {
+  const size_t N = (size_t)B * S;
+  int parts, chunk;
+  parts_for(B, S, parts, chunk);
+  WsLayout L;
+  size_t o = 0;
+  L.conv = o; o = al(o + 16);
+  L.u = o; o = al(o + (size_t)B * M * 4);
+  L.h = o; o = al(o + N * C * 4);
+  L.ft = o; o = al(o + 2 * N * C * 4);
+  L.a1 = o; o = al(o + N * M * 4);
+  L.a2 = o; o = al(o + N * M * 4);
+  L.gz2 = o; o = al(o + N * M * 4);
+  L.gz1 = o; o = al(o + N * M * 4);
+  L.gft = o; o = al(o + N * C * 4);
+  L.kw = o; o = al(o + 4 * N * 16);
+  L.tsc = o; o = al(o + ((N + 31) / 32) * 16);
+  L.slabs = o; o = al(o + (size_t)B * parts * SLAB * 4);
+  L.gu = o; o = al(o + (size_t)B * M * 4);
+  L.total = o;
+  return L;
+}
+
+int check_dyn(const fiode_dyn_config* d) {
+  if (!d) return FIODE_EINVAL;
+  if (d->n_hidden != C || d->mlp_size != M || d->x_dim != FIODE_X) return FIODE_ESHAPE;
+  if (d->qp_max_iter < 1 || d->qp_max_iter > 32) return FIODE_EINVAL;
+  if (!(d->dropout >= 0.f && d->dropout < 1.f)) return FIODE_EINVAL;
+  return FIODE_OK;
+}
+
+}  // namespace
+
+extern "C" size_t fiode_lyap_workspace_bytes(const fiode_lyap_config* cfg, const fiode_dyn_config* dyn) {
+  (void)dyn;
+  if (!cfg || cfg->batch <= 0 || cfg->sample_size <= 0) return 0;
+  return ws_layout(cfg->batch, cfg->sample_size).total;
+}
+
+extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const fiode_dyn_config* dyn,
+                               const fiode_dyn_weights* w, const fiode_lyap_io* io, fiode_lyap_grads* grads,
+                               void* workspace, size_t workspace_bytes) {
+  int rc = check_dyn(dyn);
+  if (rc) return rc;
+  if (!cfg || !w || !io || !grads || !workspace) return FIODE_EINVAL;
+  const int B = cfg->batch, S = cfg->sample_size;
+  if (B <= 0 || S <= 0 || (long long)B * S > (1LL << 30)) return FIODE_EINVAL;
+  if (cfg->n_uniform < 0 || cfg->n_uniform > S) return FIODE_EINVAL;
+  if (cfg->sampler < 0 || cfg->sampler > 2 || cfg->dropout_mode < 0 || cfg->dropout_mode > 2) return FIODE_EINVAL;
+  if (!io->x_feat || !io->y || !io->scalars) return FIODE_EINVAL;
+  if (cfg->sampler == FIODE_SAMPLER_GIVEN && !io->h) return FIODE_EINVAL;
+  if (cfg->dropout_mode == FIODE_DROPOUT_GIVEN && !io->masks) return FIODE_EINVAL;
+  if (!w->Q1 || !w->b1 || !w->Qx || !w->bx || !w->Q2 || !w->b2 || !w->Q3 || !w->b3) return FIODE_EINVAL;
+  if (!grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
+      !grads->b3 || !grads->x_feat)
+    return FIODE_EINVAL;
+  const WsLayout L = ws_layout(B, S);
+  if (workspace_bytes < L.total) return FIODE_EWORKSPACE;
+  char* ws = static_cast<char*>(workspace);
+
+  LyapArgs a{};
+  a.N = B * S; a.S = S; a.B = B; a.S1 = cfg->n_uniform;
+  a.sampler = cfg->sampler;
+  const float p = cfg->dropout_mode == FIODE_DROPOUT_OFF ? 0.f : dyn->dropout;
+  a.dropout_mode = (p == 0.f) ? FIODE_DROPOUT_OFF : cfg->dropout_mode;
+  a.bit_mode = (p == 0.5f);
+  a.thr8 = (uint32_t)lrintf((1.0f - p) * 256.0f);
+  a.drop_scale = (a.dropout_mode == FIODE_DROPOUT_OFF) ? 1.0f : 1.0f / (1.0f - p);
+  a.rng.key = make_uint2((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32));
+  a.rng.off_lo = (uint32_t)cfg->offset; a.rng.off_hi = (uint32_t)(cfg->offset >> 32);
+  a.d.alpha_1 = dyn->alpha_1; a.d.alpha_2 = dyn->alpha_2; a.d.sigma_1 = dyn->sigma_1;
+  a.d.tol = dyn->qp_tol; a.d.scale_nominal = dyn->scale_nominal; a.d.max_iter = dyn->qp_max_iter;
+  a.kappa = cfg->kappa;
+  a.invN = 1.0f / (float)a.N;
+  parts_for(B, S, a.parts, a.chunk);
+  a.x_feat = io->x_feat; a.y = io->y; a.h_in = io->h; a.masks = io->masks;
+  a.Q1 = w->Q1; a.b1 = w->b1; a.Qx = w->Qx; a.bx = w->bx; a.Q2 = w->Q2; a.b2 = w->b2; a.Q3 = w->Q3; a.b3 = w->b3;
+  a.conv = reinterpret_cast<uint32_t*>(ws + L.conv);
+  a.u = reinterpret_cast<float*>(ws + L.u);
+  a.h_ws = reinterpret_cast<float*>(ws + L.h);
+  a.ft_ws = reinterpret_cast<float*>(ws + L.ft);
+  a.a1 = reinterpret_cast<float*>(ws + L.a1);
+  a.a2 = reinterpret_cast<float*>(ws + L.a2);
+  a.gz2 = reinterpret_cast<float*>(ws + L.gz2);
+  a.gz1 = reinterpret_cast<float*>(ws + L.gz1);
+  a.gft = reinterpret_cast<float*>(ws + L.gft);
+  a.kw = reinterpret_cast<uint4*>(ws + L.kw);
+  a.tile_sc = reinterpret_cast<float*>(ws + L.tsc);
+  a.slabs = reinterpret_cast<float*>(ws + L.slabs);
+  a.g_u = reinterpret_cast<float*>(ws + L.gu);
+  a.scalars = io->scalars;
+  a.h_out = io->h_out; a.V = io->V; a.Vdot = io->Vdot; a.f = io->f; a.f_log = io->f_log;
+  a.qp_lower = io->qp_lower; a.qp_nominal = io->qp_nominal; a.g_ftilde = io->g_ftilde;
+  a.grads = *grads;
+
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int ntiles = (a.N + 31) / 32;
+  const int fwd_blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
+  const size_t lds_fwd = (size_t)(M + 32) * LDQ * sizeof(float);
+  const size_t lds_bwd = (size_t)M * LDQ * sizeof(float);
+  hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_lyap_prep, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_lyap_fwd, dim3(fwd_blocks), dim3(256), lds_fwd, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_lyap_bwd, dim3(fwd_blocks), dim3(256), lds_bwd, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_lyap_wgrad, dim3(B * a.parts), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  const int red_items = SLAB + B * M + 1;
+  hipLaunchKernelGGL(k_lyap_reduce, dim3((red_items + 255) / 256), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  const int sg_items = M * FIODE_X + M + B * FIODE_X;
+  hipLaunchKernelGGL(k_lyap_static_grads, dim3((sg_items + 255) / 256), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}

@@ -1,0 +1,110 @@
+"""ctypes binding of libfiode.so (include/fiode.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load, importing
+anything that needs it raises ``FiodeLibraryError`` immediately.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = pathlib.Path(os.environ.get("FIODE_LIB", _HERE / "libfiode.so"))
+
+FIODE_SAMPLER_GIVEN, FIODE_SAMPLER_COMPOSITE, FIODE_SAMPLER_DECISION_BOUNDARY = 0, 1, 2
+FIODE_DROPOUT_OFF, FIODE_DROPOUT_GIVEN, FIODE_DROPOUT_PHILOX = 0, 1, 2
+
+class FiodeLibraryError(RuntimeError):
+    pass
+
+
+class FiodeError(RuntimeError):
+    pass
+
+
+_fp = ct.POINTER(ct.c_float)
+_vp = ct.c_void_p
+
+
+class DynWeights(ct.Structure):
+    _fields_ = [(n, ct.c_void_p) for n in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+
+
+class DynConfig(ct.Structure):
+    _fields_ = [("n_hidden", ct.c_int32), ("mlp_size", ct.c_int32), ("x_dim", ct.c_int32),
+                ("alpha_1", ct.c_float), ("alpha_2", ct.c_float), ("sigma_1", ct.c_float),
+                ("scale_nominal", ct.c_int32), ("dropout", ct.c_float), ("qp_max_iter", ct.c_int32),
+                ("qp_tol", ct.c_float)]
+
+
+class LyapConfig(ct.Structure):
+    _fields_ = [("batch", ct.c_int32), ("sample_size", ct.c_int32), ("n_uniform", ct.c_int32),
+                ("sampler", ct.c_int32), ("dropout_mode", ct.c_int32), ("kappa", ct.c_float),
+                ("seed", ct.c_uint64), ("offset", ct.c_uint64)]
+
+
+class LyapIO(ct.Structure):
+    _fields_ = [(n, ct.c_void_p) for n in ("x_feat", "y", "h", "masks", "scalars", "h_out", "V", "Vdot",
+                                           "f", "f_log", "qp_lower", "qp_nominal", "g_ftilde")]
+
+
+class LyapGrads(ct.Structure):
+    _fields_ = [(n, ct.c_void_p) for n in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3", "x_feat")]
+
+
+class OdeConfig(ct.Structure):
+    _fields_ = [("method", ct.c_int32), ("batch", ct.c_int32), ("t0", ct.c_double), ("t1", ct.c_double),
+                ("rtol", ct.c_double), ("atol", ct.c_double), ("step_size", ct.c_double),
+                ("max_steps", ct.c_int32)]
+
+
+class CertifyConfig(ct.Structure):
+    _fields_ = [("n_points", ct.c_int64), ("label", ct.c_int32), ("T", ct.c_int32), ("eps_grid", ct.c_float),
+                ("dist", ct.c_float), ("kappa", ct.c_float), ("lips_alpha_1", ct.c_float),
+                ("lips_sigma_1", ct.c_float), ("enumerate_grid", ct.c_int32)]
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise FiodeLibraryError(
+            f"libfiode.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        lib = ct.CDLL(str(LIB_PATH))
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise FiodeLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+    sig = {
+        "fiode_lyap_workspace_bytes": (ct.c_size_t, [ct.POINTER(LyapConfig), ct.POINTER(DynConfig)]),
+        "fiode_lyap_step": (ct.c_int, [_vp, ct.POINTER(LyapConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
+                                       ct.POINTER(LyapIO), ct.POINTER(LyapGrads), _vp, ct.c_size_t]),
+        "fiode_qp_forward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, ct.c_int32, ct.c_float, _vp, _vp,
+                                        _vp, _vp, ct.c_size_t]),
+        "fiode_qp_backward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "fiode_dyn_eval_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
+        "fiode_dyn_eval": (ct.c_int, [_vp, ct.POINTER(DynConfig), ct.POINTER(DynWeights), ct.c_int32, ct.c_int32,
+                                      _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_error_string": (ct.c_char_p, [ct.c_int]),
+        "fiode_abi_version": (ct.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _load()
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().fiode_error_string(rc)
+        raise FiodeError(f"{what} failed: {msg.decode() if msg else rc} (code {rc})")

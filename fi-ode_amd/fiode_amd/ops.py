@@ -1,0 +1,187 @@
+"""Tensor-level wrappers over the C-ABI (device tensors in, device tensors out).
+
+Every wrapper checks shapes/dtypes/devices on the host before launching (a wrong shape must
+never reach a kernel), runs on the caller's current HIP stream, and caches workspaces per
+(device, size).  No CPU fallback exists: the tensors must live on a ROCm device.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib as L
+
+C, M, X = 10, 128, 10
+WEIGHT_KEYS = ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+WEIGHT_SHAPES = {"Q1": (M, C), "b1": (M,), "Qx": (M, X), "bx": (M,), "Q2": (M, M), "b2": (M,),
+                 "Q3": (C, M), "b3": (C,)}
+
+
+@dataclass
+class DynCfg:
+    """Mirror of fiode_dyn_config (the dynamics constructor fields the hot path reads)."""
+    alpha_1: float = 100.0
+    alpha_2: float = 20.0
+    sigma_1: float = 0.02
+    scale_nominal: bool = True
+    dropout: float = 0.5
+    qp_max_iter: int = 30
+    qp_tol: float = 1e-4
+
+    def to_c(self) -> L.DynConfig:
+        return L.DynConfig(C, M, X, float(self.alpha_1), float(self.alpha_2), float(self.sigma_1),
+                           int(bool(self.scale_nominal)), float(self.dropout), int(self.qp_max_iter),
+                           float(self.qp_tol))
+
+
+def _stream(dev: torch.device) -> ct.c_void_p:
+    return ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: torch.Tensor, name: str, shape, dtype, dev) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device != dev or t.device.type != "cuda":
+        raise ValueError(f"{name}: must be on {dev} (ROCm device); got {t.device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return t.contiguous()
+
+
+class _Workspace:
+    _cache: Dict[tuple, torch.Tensor] = {}
+
+    @classmethod
+    def get(cls, dev: torch.device, nbytes: int, tag: str) -> torch.Tensor:
+        key = (dev.index, tag)
+        buf = cls._cache.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            cls._cache[key] = buf
+        return buf
+
+
+def _weights_c(w: Dict[str, torch.Tensor], dev) -> tuple:
+    ws = {k: _need(w[k], k, WEIGHT_SHAPES[k], torch.float32, dev) for k in WEIGHT_KEYS}
+    return ws, L.DynWeights(*[ws[k].data_ptr() for k in WEIGHT_KEYS])
+
+
+def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg, *,
+              sample_size: int, n_uniform: int, sampler: int = L.FIODE_SAMPLER_COMPOSITE,
+              dropout_mode: int = L.FIODE_DROPOUT_PHILOX, kappa: float = 2.0, seed: int = 0, offset: int = 0,
+              h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None, debug: bool = False,
+              out: Optional[dict] = None):
+    """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict)."""
+    dev = x_feat.device
+    B = x_feat.shape[0]
+    S = int(sample_size)
+    N = B * S
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    y = _need(y, "y", (B,), torch.int64, dev)
+    if not (0 <= n_uniform <= S):
+        raise ValueError("n_uniform must be in [0, sample_size]")
+    if sampler == L.FIODE_SAMPLER_GIVEN:
+        if h is None:
+            raise ValueError("sampler GIVEN needs h")
+        h = _need(h, "h", (N, C), torch.float32, dev)
+    if dropout_mode == L.FIODE_DROPOUT_GIVEN:
+        if masks is None:
+            raise ValueError("dropout GIVEN needs masks")
+        masks = _need(masks, "masks", (4, N, M), torch.uint8, dev)
+    ws_w, cw = _weights_c(weights, dev)
+    if out is None:
+        out = {}
+    grads = out.get("grads")
+    if grads is None:
+        grads = {k: torch.empty(WEIGHT_SHAPES[k], dtype=torch.float32, device=dev) for k in WEIGHT_KEYS}
+        grads["x_feat"] = torch.empty((B, X), dtype=torch.float32, device=dev)
+        out["grads"] = grads
+    scalars = out.get("scalars")
+    if scalars is None:
+        scalars = torch.empty(8, dtype=torch.float32, device=dev)
+        out["scalars"] = scalars
+    dbg = {}
+    if debug:
+        dbg = dict(h=torch.empty((N, C), device=dev), V=torch.empty(N, device=dev), Vdot=torch.empty(N, device=dev),
+                   f=torch.empty((N, C), device=dev), f_log=torch.empty((N, C), device=dev),
+                   qp_lower=torch.empty((N, C), device=dev), qp_nominal=torch.empty((2, N, C), device=dev),
+                   g_ftilde=torch.empty((N, C), device=dev))
+    cfg = L.LyapConfig(B, S, int(n_uniform), int(sampler), int(dropout_mode), float(kappa),
+                       int(seed) & (2**64 - 1), int(offset) & (2**64 - 1))
+    dc = dyn.to_c()
+    io = L.LyapIO(x_feat.data_ptr(), y.data_ptr(), _ptr(h), _ptr(masks), scalars.data_ptr(),
+                  _ptr(dbg.get("h")), _ptr(dbg.get("V")), _ptr(dbg.get("Vdot")), _ptr(dbg.get("f")),
+                  _ptr(dbg.get("f_log")), _ptr(dbg.get("qp_lower")), _ptr(dbg.get("qp_nominal")),
+                  _ptr(dbg.get("g_ftilde")))
+    cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
+    lib = L.lib()
+    nbytes = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dc))
+    ws = _Workspace.get(dev, nbytes, "lyap")
+    rc = lib.fiode_lyap_step(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), ct.byref(io), ct.byref(cg),
+                             ct.c_void_p(ws.data_ptr()), ct.c_size_t(ws.numel()))
+    L.check(rc, "fiode_lyap_step")
+    del ws_w
+    return scalars, grads, dbg
+
+
+def qp_forward(lower: torch.Tensor, nominal: torch.Tensor, max_iter: int = 30, tol: float = 1e-4):
+    """FastBarrierProjectionNoUpper forward (batch-global exit).  Returns (v, mu[N], exit_iter[1])."""
+    dev = nominal.device
+    n = nominal.shape[0]
+    lower = _need(lower, "lower", (n, C), torch.float32, dev)
+    nominal = _need(nominal, "nominal", (n, C), torch.float32, dev)
+    v = torch.empty_like(nominal)
+    mu = torch.empty(n, dtype=torch.float32, device=dev)
+    it = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = _Workspace.get(dev, 256, "qp")
+    rc = L.lib().fiode_qp_forward(_stream(dev), n, C, lower.data_ptr(), nominal.data_ptr(), int(max_iter),
+                                  float(tol), v.data_ptr(), mu.data_ptr(), it.data_ptr(), ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_qp_forward")
+    return v, mu, it
+
+
+def qp_backward(g, v, mu, lower, nominal):
+    dev = v.device
+    n = v.shape[0]
+    g = _need(g, "g", (n, C), torch.float32, dev)
+    v = _need(v, "v", (n, C), torch.float32, dev)
+    mu = _need(mu.reshape(-1), "mu", (n,), torch.float32, dev)
+    nominal = _need(nominal, "nominal", (n, C), torch.float32, dev)
+    lower = _need(lower, "lower", (n, C), torch.float32, dev)
+    gl = torch.empty_like(v)
+    gn = torch.empty_like(v)
+    rc = L.lib().fiode_qp_backward(_stream(dev), n, C, g.data_ptr(), v.data_ptr(), mu.data_ptr(), lower.data_ptr(),
+                                   nominal.data_ptr(), gl.data_ptr(), gn.data_ptr())
+    L.check(rc, "fiode_qp_backward")
+    return gl, gn
+
+
+def dyn_eval(h: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
+             rows_per_image: int = 1):
+    """eval_dot in eval mode: f[N][C] for h[N][C]; row r uses x_feat[r // rows_per_image]."""
+    dev = h.device
+    n = h.shape[0]
+    B = x_feat.shape[0]
+    if B * rows_per_image != n:
+        raise ValueError("h rows must equal batch * rows_per_image")
+    h = _need(h, "h", (n, C), torch.float32, dev)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    ws_w, cw = _weights_c(weights, dev)
+    f = torch.empty_like(h)
+    it = torch.zeros(1, dtype=torch.int32, device=dev)
+    lib = L.lib()
+    ws = _Workspace.get(dev, lib.fiode_dyn_eval_workspace_bytes(n), "dyn")
+    dc = dyn.to_c()
+    rc = lib.fiode_dyn_eval(_stream(dev), ct.byref(dc), ct.byref(cw), B, int(rows_per_image), x_feat.data_ptr(),
+                            h.data_ptr(), f.data_ptr(), it.data_ptr(), ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_dyn_eval")
+    return f, it

@@ -1,0 +1,141 @@
+/*
+ * fiode.h -- C-ABI of the MI355X (gfx950) FI-ODE hot path (libfiode.so).
+ *
+ * The reference (yjhuangcd/FI-ODE) has no FFI: its seams are hydra `_target_` classes and
+ * duck-typed nn.Module / autograd.Function objects.  Each entry point
+ * below replaces one of those seams; the Python host mirror (fi-ode_amd/fiode_amd) binds them
+ * with ctypes (INTEGRATION.md shows the binding a maintainer would add to the reference).
+ *
+ * Conventions
+ *   - every pointer is a device pointer to caller-owned memory (PyTorch caching allocator),
+ *     fp32 row-major, nn.Linear layout [out][in]; the library never allocates or frees;
+ *   - work is stream-ordered on `stream` (a hipStream_t passed as void*), with no host syncs;
+ *   - entry points return 0 on success, a FIODE_E* code otherwise; they never throw.
+ *   - shapes: C (classes = n_hidden = ODE state) = 10, M (mlp_size) = 128, X (x_dim) = 10.
+ */
+#ifndef FIODE_H_
+#define FIODE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FIODE_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define FIODE_API __attribute__((visibility("default")))
+#else
+#define FIODE_API
+#endif
+
+enum {
+  FIODE_OK = 0,
+  FIODE_EINVAL = 1,       /* bad argument / NULL where required                   */
+  FIODE_ESHAPE = 2,       /* C, M or X not supported by this build                */
+  FIODE_EWORKSPACE = 3,   /* workspace smaller than fiode_*_workspace_bytes()     */
+  FIODE_EHIP = 100        /* a HIP runtime error; FIODE_EHIP + hipError_t         */
+};
+
+enum { FIODE_SAMPLER_GIVEN = 0, FIODE_SAMPLER_COMPOSITE = 1, FIODE_SAMPLER_DECISION_BOUNDARY = 2 };
+enum { FIODE_DROPOUT_OFF = 0, FIODE_DROPOUT_GIVEN = 1, FIODE_DROPOUT_PHILOX = 2 };
+
+/* Effective (post-Cayley) dynamics weights of OrthoClassDynProjectSimplexLips
+ * (dynamics/classification.py:68-75): hidden_to_mlp, U_x, mlp_to_mlp, mlp_to_hidden. */
+typedef struct fiode_dyn_weights {
+  const float* Q1; const float* b1; /* hidden_to_mlp  [M][C], [M] */
+  const float* Qx; const float* bx; /* U_x            [M][X], [M] */
+  const float* Q2; const float* b2; /* mlp_to_mlp     [M][M], [M] */
+  const float* Q3; const float* b3; /* mlp_to_hidden  [C][M], [C] */
+} fiode_dyn_weights;
+
+/* Constructor fields of OrthoClassDynProjectSimplexLips read by the hot path
+ * (classification.py:32-66) and of its FastBarrierProjectionNoUpper (classification.py:63). */
+typedef struct fiode_dyn_config {
+  int32_t n_hidden;      /* C, must be 10   */
+  int32_t mlp_size;      /* M, must be 128  */
+  int32_t x_dim;         /* X, must be 10   */
+  float alpha_1, alpha_2, sigma_1;
+  int32_t scale_nominal; /* sigmoid rescale of the nominal velocity (classification.py:110-112) */
+  float dropout;         /* p of nn.Dropout (classification.py:49)                             */
+  int32_t qp_max_iter;   /* 1..32 (reference: 30)                                              */
+  float qp_tol;          /* reference: 1e-4                                                    */
+} fiode_dyn_config;
+
+/* One LyapunovLearning.compute_loss (pl_modules.py:390-502): B images x S samples. */
+typedef struct fiode_lyap_config {
+  int32_t batch;         /* B                                                                  */
+  int32_t sample_size;   /* S (h_sample_size); rows N = B*S, row = b*S + s                     */
+  int32_t n_uniform;     /* S1: UniformSimplex rows per image (first S1); S-S1 CorrectCone     */
+  int32_t sampler;       /* FIODE_SAMPLER_*                                                    */
+  int32_t dropout_mode;  /* FIODE_DROPOUT_*                                                    */
+  float kappa;           /* current_kappa (pl_modules.py:447-451)                              */
+  uint64_t seed;         /* Philox key (sampler + dropout)                                     */
+  uint64_t offset;       /* Philox counter offset (advance per step)                           */
+} fiode_lyap_config;
+
+typedef struct fiode_lyap_io {
+  const float* x_feat;   /* [B][X] static features = param_map(x) (init_coordinates.py:35)     */
+  const int64_t* y;      /* [B] labels                                                         */
+  const float* h;        /* [N][C] samples when sampler == GIVEN                               */
+  const uint8_t* masks;  /* [4][N][M] keep masks (loss L1, loss L2, log L1, log L2), GIVEN mode */
+  float* scalars;        /* [8] out: loss, eff_count, mean_active, qp_exit_loss, qp_exit_log,
+                            viol_sum, active_count, rows                                       */
+  /* optional per-row outputs (NULL = not written) */
+  float* h_out;          /* [N][C] samples used                                                */
+  float* V;              /* [N] DecisionBoundary V                                             */
+  float* Vdot;           /* [N] jvp V-dot                                                      */
+  float* f;              /* [N][C] loss-pass eval_dot                                          */
+  float* f_log;          /* [N][C] logging-pass eval_dot                                       */
+  float* qp_lower;       /* [N][C] QP lower bound                                              */
+  float* qp_nominal;     /* [2][N][C] QP nominal (loss pass, logging pass)                     */
+  float* g_ftilde;       /* [N][C] d loss / d mlp_to_hidden output                             */
+} fiode_lyap_io;
+
+typedef struct fiode_lyap_grads {  /* outputs, overwritten: d loss / d (effective weights) */
+  float *Q1, *b1, *Qx, *bx, *Q2, *b2, *Q3, *b3;
+  float* x_feat;                   /* [B][X] gradient into the backbone */
+} fiode_lyap_grads;
+
+/* Workspace bytes for fiode_lyap_step (depends on B, S only). */
+FIODE_API size_t fiode_lyap_workspace_bytes(const fiode_lyap_config* cfg, const fiode_dyn_config* dyn);
+
+/* The fused forward-invariance training step: sampler fan-out, two eval_dot passes (loss pass
+ * with dropout masks 0/1, logging pass with masks 2/3), DecisionBoundary V / V-dot, hinge loss,
+ * logging statistics and the gradient of mean(relu(Vdot + kappa V)) w.r.t. the effective
+ * weights and the static features.  Replaces LyapunovLearning.compute_loss + loss.backward()
+ * below the Cayley maps (pl_modules.py:394-484; classification.py:96-115;
+ * barrier_projection.py:217-313; lya_cands.py:79-94; sampler.py:195-216). */
+FIODE_API int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const fiode_dyn_config* dyn,
+                    const fiode_dyn_weights* w, const fiode_lyap_io* io, fiode_lyap_grads* grads,
+                    void* workspace, size_t workspace_bytes);
+
+/* FastBarrierProjectionNoUpper forward (barrier_projection.py:220-269) with the reference's
+ * batch-global exit.  exit_iter: device int32[1] (0-based exit iteration).  workspace: >= 16 B. */
+FIODE_API int fiode_qp_forward(void* stream, int32_t n, int32_t c, const float* lower, const float* nominal,
+                     int32_t max_iter, float tol, float* v, float* mu, int32_t* exit_iter,
+                     void* workspace, size_t workspace_bytes);
+
+/* FastBarrierProjectionNoUpper backward (barrier_projection.py:271-311), O(C) per row. */
+FIODE_API int fiode_qp_backward(void* stream, int32_t n, int32_t c, const float* g, const float* v,
+                      const float* mu, const float* lower, const float* nominal, float* g_lower,
+                      float* g_nominal);
+
+/* eval_dot / eval_dot_light / ode_forward in eval mode (no dropout; classification.py:104-132):
+ * f[N][C] for h[N][C], rows grouped S per image of x_feat[B][X] (N = B*S).  The QP exit is
+ * global over the N rows of the call.  workspace: fiode_dyn_eval_workspace_bytes(). */
+FIODE_API size_t fiode_dyn_eval_workspace_bytes(int32_t n);
+FIODE_API int fiode_dyn_eval(void* stream, const fiode_dyn_config* dyn, const fiode_dyn_weights* w,
+                   int32_t batch, int32_t rows_per_image, const float* x_feat, const float* h,
+                   float* f, int32_t* exit_iter, void* workspace, size_t workspace_bytes);
+
+/* Error text for a return code. */
+FIODE_API const char* fiode_error_string(int code);
+FIODE_API int fiode_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FIODE_H_ */

@@ -5,8 +5,9 @@ import pathlib
 import pytest
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-if str(ROOT) not in sys.path:
-    sys.path.insert(0, str(ROOT))
+for p in (ROOT, ROOT / "fi-ode_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
 
 
 def pytest_configure(config):

@@ -1,0 +1,52 @@
+"""CPU checks of the C-ABI boundary: libfiode.so loads and exports every symbol include/fiode.h
+declares, with host-only entry points callable (no GPU needed)."""
+import ctypes as ct
+import pathlib
+import re
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "fiode.h").read_text()
+    return re.findall(r"FIODE_API\s+[\w\s\*]+?\b(fiode_\w+)\s*\(", text)
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    for s in ("fiode_lyap_step", "fiode_lyap_workspace_bytes", "fiode_qp_forward", "fiode_qp_backward",
+              "fiode_dyn_eval", "fiode_error_string", "fiode_abi_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from fiode_amd import _lib
+    lib = ct.CDLL(str(_lib.LIB_PATH))
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_host_only_entry_points():
+    from fiode_amd import _lib
+    lib = _lib.lib()
+    assert lib.fiode_abi_version() == 1
+    assert lib.fiode_error_string(2).decode().startswith("unsupported shape")
+    cfg = _lib.LyapConfig(128, 256, 204, 1, 2, 2.0, 0, 0)
+    dyn = _lib.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 30, 1e-4)
+    nb = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dyn))
+    assert nb > 4 * 128 * 256 * 128 * 4      # a1, a2, gz2, gz1 at least
+
+
+def test_bad_shapes_rejected_before_launch():
+    """Shape/argument errors are refused on the host (no kernel is launched)."""
+    from fiode_amd import _lib
+    lib = _lib.lib()
+    dyn_bad = _lib.DynConfig(12, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 30, 1e-4)
+    cfg = _lib.LyapConfig(4, 8, 8, 0, 0, 2.0, 0, 0)
+    rc = lib.fiode_lyap_step(None, ct.byref(cfg), ct.byref(dyn_bad), None, None, None, None, 0)
+    assert rc == 2
+    assert lib.fiode_qp_forward(None, 5, 11, None, None, 30, 1e-4, None, None, None, None, 0) == 2
+    dyn = _lib.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 40, 1e-4)     # qp_max_iter > 32
+    assert lib.fiode_lyap_step(None, ct.byref(cfg), ct.byref(dyn), None, None, None, None, 0) == 1
