@@ -1,0 +1,227 @@
+"""Benchmark: CIFAR-10 forward-invariance (Lyapunov) train step, images/sec, on 1..N MI355X.
+
+python bench.py --gpus N --steps K --warmup W           (N>1: launched by torch.distributed.run)
+
+One step (per rank, B=128 images, h_sample_size S=256 at epoch 20: S1=204 Uniform + S2=52
+CorrectCone rows per image, N=32,768 rows) = the reference's training_step + backward + Adam:
+  backbone KWLarge-Cayley (PyTorch-ROCm)  ->  Cayley maps of the 4 dynamics layers  ->
+  fused HIP fan-out step (libfiode.so: sampler, 2 eval_dot passes incl. the bisection QP with the
+  batch-global exit, V / V-dot, hinge loss, logging statistics, all dynamics gradients)  ->
+  autograd through Cayley + backbone  ->  [RCCL all-reduce of the flat gradient + the fused
+  metric scalars]  ->  Adam.
+Inputs are synthetic (x ~ U[0,1), y ~ randint(10), seeded), resident in HBM before timing.
+
+Besides the JSON fields of the contract, the line carries:
+  roofline      the dominant fused kernel's algorithmic FLOP / its mean duration (HIP events
+                recorded by libfiode on the kernels' stream) vs the f32 MFMA peak
+  cpu_baseline  the op-for-op torch-CPU restatement of the reference fan-out (oracle/torch_ref.py)
+                on a bounded sample, rank 0 at N=1 only
+  hot_path      images/sec of the fused kernels alone (no backbone / optimizer)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+for _p in (ROOT, ROOT / "fi-ode_amd"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "CIFAR-10 train-step images/sec (B=128, h_sample=256) at 1/2/4/8 MI355X"
+B_PER_RANK = 128
+H_SAMPLE = 256
+EPOCH = 20
+MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
+HBM_PEAK_GBS = 8000.0
+# algorithmic FLOP per (image, sample) row
+FLOP_ROW_FWD_PASS = 2 * (10 * 128 + 128 * 128 + 128 * 10)          # 37,888 per eval_dot pass
+FLOP_ROW = {"k_lyap_fwd": 2 * FLOP_ROW_FWD_PASS,                   # loss pass + logging pass
+            "k_lyap_bwd": 2 * (128 * 128 + 128 * 10),              # input grads dL/da2 -> dL/da1
+            "k_lyap_wgrad": FLOP_ROW_FWD_PASS}                     # weight grads dQ3, dQ2, dQ1
+
+
+def build_module(dev, seed=0):
+    from fiode_amd.dynamics import OrthoClassDynProjectSimplexLips
+    from fiode_amd.lyapunov import LyapunovLearning, UniformInitFun, DecisionBoundary
+    from fiode_amd.models import make_ortho_KWLarge_Concat
+    from fiode_amd.sampling import (CompositeSampler, CompositeSamplerScheduler, CorrectConeSampling,
+                                    LinearScheduler, UniformSimplexSampling)
+    torch.manual_seed(seed)
+    # README.md:27 over configs/classification/cifar_train.yaml
+    dyn = OrthoClassDynProjectSimplexLips(n_hidden=10, activation="ReLU", dropout=0.5, mlp_size=128, kappa=2.0,
+                                          kappa_length=0, alpha_1=100.0, alpha_2=20.0, sigma_1=0.02,
+                                          scale_nominal=True, x_dim=10, cayley=True)
+    backbone = make_ortho_KWLarge_Concat(out_dim=10, act="GroupSort")
+    sampler = CompositeSampler((10,), [UniformSimplexSampling(), CorrectConeSampling()])
+    sched = CompositeSamplerScheduler([LinearScheduler(-0.02, 1.0, "min", 0.02, 10),
+                                       LinearScheduler(0.02, 0.0, "max", 0.98, 10)], [1.0, 1.0])
+    mod = LyapunovLearning(order=1, h_sample_size=H_SAMPLE, h_dist_lim=15.0, sampler=sampler,
+                           sampler_scheduler=sched, dynamics=dyn, init_fun=UniformInitFun((10,), backbone),
+                           lya_cand=DecisionBoundary(on_simplex=True), t_max=1.0, opt_name="Adam", lr=5e-3,
+                           weight_decay=0.0, warmup=-1, max_epochs=300, simplex=True, act="relu", val_adv=False,
+                           seed=seed)
+    mod.current_epoch = EPOCH
+    mod.dyn_fun.scale_nominal = False      # switched off at epoch_off_scale=10 (pl_modules.py:392-393)
+    return mod.to(dev).train()
+
+
+def cpu_baseline(budget_s: float = 10.0, images: int = 16):
+    """The reference fan-out path restated op-for-op in torch (oracle/torch_ref.py) on host cores."""
+    import numpy as np
+    from oracle import torch_ref as T
+    from tests._util import make_params, make_step_inputs
+    threads = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    P = make_params(0)
+    inp = make_step_inputs(B=images, S=H_SAMPLE, S1=204, seed=1)
+    W = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))) for k in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")}
+    tm = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    args = (tm(inp.h), tm(inp.x_feat), torch.from_numpy(inp.y), H_SAMPLE, W)
+    kw = dict(scale_nominal=False, kappa=2.0, mask1=tm(inp.mask1), mask2=tm(inp.mask2), lmask1=tm(inp.lmask1),
+              lmask2=tm(inp.lmask2))
+    T.step_with_grads(*args, **kw)
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or time.perf_counter() - t0 < budget_s:
+        T.step_with_grads(*args, **kw)
+        n += 1
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(images / dt, 2), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps of B={images} x S={H_SAMPLE} rows (S1=204/S2=52) of the fan-out path "
+                      f"(jvp(DecisionBoundary, eval_dot) + QP + hinge + logging pass + backward) in "
+                      f"oracle/torch_ref.py, float32, {dt * 1e3:.1f} ms/step; backbone and optimizer excluded"}
+
+
+def load_pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary (if present)."""
+    p = ROOT / "profiles" / "pmc_summary.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--prof-reps", type=int, default=20)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    mod = build_module(dev, seed=0)
+    mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
+    opt = mod.configure_optimizers()[0][0]
+    params = [p for p in mod.parameters() if p.requires_grad]
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
+    metrics = torch.zeros(4, device=dev)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)                 # one RCCL all-reduce of the whole gradient
+            flat /= world
+            o = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p))
+                o += n
+            sc = mod.last_plan["scalars"]
+            metrics[0] = sc[0]; metrics[1] = sc[1]; metrics[2] = sc[2]; metrics[3] = 1.0
+            dist.all_reduce(metrics)              # fused sync_dist of the logged scalars
+        opt.step()
+        mod.global_step += 1
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    elapsed = float(dt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B_PER_RANK * args.steps / elapsed
+
+    # ---- per-kernel timing of the fused hot path with HIP events (same inputs as a step) ----
+    from fiode_amd import _lib as L, ops
+    with torch.no_grad():
+        feat = mod.init_coordinates.param_map(x).float().contiguous()
+        w = {k: v.detach().float().contiguous() for k, v in mod.dyn_fun.effective_weights().items()}
+    plan = mod.step_plan(y)
+    nk = len(L.LYAP_KERNELS)
+    tot = [0.0] * nk
+    for r in range(args.prof_reps + 2):
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(nk + 1)]
+        ops.lyap_step(feat, y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"], sampler=plan["sampler"],
+                      dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"], offset=r, events=evs)
+        torch.cuda.synchronize()
+        if r >= 2:
+            for i in range(nk):
+                tot[i] += evs[i].elapsed_time(evs[i + 1])
+    kern_ms = {L.LYAP_KERNELS[i]: tot[i] / args.prof_reps for i in range(nk)}
+    hot_ms = sum(kern_ms.values())
+    rows = B_PER_RANK * H_SAMPLE
+    dom = max(FLOP_ROW, key=lambda k: kern_ms[k])
+    ach = FLOP_ROW[dom] * rows / (kern_ms[dom] * 1e-3) / 1e12
+    traffic = load_pmc_traffic(dom)
+    roofline = {"bound": "mfma", "achieved": round(ach, 3), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
+                "kernel_ms": round(kern_ms[dom], 4), "flop_per_launch": FLOP_ROW[dom] * rows,
+                "per_kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
+                "hot_path_tflops": round(sum(FLOP_ROW.values()) * rows / (hot_ms * 1e-3) / 1e12, 3)}
+    out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic (x~U[0,1) 128x3x32x32 per rank, y~randint(10))",
+           "config": {"workload": "Lyapunov train step of README.md:27 at epoch 20 (configs[1] shape: B=128, "
+                                  "h_sample_size=256 -> 204 uniform + 52 correct-cone rows/image), KWLarge-Cayley "
+                                  "backbone + fused HIP fan-out + Adam",
+                      "global_batch": world * B_PER_RANK, "h_sample_size": H_SAMPLE,
+                      "rows_per_rank": rows, "parallelism": f"dp{world}"},
+           "roofline": roofline,
+           "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -424,42 +424,74 @@ __global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
   }
 }
 
-// Sum of the slabs (fixed order) -> dQ2, dQ3, dQ1, db2, db3; per-image g_u; scalars.
+// Sum of the slabs (fixed order, deterministic) -> dQ2, dQ3, dQ1, db2, db3; per-image g_u;
+// scalars.  Workgroup w < n_el_blocks sums 64 consecutive slab entries: its 4 waves each add a
+// quarter of the slabs (8 independent loads in flight per lane), then combine through LDS.
+// The last workgroup reduces the per-tile scalars.
+constexpr int RED_COLS = 64;
 __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float part[4][RED_COLS];
+  __shared__ double dpart[3][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nwg = a.B * a.parts;
-  if (e < SLAB_B1) {
+  const int n_el_blocks = (SLAB + RED_COLS - 1) / RED_COLS;
+  const int n_gu_blocks = (a.B * M + RED_COLS - 1) / RED_COLS;
+  if ((int)blockIdx.x < n_el_blocks) {
+    const int e = blockIdx.x * RED_COLS + lane;
     float s = 0.f;
-    for (int k = 0; k < nwg; ++k) s += a.slabs[(size_t)k * SLAB + e];
-    if (e < SLAB_Q3) a.grads.Q2[e] = s;
-    else if (e < SLAB_Q1) a.grads.Q3[e - SLAB_Q3] = s;
-    else if (e < SLAB_B2) a.grads.Q1[e - SLAB_Q1] = s;
-    else a.grads.b2[e - SLAB_B2] = s;
-  } else if (e >= SLAB_B3 && e < SLAB_B3 + C) {
-    float s = 0.f;
-    for (int k = 0; k < nwg; ++k) s += a.slabs[(size_t)k * SLAB + e];
-    a.grads.b3[e - SLAB_B3] = s;
-  } else if (e >= SLAB + 0 && e < SLAB + a.B * M) {       // g_u[b][i]
-    const int q = e - SLAB, b = q / M, i = q - b * M;
-    float s = 0.f;
-    for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
-    a.g_u[q] = s;
-  } else if (e == SLAB + a.B * M) {                      // scalars
+    if (e < SLAB) {
+      const int k0 = (nwg * wv) / 4, k1 = (nwg * (wv + 1)) / 4;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int k = k0;
+      for (; k + 8 <= k1; k += 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += a.slabs[(size_t)(k + u) * SLAB + e];
+      for (; k < k1; ++k) acc[0] += a.slabs[(size_t)k * SLAB + e];
+      s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    part[wv][lane] = s;
+    __syncthreads();
+    if (wv == 0 && e < SLAB) {
+      const float t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+      if (e < SLAB_Q3) a.grads.Q2[e] = t;
+      else if (e < SLAB_Q1) a.grads.Q3[e - SLAB_Q3] = t;
+      else if (e < SLAB_B2) a.grads.Q1[e - SLAB_Q1] = t;
+      else if (e < SLAB_B1) a.grads.b2[e - SLAB_B2] = t;
+      else if (e >= SLAB_B3 && e < SLAB_B3 + C) a.grads.b3[e - SLAB_B3] = t;
+    }
+  } else if ((int)blockIdx.x < n_el_blocks + n_gu_blocks) {      // g_u[b][i] = sum over the image's parts
+    const int q = (blockIdx.x - n_el_blocks) * RED_COLS + (threadIdx.x & (RED_COLS - 1));
+    if (threadIdx.x < RED_COLS && q < a.B * M) {
+      const int b = q / M, i = q - b * M;
+      float s = 0.f;
+      for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
+      a.g_u[q] = s;
+    }
+  } else {                                                          // scalars
     const int ntiles = (a.N + 31) / 32;
     double v = 0.0, ef = 0.0, ac = 0.0;
-    for (int t = 0; t < ntiles; ++t) {
-      v += a.tile_sc[4 * t];
-      ef += a.tile_sc[4 * t + 1];
-      ac += a.tile_sc[4 * t + 2];
+    for (int t = threadIdx.x; t < ntiles; t += 256) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(a.tile_sc + 4 * t);
+      v += q[0]; ef += q[1]; ac += q[2];
     }
-    a.scalars[0] = (float)(v / a.N);
-    a.scalars[1] = (float)ef;
-    a.scalars[2] = (float)(ac / ((double)a.N * C));
-    a.scalars[3] = (float)qp_exit_iter(a.conv[0], a.d.max_iter);
-    a.scalars[4] = (float)qp_exit_iter(a.conv[1], a.d.max_iter);
-    a.scalars[5] = (float)v;
-    a.scalars[6] = (float)ac;
-    a.scalars[7] = (float)a.N;
+    dpart[0][threadIdx.x] = v; dpart[1][threadIdx.x] = ef; dpart[2][threadIdx.x] = ac;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o)
+        for (int c = 0; c < 3; ++c) dpart[c][threadIdx.x] += dpart[c][threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      v = dpart[0][0]; ef = dpart[1][0]; ac = dpart[2][0];
+      a.scalars[0] = (float)(v / a.N);
+      a.scalars[1] = (float)ef;
+      a.scalars[2] = (float)(ac / ((double)a.N * C));
+      a.scalars[3] = (float)qp_exit_iter(a.conv[0], a.d.max_iter);
+      a.scalars[4] = (float)qp_exit_iter(a.conv[1], a.d.max_iter);
+      a.scalars[5] = (float)v;
+      a.scalars[6] = (float)ac;
+      a.scalars[7] = (float)a.N;
+    }
   }
 }
 
@@ -594,25 +626,42 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.grads = *grads;
 
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool prof = io->events && io->n_events >= FIODE_LYAP_NKERNELS + 1;
+  int ev = 0;
+  auto mark = [&]() -> int {
+    if (prof) {
+      hipError_t e = hipEventRecord(static_cast<hipEvent_t>(io->events[ev++]), st);
+      if (e != hipSuccess) return 100 + (int)e;
+    }
+    return 0;
+  };
   const int ntiles = (a.N + 31) / 32;
   const int fwd_blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
   const size_t lds_fwd = (size_t)(M + 32) * LDQ * sizeof(float);
   const size_t lds_bwd = (size_t)M * LDQ * sizeof(float);
+  if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_prep, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_fwd, dim3(fwd_blocks), dim3(256), lds_fwd, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_bwd, dim3(fwd_blocks), dim3(256), lds_bwd, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_wgrad, dim3(B * a.parts), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
-  const int red_items = SLAB + B * M + 1;
-  hipLaunchKernelGGL(k_lyap_reduce, dim3((red_items + 255) / 256), dim3(256), 0, st, a);
+  if ((rc = mark())) return rc;
+  const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (B * M + RED_COLS - 1) / RED_COLS + 1;
+  hipLaunchKernelGGL(k_lyap_reduce, dim3(red_blocks), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   const int sg_items = M * FIODE_X + M + B * FIODE_X;
   hipLaunchKernelGGL(k_lyap_static_grads, dim3((sg_items + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  if ((rc = mark())) return rc;
   return FIODE_OK;
 }

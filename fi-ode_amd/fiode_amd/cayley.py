@@ -1,0 +1,114 @@
+"""Cayley-orthogonal layers (host side, PyTorch-ROCm).
+
+The reference imports ``CayleyLinear``, ``CayleyConv`` and ``GroupSort`` from the
+``libs/ortho_conv`` submodule, which is empty in the reference tree.
+The only in-tree statement of the parametrisation is ``convert_cayley``
+(dynamics/classification.py:281-294): Q = cayley(alpha * W / ||W||) with the bias kept apart.
+This module restates the public orthogonal-convolutions design (Trockman & Kolter, ICLR 2021):
+parity with the absent submodule is unpinned; orthogonality is tested (Q^T Q = I).
+
+These maps are tiny per-step parameter transforms (10x10 and 128x128 inverses for the dynamics)
+and stay in PyTorch: their gradients come from autograd, fed by the fused HIP step's dL/dQ.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def cayley(W: torch.Tensor) -> torch.Tensor:
+    """Orthogonal (or orthonormal-column) matrix from an unconstrained W [.., cout, cin]:
+    with U = W[:cin], V = W[cin:], A = U - U^H + V^H V:  Q = [(I+A)^-1 (I-A); -2 V (I+A)^-1].
+    Wide matrices (cin > cout) are handled through the transpose."""
+    if W.dim() == 2:
+        return cayley(W.unsqueeze(0)).squeeze(0)
+    cout, cin = W.shape[-2], W.shape[-1]
+    if cin > cout:
+        return cayley(W.transpose(-2, -1)).transpose(-2, -1)
+    U, V = W[..., :cin, :], W[..., cin:, :]
+    eye = torch.eye(cin, dtype=W.dtype, device=W.device).expand(W.shape[:-2] + (cin, cin))
+    Uh = U.conj().transpose(-2, -1)
+    A = U - Uh + V.conj().transpose(-2, -1) @ V
+    inv = torch.linalg.inv(eye + A)
+    return torch.cat([inv @ (eye - A), -2.0 * (V @ inv)], dim=-2)
+
+
+class CayleyLinear(nn.Linear):
+    """nn.Linear whose effective weight is cayley(alpha * W / ||W||_F) (state_dict keys
+    ``weight``, ``bias``, ``alpha``, as the reference's checkpoints carry)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True):
+        super().__init__(in_features, out_features, bias)
+        self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
+        self._Q = None
+
+    def reset_parameters(self) -> None:
+        std = 1.0 / math.sqrt(self.weight.shape[1])
+        nn.init.uniform_(self.weight, -std, std)
+        if self.bias is not None:
+            nn.init.uniform_(self.bias, -std, std)
+        self._Q = None
+
+    def effective_weight(self) -> torch.Tensor:
+        return cayley(self.alpha * self.weight / self.weight.norm())
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training or self._Q is None:
+            self._Q = self.effective_weight()
+        return F.linear(x, self._Q if self.training else self._Q.detach(), self.bias)
+
+
+class GroupSort(nn.Module):
+    """Sort pairs of channel halves: [max(a, b), min(a, b)] along dim 1."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        a, b = x.split(x.size(1) // 2, 1)
+        return torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=1)
+
+
+class CayleyConv(nn.Conv2d):
+    """Orthogonal circular convolution parametrised per frequency: for each of the n*(n/2+1)
+    rFFT frequencies the cout x cin channel matrix is Cayley-mapped, y = irfft2(Q(w) xfft).
+    stride=2 is an invertible 2x2 space-to-channel downsample followed by a stride-1 conv on
+    4*cin channels (the public design's StridedConv)."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1, bias: bool = True):
+        self.downsample = stride == 2
+        super().__init__(in_channels * (4 if self.downsample else 1), out_channels, kernel_size, stride=1,
+                         padding=kernel_size // 2, bias=bias)
+        self.alpha = nn.Parameter(torch.ones(1))
+        self._alpha_init = False
+        self._shift = {}
+
+    def _shift_matrix(self, n: int, device) -> torch.Tensor:
+        key = (n, str(device))
+        if key not in self._shift:
+            s = -((self.weight.shape[2] - 1) // 2)
+            k = torch.arange(n, device=device, dtype=torch.float64)
+            grid = k[None, :] + k[:, None]
+            sh = torch.exp(2j * math.pi * s * grid / n)[:, : n // 2 + 1]
+            self._shift[key] = sh.reshape(n * (n // 2 + 1), 1, 1).to(torch.complex64)
+        return self._shift[key]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.downsample:
+            b, c, h, w = x.shape
+            x = x.reshape(b, c, h // 2, 2, w // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(b, c * 4, h // 2, w // 2)
+        cout, cin = self.weight.shape[:2]
+        B, _, n, _ = x.shape
+        nf = n * (n // 2 + 1)
+        xf = torch.fft.rfft2(x).permute(2, 3, 1, 0).reshape(nf, cin, B)
+        wf = torch.fft.rfft2(self.weight, (n, n)).reshape(cout, cin, nf).permute(2, 0, 1).conj()
+        wf = self._shift_matrix(n, x.device) * wf
+        if not self._alpha_init:
+            with torch.no_grad():
+                self.alpha.fill_(float(wf.norm()))
+            self._alpha_init = True
+        yf = (cayley(self.alpha * wf / wf.norm()) @ xf).reshape(n, n // 2 + 1, cout, B)
+        y = torch.fft.irfft2(yf.permute(3, 2, 0, 1), s=(n, n))
+        if self.bias is not None:
+            y = y + self.bias[:, None, None]
+        return y

@@ -1,0 +1,198 @@
+"""LyapunovLearning with the fused HIP training step (pl_modules.py:338-502).
+
+``LyapunovLossFn`` is the drop-in for the reference's per-sample autograd graph
+(x_in expand -> sampler -> jvp(DecisionBoundary, eval_dot) -> relu -> mean, pl_modules.py:394-466):
+one call of ``fiode_lyap_step`` computes the loss, the logging statistics and the gradient of the
+loss w.r.t. the effective dynamics weights and the backbone features; backward() only scales the
+saved gradients by the incoming grad and hands them to autograd, which continues through the
+Cayley maps and the backbone.
+
+pytorch_lightning and hydra are absent in this image, so ``LyapunovLearning`` is a plain
+nn.Module keeping the LightningModule method names (training_step, compute_loss,
+validation_step, configure_optimizers, log, current_epoch, global_step).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import ops
+from .dynamics import OrthoClassDynProjectSimplexLips
+from .sampling import CompositeSampler, CompositeSamplerScheduler
+
+
+class LyapunovLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_feat, Q1, b1, Qx, bx, Q2, b2, Q3, b3, y, plan: dict):
+        w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
+        w = {k: v.detach().contiguous() for k, v in w.items()}
+        sc, grads, dbg = ops.lyap_step(
+            x_feat.detach().contiguous(), y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"],
+            sampler=plan["sampler"], dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"],
+            offset=plan["offset"], h=plan.get("h"), masks=plan.get("masks"), debug=plan.get("debug", False),
+            out=plan.get("out"))
+        plan["scalars"] = sc
+        plan["debug_out"] = dbg
+        g = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+        ctx.save_for_backward(*g)
+        return sc[0].clone()
+
+    @staticmethod
+    def backward(ctx, go):
+        g = ctx.saved_tensors
+        return tuple(t * go for t in g) + (None, None)
+
+
+class DecisionBoundary(nn.Module):
+    """lya_cands.py:72-94 (kept for the validation/ODE path; the training step fuses it)."""
+
+    def __init__(self, on_simplex=False, log_mode=False, num_class=10):
+        super().__init__()
+        self.on_simplex, self.log_mode, self.num_class = on_simplex, log_mode, num_class
+
+    def forward(self, state_output, y):
+        prob = state_output if self.on_simplex else F.softmax(state_output, dim=1)
+        prob_y = torch.gather(prob, 1, y[:, None])[:, 0]
+        wrong = torch.masked_select(prob, ~F.one_hot(y, self.num_class).bool()).unflatten(
+            0, (prob.shape[0], prob.shape[1] - 1))
+        v = 1 + wrong.max(dim=-1).values - prob_y
+        return torch.log(v) if self.log_mode else v
+
+
+class UniformInitFun(nn.Module):
+    """dynamics/init_coordinates.py:38-44: h0 = 1/C, static = param_map(x)."""
+
+    def __init__(self, h_dims=(10,), param_map: Optional[nn.Module] = None):
+        super().__init__()
+        self.h_dims = tuple(h_dims)
+        self.param_map = param_map if param_map is not None else nn.Identity()
+        for i, d in enumerate(self.h_dims):
+            self.register_buffer(f"h0_{i}", torch.ones(d) / d)
+
+    def forward(self, x, dyn=None):
+        h0 = tuple(getattr(self, f"h0_{i}")[None].repeat(x.shape[0], 1).to(x.device) for i in range(len(self.h_dims)))
+        return self.param_map(x), h0
+
+
+class DefaultOutputFun(nn.Module):
+    def forward(self, h):
+        return h[-1]
+
+
+class LyapunovLearning(nn.Module):
+    """pl_modules.py:338-502 (order=1, act='relu', DecisionBoundary candidate)."""
+
+    def __init__(self, order, h_sample_size, h_dist_lim, sampler: CompositeSampler,
+                 sampler_scheduler: CompositeSamplerScheduler, dynamics: OrthoClassDynProjectSimplexLips,
+                 init_fun: UniformInitFun, lya_cand=None, output=None, n_input=None, n_output=10, t_max=1.0,
+                 train_ode_solver="dopri5", train_ode_tol=1e-6, val_ode_solver="dopri5", val_ode_tol=1e-6,
+                 opt_name="SGD", lr=1e-3, momentum=0.9, weight_decay=1e-4, decay_epochs=(30, 60, 90),
+                 beta1=0.9, beta2=0.999, scheduler_name="cos_anneal", max_epochs=200, warmup=20,
+                 adv_train=False, eps=36 / 255, norm="L2", simplex=False, act="relu", fix_backbone=False,
+                 val_adv=True, barrier_loss=False, lips_train=False, relax_exp_stable=False, scaleLeps=3.0,
+                 train_ode=False, train_ode_epoch=100, epoch_off_scale=10, lips_warmup=0, seed=0):
+        super().__init__()
+        if order != 1:
+            raise NotImplementedError("order=1 (the reference raises for order 0; higher orders are unused)")
+        if act != "relu":
+            raise NotImplementedError("act='relu' is the README configuration")
+        if barrier_loss or lips_train or relax_exp_stable or adv_train or train_ode:
+            raise NotImplementedError("barrier_loss / lips_train / relax_exp_stable / adv_train / train_ode are off "
+                                      "in the north-star configuration and not fused")
+        self.order, self.h_sample_size, self.h_dist_lim = order, h_sample_size, h_dist_lim
+        self.sampler, self.sampler_scheduler = sampler, sampler_scheduler
+        self.dyn_fun = dynamics
+        self.init_coordinates = init_fun
+        self.lya_cand = lya_cand if lya_cand is not None else DecisionBoundary(on_simplex=True)
+        self.output_fun = output if output is not None else DefaultOutputFun()
+        self.t_max = t_max
+        self.train_ode_solver, self.train_ode_tol = train_ode_solver, train_ode_tol
+        self.val_ode_solver, self.val_ode_tol = val_ode_solver, val_ode_tol
+        self.opt_name, self.lr, self.momentum, self.weight_decay = opt_name, lr, momentum, weight_decay
+        self.decay_epochs, self.betas = list(decay_epochs), (beta1, beta2)
+        self.scheduler_name, self.max_epochs, self.warmup = scheduler_name, max_epochs, warmup
+        self.simplex, self.act, self.eps, self.norm = simplex, act, eps, norm
+        self.epoch_off_scale = epoch_off_scale
+        self.current_epoch = 0
+        self.global_step = 0
+        self.seed = seed
+        self._rng_offset = 0
+        self.logged: Dict[str, float] = {}
+        self._out = None
+
+    # Lightning-like surface -------------------------------------------------------------------
+    def log(self, name, value, **kw):
+        self.logged[name] = value
+
+    def configure_optimizers(self):
+        """pl_modules.py:97-147 (Adam/AdamW/SGD; cosine or step schedule; warm-up Adam)."""
+        params = self.parameters()
+        if self.current_epoch < self.warmup:
+            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas)]
+        if self.opt_name == "Adam":
+            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas)
+        elif self.opt_name == "AdamW":
+            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas)
+        elif self.opt_name == "SGD":
+            opt = torch.optim.SGD(params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
+        else:
+            raise RuntimeError(f"[ERROR] Invalid Optimizer Param: {self.opt_name}")
+        if self.scheduler_name == "cos_anneal":
+            sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=self.max_epochs)
+        elif self.scheduler_name == "step":
+            sch = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=self.decay_epochs, gamma=0.1)
+        else:
+            return [opt]
+        return [opt], [sch]
+
+    def training_step(self, batch, batch_idx=0):
+        x, y = batch
+        loss = self.compute_loss(x, y, x.shape[0], self.act)
+        self.log("training_loss", loss)
+        return loss
+
+    # the hot path -----------------------------------------------------------------------------
+    def current_kappa(self) -> float:
+        """pl_modules.py:447-450."""
+        dyn = self.dyn_fun
+        if self.global_step < dyn.kappa_length:
+            return self.global_step / dyn.kappa_length * dyn.kappa
+        return dyn.kappa
+
+    def step_plan(self, y: torch.Tensor, h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None,
+                  debug: bool = False) -> dict:
+        mix = self.sampler_scheduler.get_mixer_coefficients(self.current_epoch)
+        for i, m in enumerate(mix):
+            self.log(f"mixing_weight_{i}", float(m))
+        kind, s1 = self.sampler.kernel_plan(self.h_sample_size, mix)
+        drop = L.FIODE_DROPOUT_PHILOX if self.training else L.FIODE_DROPOUT_OFF
+        if masks is not None:
+            drop = L.FIODE_DROPOUT_GIVEN
+        if h is not None:
+            kind = L.FIODE_SAMPLER_GIVEN
+        plan = dict(dyn=self.dyn_fun.dyn_cfg(), S=self.h_sample_size, S1=s1, sampler=kind, dropout_mode=drop,
+                    kappa=self.current_kappa(), seed=self.seed, offset=self._rng_offset, h=h, masks=masks,
+                    debug=debug, out=None)
+        self._rng_offset += 1
+        return plan
+
+    def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
+        """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""
+        if self.current_epoch == self.epoch_off_scale:
+            self.dyn_fun.scale_nominal = False
+        static_state, _ = self.init_coordinates(x, self.dyn_fun)
+        plan = self.step_plan(y, h=h, masks=masks, debug=debug)
+        w = self.dyn_fun.effective_weights()
+        loss = LyapunovLossFn.apply(static_state.float(), w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"],
+                                    w["Q3"], w["b3"], y, plan)
+        sc = plan["scalars"]
+        self.log("kappa", plan["kappa"])
+        self.log("effective_batch_size", sc[1])
+        self.log("mean_active_constraints", sc[2])
+        self.last_plan = plan
+        return loss

@@ -79,8 +79,10 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
               sample_size: int, n_uniform: int, sampler: int = L.FIODE_SAMPLER_COMPOSITE,
               dropout_mode: int = L.FIODE_DROPOUT_PHILOX, kappa: float = 2.0, seed: int = 0, offset: int = 0,
               h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None, debug: bool = False,
-              out: Optional[dict] = None):
-    """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict)."""
+              out: Optional[dict] = None, events=None):
+    """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict).
+    ``events``: optional list of len(_lib.LYAP_KERNELS)+1 torch.cuda.Event(enable_timing=True),
+    recorded by the library around each of its kernels on the current stream."""
     dev = x_feat.device
     B = x_feat.shape[0]
     S = int(sample_size)
@@ -118,10 +120,20 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
     cfg = L.LyapConfig(B, S, int(n_uniform), int(sampler), int(dropout_mode), float(kappa),
                        int(seed) & (2**64 - 1), int(offset) & (2**64 - 1))
     dc = dyn.to_c()
+    ev_arr, n_ev = None, 0
+    if events is not None:
+        if len(events) < len(L.LYAP_KERNELS) + 1:
+            raise ValueError("need len(LYAP_KERNELS)+1 events")
+        st = torch.cuda.current_stream(dev)
+        for e in events:          # torch creates the hipEvent lazily on first record
+            if e.cuda_event == 0:
+                e.record(st)
+        ev_arr = (ct.c_void_p * len(events))(*[e.cuda_event for e in events])
+        n_ev = len(events)
     io = L.LyapIO(x_feat.data_ptr(), y.data_ptr(), _ptr(h), _ptr(masks), scalars.data_ptr(),
                   _ptr(dbg.get("h")), _ptr(dbg.get("V")), _ptr(dbg.get("Vdot")), _ptr(dbg.get("f")),
                   _ptr(dbg.get("f_log")), _ptr(dbg.get("qp_lower")), _ptr(dbg.get("qp_nominal")),
-                  _ptr(dbg.get("g_ftilde")))
+                  _ptr(dbg.get("g_ftilde")), ct.cast(ev_arr, ct.c_void_p) if ev_arr is not None else None, n_ev)
     cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
     lib = L.lib()
     nbytes = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dc))

@@ -92,7 +92,16 @@ typedef struct fiode_lyap_io {
   float* qp_lower;       /* [N][C] QP lower bound                                              */
   float* qp_nominal;     /* [2][N][C] QP nominal (loss pass, logging pass)                     */
   float* g_ftilde;       /* [N][C] d loss / d mlp_to_hidden output                             */
+  /* optional profiling: hipEvent_t handles recorded on `stream` before the first kernel and
+   * after each of the FIODE_LYAP_NKERNELS kernels (needs n_events >= FIODE_LYAP_NKERNELS + 1) */
+  void* const* events;
+  int32_t n_events;
 } fiode_lyap_io;
+
+/* kernels of one fiode_lyap_step, in launch order (for the profiling events) */
+#define FIODE_LYAP_NKERNELS 7
+/* static_proj, prep (sampler + dropout words), fwd (2 eval_dot passes), bwd (QP finalize + loss +
+ * activation grads), wgrad (weight-gradient GEMMs), reduce, static_grads */
 
 typedef struct fiode_lyap_grads {  /* outputs, overwritten: d loss / d (effective weights) */
   float *Q1, *b1, *Qx, *bx, *Q2, *b2, *Q3, *b3;
