@@ -66,6 +66,7 @@ def build_module(dev, seed=0):
     mod = LyapunovLearning(order=1, h_sample_size=H_SAMPLE, h_dist_lim=15.0, sampler=sampler,
                            sampler_scheduler=sched, dynamics=dyn, init_fun=UniformInitFun((10,), backbone),
                            lya_cand=DecisionBoundary(on_simplex=True), t_max=1.0, opt_name="Adam", lr=5e-3,
+                           train_ode_tol=1e-3, val_ode_solver="dopri5", val_ode_tol=1e-3,
                            weight_decay=0.0, warmup=-1, max_epochs=300, simplex=True, act="relu", val_adv=False,
                            seed=seed)
     mod.current_epoch = EPOCH

@@ -58,10 +58,13 @@ class LyapGrads(ct.Structure):
     _fields_ = [(n, ct.c_void_p) for n in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3", "x_feat")]
 
 
+FIODE_ODE_RK4, FIODE_ODE_DOPRI5 = 0, 1
+FIODE_ODE_MAX_BATCH = 4096
+
+
 class OdeConfig(ct.Structure):
-    _fields_ = [("method", ct.c_int32), ("batch", ct.c_int32), ("t0", ct.c_double), ("t1", ct.c_double),
-                ("rtol", ct.c_double), ("atol", ct.c_double), ("step_size", ct.c_double),
-                ("max_steps", ct.c_int32)]
+    _fields_ = [("method", ct.c_int32), ("batch", ct.c_int32), ("n_times", ct.c_int32), ("max_steps", ct.c_int32),
+                ("rtol", ct.c_double), ("atol", ct.c_double), ("step_size", ct.c_double)]
 
 
 class CertifyConfig(ct.Structure):
@@ -89,6 +92,9 @@ def _load():
         "fiode_dyn_eval_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_dyn_eval": (ct.c_int, [_vp, ct.POINTER(DynConfig), ct.POINTER(DynWeights), ct.c_int32, ct.c_int32,
                                       _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_odeint_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
+        "fiode_odeint": (ct.c_int, [_vp, ct.POINTER(OdeConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

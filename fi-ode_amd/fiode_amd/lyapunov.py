@@ -23,6 +23,8 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import ops
 from .dynamics import OrthoClassDynProjectSimplexLips
+from .models import IVP, DefaultOutputFun
+from .odeint import make_solver_params
 from .sampling import CompositeSampler, CompositeSamplerScheduler
 
 
@@ -79,11 +81,6 @@ class UniformInitFun(nn.Module):
         return self.param_map(x), h0
 
 
-class DefaultOutputFun(nn.Module):
-    def forward(self, h):
-        return h[-1]
-
-
 class LyapunovLearning(nn.Module):
     """pl_modules.py:338-502 (order=1, act='relu', DecisionBoundary candidate)."""
 
@@ -106,11 +103,13 @@ class LyapunovLearning(nn.Module):
                                       "in the north-star configuration and not fused")
         self.order, self.h_sample_size, self.h_dist_lim = order, h_sample_size, h_dist_lim
         self.sampler, self.sampler_scheduler = sampler, sampler_scheduler
-        self.dyn_fun = dynamics
-        self.init_coordinates = init_fun
+        # same module tree as the reference (state_dict keys model.dyn_fun.*, model.init_coordinates.*)
+        self.model = IVP(n_input=n_input, n_output=n_output, dyn_fun=dynamics, init_coordinates=init_fun,
+                         output_fun=output if output is not None else DefaultOutputFun(), ode_tol=train_ode_tol,
+                         ts=torch.linspace(0, t_max, 2))
         self.lya_cand = lya_cand if lya_cand is not None else DecisionBoundary(on_simplex=True)
-        self.output_fun = output if output is not None else DefaultOutputFun()
         self.t_max = t_max
+        self.use_adjoint = False
         self.train_ode_solver, self.train_ode_tol = train_ode_solver, train_ode_tol
         self.val_ode_solver, self.val_ode_tol = val_ode_solver, val_ode_tol
         self.opt_name, self.lr, self.momentum, self.weight_decay = opt_name, lr, momentum, weight_decay
@@ -124,6 +123,42 @@ class LyapunovLearning(nn.Module):
         self._rng_offset = 0
         self.logged: Dict[str, float] = {}
         self._out = None
+
+    @property
+    def dyn_fun(self):
+        return self.model.dyn_fun
+
+    @property
+    def init_coordinates(self):
+        return self.model.init_coordinates
+
+    @property
+    def train_solver_params(self):
+        return make_solver_params(self.train_ode_solver, self.train_ode_tol)
+
+    @property
+    def val_solver_params(self):
+        return make_solver_params(self.val_ode_solver, self.val_ode_tol)
+
+    def forward(self, x, t_steps=2, return_traj=False):
+        """ODELearning.forward (pl_modules.py:322-325): validation/inference ODE solve."""
+        return self.model(x, ts=torch.linspace(0.0, self.t_max, t_steps, device=x.device),
+                          int_params=self.val_solver_params, use_adjoint=self.use_adjoint, return_traj=return_traj)
+
+    def validation_step(self, batch, batch_idx=0):
+        """GeneralLearning.validation_step without attacks (val_adv=False, pl_modules.py:203-219)."""
+        x, y = batch
+        with torch.no_grad():
+            net_out = self(x)
+        error = (net_out.argmax(dim=-1) != y).float().mean()
+        if self.simplex:
+            loss = F.nll_loss(torch.log(torch.clamp(net_out, min=1e-12)), y)
+        else:
+            loss = F.cross_entropy(net_out, y)
+        self.log("validation_loss", loss)
+        self.log("validation_error", error)
+        self.log("validation_adv_error", error)
+        return loss
 
     # Lightning-like surface -------------------------------------------------------------------
     def log(self, name, value, **kw):

@@ -55,3 +55,44 @@ def make_ortho_KWLarge_Concat(n_in_channels=3, n_outputs=10, mu=(0.485, 0.456, 0
                               out_dim=10, act="GroupSort"):
     """models.py:29-35 (CIFAR10 MU/STD from ExpConfig.py:57-58)."""
     return nn.Sequential(Normalize(mu, std), KWLargeConcat(out_dim=out_dim, act=act))
+
+
+class DefaultOutputFun(nn.Module):
+    """dynamics/output_coordinates.py:4-9."""
+
+    def forward(self, h):
+        return h[-1]
+
+
+class IVP(nn.Module):
+    """models.py:181-242: holds dyn_fun / init_coordinates / output_fun; ``integrate`` calls the
+    torchdiffeq-compatible odeint, which runs the HIP solver for the HIP dynamics."""
+
+    def __init__(self, n_input, n_output, dyn_fun, init_coordinates, output_fun=None, ode_tol=1e-2, ts=None):
+        super().__init__()
+        self.n_input = n_input
+        self.n_output = n_output
+        self.dyn_fun = dyn_fun
+        self.ode_tol = ode_tol
+        self.register_buffer("ts", torch.linspace(0, 1, 200) if ts is None else ts)
+        self.output_fun = output_fun if output_fun is not None else DefaultOutputFun()
+        self.init_coordinates = init_coordinates
+
+    def h_dot(self, t, h):
+        return self.dyn_fun.ode_forward(t, h)
+
+    def forward(self, x, ts=None, int_params=None, use_adjoint=False, return_traj=False):
+        solution = self.integrate(x, ts=ts, int_params=int_params, use_adjoint=use_adjoint)
+        if return_traj:
+            return self.output_fun(solution)
+        return self.output_fun(solution)[-1]
+
+    def integrate(self, x, ts=None, int_params=None, use_adjoint=False):
+        from .odeint import odeint
+        if use_adjoint:
+            raise NotImplementedError("odeint_adjoint (SURVEY.md section 8f row 3)")
+        ts = self.ts if ts is None else ts
+        int_params = dict(rtol=self.ode_tol, atol=self.ode_tol) if int_params is None else dict(int_params)
+        static_state, state = self.init_coordinates(x, self.dyn_fun)
+        self.dyn_fun.static_state = static_state
+        return odeint(self.h_dot, state, ts, **int_params)

@@ -197,3 +197,40 @@ def dyn_eval(h: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Ten
                             h.data_ptr(), f.data_ptr(), it.data_ptr(), ws.data_ptr(), ws.numel())
     L.check(rc, "fiode_dyn_eval")
     return f, it
+
+
+def odeint_dyn(x_feat: torch.Tensor, h0: torch.Tensor, times: torch.Tensor, weights: Dict[str, torch.Tensor],
+               dyn: DynCfg, method: str = "dopri5", rtol: float = 1e-3, atol: float = 1e-3,
+               step_size: Optional[float] = None, max_steps: int = 100000):
+    """fiode_odeint: solve dh/dt = eval_dot(h, x_feat) (eval mode) from h0 over ``times``.
+    Returns (solution [T,B,C], stats int32[8], dstats float64[4]) -- all on the device."""
+    dev = h0.device
+    B = h0.shape[0]
+    if B > L.FIODE_ODE_MAX_BATCH:
+        raise ValueError(f"batch {B} > FIODE_ODE_MAX_BATCH")
+    h0 = _need(h0, "h0", (B, C), torch.float32, dev)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    T = times.shape[0]
+    times = _need(times.reshape(-1), "times", (T,), torch.float64, dev)
+    if method == "rk4":
+        if step_size is None or not step_size > 0:
+            raise ValueError("rk4 needs options.step_size > 0")
+        m = L.FIODE_ODE_RK4
+    elif method == "dopri5":
+        m = L.FIODE_ODE_DOPRI5
+    else:
+        raise NotImplementedError(f"method {method!r}: the HIP stepper implements 'rk4' and 'dopri5'")
+    ws_w, cw = _weights_c(weights, dev)
+    sol = torch.empty((T, B, C), dtype=torch.float32, device=dev)
+    stats = torch.zeros(8, dtype=torch.int32, device=dev)
+    dstats = torch.zeros(4, dtype=torch.float64, device=dev)
+    cfg = L.OdeConfig(m, B, T, int(max_steps), float(rtol), float(atol), float(step_size or 0.0))
+    lib = L.lib()
+    ws = _Workspace.get(dev, lib.fiode_odeint_workspace_bytes(B), "ode")
+    dc = dyn.to_c()
+    rc = lib.fiode_odeint(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(), h0.data_ptr(),
+                          times.data_ptr(), sol.data_ptr(), stats.data_ptr(), dstats.data_ptr(), ws.data_ptr(),
+                          ws.numel())
+    L.check(rc, "fiode_odeint")
+    del ws_w
+    return sol, stats, dstats

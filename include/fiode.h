@@ -140,6 +140,32 @@ FIODE_API int fiode_dyn_eval(void* stream, const fiode_dyn_config* dyn, const fi
                    int32_t batch, int32_t rows_per_image, const float* x_feat, const float* h,
                    float* f, int32_t* exit_iter, void* workspace, size_t workspace_bytes);
 
+/* ---- ODE solves (models.py:211-242 IVP.integrate -> torchdiffeq.odeint) ------------------- */
+enum { FIODE_ODE_RK4 = 0, FIODE_ODE_DOPRI5 = 1 };
+#define FIODE_ODE_MAX_BATCH 4096
+
+typedef struct fiode_ode_config {
+  int32_t method;        /* FIODE_ODE_RK4 (fixed grid, 3/8 rule) or FIODE_ODE_DOPRI5          */
+  int32_t batch;         /* B rows (one per image), <= FIODE_ODE_MAX_BATCH                     */
+  int32_t n_times;       /* >= 2 output times (device float64 array, increasing)              */
+  int32_t max_steps;     /* dopri5 step cap (<= 0: 100000)                                     */
+  double rtol, atol;     /* dopri5 (make_solver_params: rtol = atol = ode_tol, pl_modules.py:26) */
+  double step_size;      /* rk4 (make_solver_params: options.step_size = ode_tol, :27-33)       */
+} fiode_ode_config;
+
+FIODE_API size_t fiode_odeint_workspace_bytes(int32_t batch);
+
+/* odeint(IVP.h_dot, (h0,), times, method, rtol/atol | step_size) with f = ode_forward in eval
+ * mode (no dropout), static_state = x_feat.  solution: [n_times][B][C] (solution[0] = h0).
+ * stats (device int32[8]): nfe, n_accept (rk4: steps), n_reject, status (0 ok, 2 max_steps,
+ * 3 dt underflow), last QP exit iteration, dopri5 attempted steps.  dstats (device double[4]):
+ * next dt, final t, last error ratio.  One persistent workgroup per solve (batch-global QP exit
+ * and RMS error norm are workgroup reductions). */
+FIODE_API int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fiode_dyn_config* dyn,
+                           const fiode_dyn_weights* w, const float* x_feat, const float* h0,
+                           const double* times, float* solution, int32_t* stats, double* dstats,
+                           void* workspace, size_t workspace_bytes);
+
 /* Error text for a return code. */
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);

@@ -572,24 +572,63 @@ def make_ode_func(x_feat: np.ndarray, P: DynParams, cfg: DynConfig, counter: Opt
     return func
 
 
-def rk4_fixed_grid(func, y0: np.ndarray, t0: float, t1: float, step_size: float):
+def linspace32(t0: float, t1: float, steps: int) -> np.ndarray:
+    """torch.linspace(t0, t1, steps) in float32 (the reference builds ts this way,
+    pl_modules.py:323): start + i*step for the first half, end - (steps-1-i)*step after."""
+    if steps == 1:
+        return np.array([t0], np.float32)
+    a, b = F32(t0), F32(t1)
+    step = F32((b - a) / F32(steps - 1))
+    out = np.empty(steps, np.float32)
+    half = steps // 2
+    for i in range(steps):
+        out[i] = F32(a + step * F32(i)) if i < half else F32(b - step * F32(steps - 1 - i))
+    return out
+
+
+def rk4_grid(t0: float, t1: float, step_size: float) -> np.ndarray:
+    """FixedGridODESolver._grid_constructor_from_step_size in float32 (the reference's ts are
+    float32): niters = ceil((t1-t0)/h + 1); t_k = k*h + t0; last point snapped to t1."""
+    a, b, h = F32(t0), F32(t1), F32(step_size)
+    niters = int(math.ceil(float(F32(F32(b - a) / h) + F32(1))))
+    grid = (np.arange(niters, dtype=np.float32) * h + a).astype(np.float32)
+    grid[-1] = b
+    return grid
+
+
+def rk4_fixed_grid(func, y0: np.ndarray, t0: float, t1: float, step_size: float,
+                   times: Optional[np.ndarray] = None):
     """torchdiffeq method='rk4' (FixedGridODESolver + rk4_alt_step_func, the 3/8 rule) with
-    ``options.step_size`` (pl_modules.py:27-33).  Grid: niters = ceil((t1-t0)/h + 1),
-    t_k = k*h + t0, last point snapped to t1; returns y(t1) (linear interp at t == t1 is y1)."""
+    ``options.step_size`` (pl_modules.py:27-33).  Returns (solution at ``times`` [T,B,C] -- or
+    y(t1) when times is None --, number of steps).  Output points use the solver's linear
+    interpolation (exact grid hits return the grid value)."""
     y = np.asarray(y0, F32)
-    niters = int(math.ceil(float(F32(t1 - t0)) / step_size + 1))
-    grid = [k * step_size + t0 for k in range(niters)]
-    grid[-1] = t1
-    third, two_thirds = 1.0 / 3.0, 2.0 / 3.0
+    grid = rk4_grid(t0, t1, step_size)
+    ts = np.array([t0, t1], np.float32) if times is None else np.asarray(times, np.float32)
+    sol = [y.copy()]
+    j = 1
+    third = F32(1.0 / 3.0)
     for a, b in zip(grid[:-1], grid[1:]):
         dt = F32(b - a)
-        k1 = func(a, y)
-        k2 = func(a + dt * third, (y + (dt * k1).astype(F32) * F32(third)).astype(F32))
-        k3 = func(a + dt * two_thirds, (y + dt * (k2 - (k1 * F32(third)).astype(F32)).astype(F32)).astype(F32))
-        k4 = func(b, (y + dt * ((k1 - k2).astype(F32) + k3).astype(F32)).astype(F32))
+        k1 = func(float(a), y)
+        k2 = func(float(a + dt * third), (y + (dt * k1).astype(F32) * third).astype(F32))
+        k3 = func(float(a + dt * F32(2.0 / 3.0)), (y + dt * (k2 - (k1 * third).astype(F32)).astype(F32)).astype(F32))
+        k4 = func(float(b), (y + dt * ((k1 - k2).astype(F32) + k3).astype(F32)).astype(F32))
         dy = ((((k1 + F32(3) * (k2 + k3).astype(F32)).astype(F32) + k4).astype(F32) * dt).astype(F32) * F32(0.125)).astype(F32)
-        y = (y + dy).astype(F32)
-    return y, len(grid) - 1
+        y1 = (y + dy).astype(F32)
+        while j < len(ts) and b >= ts[j]:
+            if ts[j] == a:
+                sol.append(y.copy())
+            elif ts[j] == b:
+                sol.append(y1.copy())
+            else:
+                slope = F32((ts[j] - a) / (b - a))
+                sol.append((y + slope * (y1 - y).astype(F32)).astype(F32))
+            j += 1
+        y = y1
+    if times is None:
+        return y, len(grid) - 1
+    return np.stack(sol), len(grid) - 1
 
 
 DOPRI5_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1.0, 1.0]
@@ -628,7 +667,7 @@ class Dopri5Stats:
 
 def dopri5(func, y0: np.ndarray, t0: float, t1: float, rtol: float, atol: float,
            safety: float = 0.9, ifactor: float = 10.0, dfactor: float = 0.2,
-           max_steps: int = 100000) -> Tuple[np.ndarray, Dopri5Stats]:
+           max_steps: int = 100000, times: Optional[np.ndarray] = None) -> Tuple[np.ndarray, Dopri5Stats]:
     """torchdiffeq 0.2.2 RKAdaptiveStepsizeODESolver with the Dormand-Prince tableau: initial
     step from _select_initial_step(order-1=4), FSAL stages, batch-global RMS error ratio,
     accept iff ratio <= 1, _optimal_step_size(order 5), dense output at t1 by the 4th-order
@@ -660,57 +699,62 @@ def dopri5(func, y0: np.ndarray, t0: float, t1: float, rtol: float, atol: float,
     fcur = f0
     interp = None
     tprev, tnext = t0, t0
-    while t1 > tnext:
-        if len(st.steps) >= max_steps:
-            raise RuntimeError("dopri5: too many steps")
-        assert tcur + dt > tcur, "underflow in dt"
-        ta = tcur + dt
-        dt32 = F32(dt)
-        k = [fcur]
-        for i in range(6):
-            coeffs = (beta[i] * dt32).astype(F32)
-            acc = np.zeros_like(y)
-            for j in range(i + 1):
-                acc = (acc + k[j] * coeffs[j]).astype(F32)
-            yi = (y + acc).astype(F32)
-            k.append(func(ta if DOPRI5_ALPHA[i] == 1.0 else tcur + DOPRI5_ALPHA[i] * dt, yi)); st.nfe += 1
-        ynew = yi
-        ce = (cerr * dt32).astype(F32)
-        err = np.zeros_like(y)
-        for j in range(7):
-            err = (err + k[j] * ce[j]).astype(F32)
-        etol = (atol32 + rtol32 * np.maximum(np.abs(y), np.abs(ynew))).astype(F32)
-        ratio = rms_norm((err / etol).astype(F32))
-        accept = ratio <= 1
-        st.steps.append((tcur, dt, bool(accept), float(ratio)))
-        if accept:
-            cm = (cmid * dt32).astype(F32)
-            acc = np.zeros_like(y)
+    ts = [t0, t1] if times is None else [float(t) for t in times]
+    sol = [y.copy()]
+    for tout in ts[1:]:
+        while tout > tnext:
+            if len(st.steps) >= max_steps:
+                raise RuntimeError("dopri5: too many steps")
+            assert tcur + dt > tcur, "underflow in dt"
+            ta = tcur + dt
+            dt32 = F32(dt)
+            k = [fcur]
+            for i in range(6):
+                coeffs = (beta[i] * dt32).astype(F32)
+                acc = np.zeros_like(y)
+                for j in range(i + 1):
+                    acc = (acc + k[j] * coeffs[j]).astype(F32)
+                yi = (y + acc).astype(F32)
+                k.append(func(ta if DOPRI5_ALPHA[i] == 1.0 else tcur + DOPRI5_ALPHA[i] * dt, yi)); st.nfe += 1
+            ynew = yi
+            ce = (cerr * dt32).astype(F32)
+            err = np.zeros_like(y)
             for j in range(7):
-                acc = (acc + k[j] * cm[j]).astype(F32)
-            ymid = (y + acc).astype(F32)
-            fa, fb = k[0], k[6]
-            a = (F32(2) * dt32 * (fb - fa) - F32(8) * (ynew + y) + F32(16) * ymid).astype(F32)
-            b = (dt32 * (F32(5) * fa - F32(3) * fb) + F32(18) * y + F32(14) * ynew - F32(32) * ymid).astype(F32)
-            c = (dt32 * (fb - F32(4) * fa) - F32(11) * y - F32(5) * ynew + F32(16) * ymid).astype(F32)
-            d = (dt32 * fa).astype(F32)
-            interp = [y.copy(), d, c, b, a]
-            tprev, tnext = tcur, ta
-            y, fcur, tcur = ynew, k[6], ta
-            st.n_accept += 1
-        else:
-            tprev, tnext = tcur, tcur
-            st.n_reject += 1
-        # _optimal_step_size (float64)
-        if ratio == 0:
-            dt = dt * ifactor
-        else:
-            df = 1.0 if ratio < 1 else dfactor
-            dt = dt * min(ifactor, max(safety / float(ratio) ** (1.0 / 5.0), df))
-    x = F32((t1 - tprev) / (tnext - tprev))
-    total = (interp[0] + x * interp[1]).astype(F32)
-    xp = x
-    for coef in interp[2:]:
-        xp = F32(xp * x)
-        total = (total + xp * coef).astype(F32)
-    return total, st
+                err = (err + k[j] * ce[j]).astype(F32)
+            etol = (atol32 + rtol32 * np.maximum(np.abs(y), np.abs(ynew))).astype(F32)
+            ratio = rms_norm((err / etol).astype(F32))
+            accept = ratio <= 1
+            st.steps.append((tcur, dt, bool(accept), float(ratio)))
+            if accept:
+                cm = (cmid * dt32).astype(F32)
+                acc = np.zeros_like(y)
+                for j in range(7):
+                    acc = (acc + k[j] * cm[j]).astype(F32)
+                ymid = (y + acc).astype(F32)
+                fa, fb = k[0], k[6]
+                a = (F32(2) * dt32 * (fb - fa) - F32(8) * (ynew + y) + F32(16) * ymid).astype(F32)
+                b = (dt32 * (F32(5) * fa - F32(3) * fb) + F32(18) * y + F32(14) * ynew - F32(32) * ymid).astype(F32)
+                c = (dt32 * (fb - F32(4) * fa) - F32(11) * y - F32(5) * ynew + F32(16) * ymid).astype(F32)
+                d = (dt32 * fa).astype(F32)
+                interp = [y.copy(), d, c, b, a]
+                tprev, tnext = tcur, ta
+                y, fcur, tcur = ynew, k[6], ta
+                st.n_accept += 1
+            else:
+                st.n_reject += 1
+            # _optimal_step_size (float64)
+            if ratio == 0:
+                dt = dt * ifactor
+            else:
+                df = 1.0 if ratio < 1 else dfactor
+                dt = dt * min(ifactor, max(safety / float(ratio) ** (1.0 / 5.0), df))
+        x = F32((tout - tprev) / (tnext - tprev))
+        total = (interp[0] + x * interp[1]).astype(F32)
+        xp = x
+        for coef in interp[2:]:
+            xp = F32(xp * x)
+            total = (total + xp * coef).astype(F32)
+        sol.append(total)
+    if times is None:
+        return sol[-1], st
+    return np.stack(sol), st
