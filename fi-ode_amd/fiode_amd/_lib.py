@@ -68,9 +68,8 @@ class OdeConfig(ct.Structure):
 
 
 class CertifyConfig(ct.Structure):
-    _fields_ = [("n_points", ct.c_int64), ("label", ct.c_int32), ("T", ct.c_int32), ("eps_grid", ct.c_float),
-                ("dist", ct.c_float), ("kappa", ct.c_float), ("lips_alpha_1", ct.c_float),
-                ("lips_sigma_1", ct.c_float), ("enumerate_grid", ct.c_int32)]
+    _fields_ = [("n_classes", ct.c_int32), ("T", ct.c_int32), ("batches", ct.c_int32), ("label", ct.c_int32),
+                ("eps", ct.c_float), ("min_std", ct.c_float)]
 
 
 def _load():
@@ -95,6 +94,11 @@ def _load():
         "fiode_odeint_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_odeint": (ct.c_int, [_vp, ct.POINTER(OdeConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_certify_grid_rows": (ct.c_int64, [ct.c_int32, ct.c_int32]),
+        "fiode_certify_grid": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp]),
+        "fiode_certify_workspace_bytes": (ct.c_size_t, [ct.c_int64, ct.c_int32]),
+        "fiode_certify": (ct.c_int, [_vp, ct.POINTER(CertifyConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
+                                     _vp, _vp, ct.c_int64, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

@@ -234,3 +234,38 @@ def odeint_dyn(x_feat: torch.Tensor, h0: torch.Tensor, times: torch.Tensor, weig
     L.check(rc, "fiode_odeint")
     del ws_w
     return sol, stats, dstats
+
+
+def certify_grid(T: int = 40, n: int = C, device="cuda") -> torch.Tensor:
+    """grid_label_0 of sample_decision_boundary(n, T) as uint8 counts [G][n] (eta = v/T)."""
+    lib = L.lib()
+    G = lib.fiode_certify_grid_rows(n, T)
+    if G < 0:
+        raise ValueError(f"unsupported grid n={n} T={T}")
+    dev = torch.device(device)
+    grid = torch.empty((max(G, 1), n), dtype=torch.uint8, device=dev)
+    L.check(lib.fiode_certify_grid(_stream(dev), n, T, grid.data_ptr()), "fiode_certify_grid")
+    return grid[:G]
+
+
+def certify_image(x_feat: torch.Tensor, label: int, grid: torch.Tensor, weights: Dict[str, torch.Tensor],
+                  dyn: DynCfg, T: int = 40, batches: int = 10, eps: float = 0.141, min_std: float = 0.225):
+    """One image of certify_lipschitz.py:104-143: returns (out [nb][2] = per-batch max violation and
+    max violation_larger_T, exit_iters [nb]) on the device."""
+    dev = grid.device
+    G = grid.shape[0]
+    x_feat = _need(x_feat.reshape(-1), "x_feat", (X,), torch.float32, dev)
+    grid = _need(grid, "grid", (G, C), torch.uint8, dev)
+    nb = batches + (1 if G % batches else 0)
+    out = torch.empty((nb, 2), dtype=torch.float32, device=dev)
+    it = torch.empty(nb, dtype=torch.int32, device=dev)
+    ws_w, cw = _weights_c(weights, dev)
+    lib = L.lib()
+    ws = _Workspace.get(dev, lib.fiode_certify_workspace_bytes(G, batches), "cert")
+    cfg = L.CertifyConfig(C, int(T), int(batches), int(label), float(eps), float(min_std))
+    dc = dyn.to_c()
+    rc = lib.fiode_certify(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(), grid.data_ptr(),
+                           G, out.data_ptr(), it.data_ptr(), ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_certify")
+    del ws_w
+    return out, it

@@ -166,6 +166,29 @@ FIODE_API int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fiod
                            const double* times, float* solution, int32_t* stats, double* dstats,
                            void* workspace, size_t workspace_bytes);
 
+/* ---- Certification grid (robustness/eval_utils.py:31-89, certify_lipschitz.py:37-143) ------ */
+typedef struct fiode_certify_config {
+  int32_t n_classes;     /* 10                                                                   */
+  int32_t T;             /* grid density (reference: 40)                                         */
+  int32_t batches;       /* cfg.batches: G // batches rows per batch, +1 tail batch (ref: 10)     */
+  int32_t label;         /* the image's label (selects the column swap of get_grid_for_label)    */
+  float eps;             /* cfg.eps (0.141): kappa = sqrt(2) * Lfx * eps                         */
+  float min_std;         /* min(Normalize.std): Lfx = (scale_nominal ? alpha_1 : 1) / min_std    */
+} fiode_certify_config;
+
+/* Rows G of the decision-boundary grid {v in Z>=0^n : sum v = T, v_0 = max_{i>=1} v_i}; -1 if
+ * unsupported (n <= 16, T <= 64, G < 2^32).  Host only. */
+FIODE_API int64_t fiode_certify_grid_rows(int32_t n, int32_t T);
+/* Build grid_label_0 as uint8 counts [G][n] (eta = v/T) in sample_decision_boundary's row order. */
+FIODE_API int fiode_certify_grid(void* stream, int32_t n, int32_t T, uint8_t* grid);
+FIODE_API size_t fiode_certify_workspace_bytes(int64_t G, int32_t batches);
+/* One image: per batch of grid rows, out[b] = (max violation, max violation_larger_T) with the
+ * QP exit global over the batch (eval_dot_light on the batch), exit_iters[b] its exit iteration.
+ * x_feat: [X] the image's static features.  nb = batches + (G % batches != 0). */
+FIODE_API int fiode_certify(void* stream, const fiode_certify_config* cfg, const fiode_dyn_config* dyn,
+                            const fiode_dyn_weights* w, const float* x_feat, const uint8_t* grid, int64_t G,
+                            float* out, int32_t* exit_iters, void* workspace, size_t workspace_bytes);
+
 /* Error text for a return code. */
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);

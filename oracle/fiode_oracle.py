@@ -758,3 +758,164 @@ def dopri5(func, y0: np.ndarray, t0: float, t1: float, rtol: float, atol: float,
     if times is None:
         return sol[-1], st
     return np.stack(sol), st
+
+
+# ---------------------------------------------------------------------------------------------
+# Certification grid -- robustness/eval_utils.py:31-89, robustness/certify_lipschitz.py:37-143
+# ---------------------------------------------------------------------------------------------
+
+def db_count_table(n: int = 10, T: int = 40) -> List[List[int]]:
+    """Row counts of the decision-boundary grid construction (count_samples_decision_boundary,
+    eval_utils.py:72-89): f[j][k] = number of k-dim non-negative integer vectors with sum j whose
+    coordinate 0 equals the max of the others, in the construction's case split."""
+    f = [[0] * (n + 1) for _ in range(T + 1)]
+    for j in range(T + 1):
+        for k in range(n + 1):
+            if j == 0:
+                f[j][k] = 1
+            elif k < 2 or j == 1:
+                f[j][k] = 0
+            elif k == 2:
+                f[j][k] = 1 if j % 2 == 0 else 0
+            else:
+                f[j][k] = sum(f[j - k + l][k - l] * math.comb(k - 1, l)
+                              for l in range(k - 1) if j - k + l >= 0)
+    return f
+
+
+def db_grid_rows(n: int, T: int) -> np.ndarray:
+    """The grid of sample_decision_boundary (eval_utils.py:31-61) as integer vectors v (eta = v/T),
+    in the construction's row order: for a (sum j, dim k) block, rows are grouped by the number l
+    of zero coordinates among 1..k-1, then by the lexicographic position set c of the non-zero
+    ones, then by the row order of the (sum j-k+l, dim k-l) sub-block plus one."""
+    memo = {}
+
+    def block(j, k):
+        key = (j, k)
+        if key in memo:
+            return memo[key]
+        if j == 0:
+            out = np.zeros((1, k), np.int64)
+        elif k < 2 or j == 1:
+            out = np.zeros((0, k), np.int64)
+        elif k == 2:
+            out = np.array([[j // 2, j // 2]], np.int64) if j % 2 == 0 else np.zeros((0, 2), np.int64)
+        else:
+            parts = []
+            for l in range(k - 1):
+                if j - k + l < 0:
+                    continue
+                sub = block(j - k + l, k - l) + 1
+                for c in __import__("itertools").combinations(range(1, k), k - l - 1):
+                    rows = np.zeros((sub.shape[0], k), np.int64)
+                    rows[:, [0] + list(c)] = sub
+                    parts.append(rows)
+            out = np.concatenate(parts) if parts else np.zeros((0, k), np.int64)
+        memo[key] = out
+        return out
+
+    return block(T, n)
+
+
+def db_unrank(r: int, n: int, T: int, f: List[List[int]]) -> List[int]:
+    """Row r of db_grid_rows(n, T) without materialising the grid (what the device kernel does)."""
+    out = [0] * n
+    idx = list(range(n))
+    add, j, k = 0, T, n
+    while True:
+        if j == 0:
+            for p in idx:
+                out[p] = add
+            return out
+        if k == 2:
+            out[idx[0]] = out[idx[1]] = add + j // 2
+            return out
+        for l in range(k - 1):
+            if j - k + l < 0:
+                continue
+            sub = f[j - k + l][k - l]
+            blk = math.comb(k - 1, k - l - 1) * sub
+            if r < blk:
+                break
+            r -= blk
+        m = k - l - 1
+        ci, r = divmod(r, sub)
+        c, e = [], 1
+        while len(c) < m:                      # lexicographic combination unranking over 1..k-1
+            cnt = math.comb(k - 1 - e, m - len(c) - 1)
+            if ci < cnt:
+                c.append(e)
+            else:
+                ci -= cnt
+            e += 1
+        keep = [0] + c
+        for p in range(k):
+            if p not in keep:
+                out[idx[p]] = add
+        idx = [idx[p] for p in keep]
+        add, j, k = add + 1, j - k + l, k - l
+
+
+def db_grid_for_label(grid_v: np.ndarray, label: int, T: int) -> np.ndarray:
+    """get_grid_for_label (eval_utils.py:64-69): swap columns 0 and label; eta = v / T as float32."""
+    g = np.asarray(grid_v, np.float64) / T
+    if label != 0:
+        g[:, [label, 0]] = g[:, [0, label]]
+    return g.astype(F32)
+
+
+@dataclass
+class CertifyConst:
+    T: int = 40
+    n: int = 10
+    eps_cfg: float = 0.141          # cfg.eps (CertifyExpCfg, ExpConfig.py:353)
+    min_std: float = 0.225          # min(param_map[0].std)
+    batches: int = 10
+
+    def kappa(self, cfg: DynConfig) -> float:
+        lfx = (cfg.alpha_1 if cfg.scale_nominal else 1.0) / self.min_std   # certify_lipschitz.py:67-70
+        return math.sqrt(2) * lfx * self.eps_cfg                              # :72
+
+
+def certify_batches(G: int, batches: int) -> List[Tuple[int, int]]:
+    """certify_lipschitz.py:100-102, 115-119: ebs = G // batches, +1 batch when G % batches != 0,
+    the last batch takes the tail."""
+    ebs = G // batches
+    nb = batches + (1 if G % batches != 0 else 0)
+    out = []
+    for b in range(nb):
+        if (b + 1) * ebs < G:
+            out.append((b * ebs, (b + 1) * ebs))
+        else:
+            out.append((b * ebs, G))
+    return out
+
+
+def certify_image(x_feat: np.ndarray, label: int, grid_v: np.ndarray, P: DynParams, cfg: DynConfig,
+                  cc: CertifyConst) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-batch max violation and max violation_larger_T for one image (certify_lipschitz.py:104-136).
+    The QP's global exit runs over each batch's rows, as eval_dot_light sees them."""
+    eta_all = db_grid_for_label(grid_v, label, cc.T)
+    u = static_projection(np.asarray(x_feat, F32).reshape(1, -1), P)
+    eps_g = F32(1.0 / cc.T)
+    dist = F32(math.sqrt(cc.n) / cc.T)
+    kappa = F32(cc.kappa(cfg))
+    vmax, vtmax = [], []
+    for lo, hi in certify_batches(len(eta_all), cc.batches):
+        eta = eta_all[lo:hi]
+        if len(eta) == 0:
+            continue
+        ev = eval_dot(eta, np.repeat(u, len(eta), 0), P, cfg)
+        f = ev.f
+        ub = (eta.max(1) + eps_g).astype(F32)
+        lf = ((F32(math.sqrt(cc.n)) * (F32(cfg.sigma_1 * cfg.alpha_1) * np.exp(F32(cfg.sigma_1) * ub).astype(F32)))
+              .astype(F32) + F32(1)).astype(F32)
+        perturb = ((F32(math.sqrt(2)) * lf).astype(F32) * dist).astype(F32)
+        mx = eta.max(1, keepdims=True)
+        wrong = eta == mx
+        wrong[:, label] = False
+        fw = np.where(wrong, f, -np.inf).max(1).astype(F32)
+        hv = ((-f[:, label]).astype(F32) + fw).astype(F32)
+        vmax.append(float(((hv + perturb).astype(F32) + kappa).astype(F32).max()))
+        vtmax.append(float((hv + kappa).astype(F32).max()))
+    return np.array(vmax, np.float32), np.array(vtmax, np.float32)

@@ -1,0 +1,79 @@
+"""GPU parity of the certification path (fiode_certify_grid / fiode_certify) against the oracle
+(grid construction order, per-batch max violations with the per-batch QP exit).
+
+Tolerance on the per-batch maxima: 2e-3 absolute (the max over rows of a QP output; a row whose
+batch exit iteration differs by one bisection step between the MFMA and the float64 oracle MLP
+moves f by at most the bracket / 2^K)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fiode_oracle as O
+from tests._util import make_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("T", [4, 8, 12])
+def test_grid_matches_construction_order(T):
+    from fiode_amd import ops
+    dev = _dev()
+    g = ops.certify_grid(T, device=dev).cpu().numpy()
+    ref = O.db_grid_rows(10, T)
+    assert g.shape == ref.shape
+    assert np.array_equal(g.astype(np.int64), ref)
+
+
+def test_grid_T40_count_and_rows():
+    from fiode_amd import ops
+    dev = _dev()
+    g = ops.certify_grid(40, device=dev)
+    assert tuple(g.shape) == (41_320_837, 10)
+    f = O.db_count_table(10, 40)
+    rng = np.random.default_rng(0)
+    rows = np.concatenate([[0, 1, 41_320_836], rng.integers(0, 41_320_837, 200)])
+    gs = g[torch.from_numpy(rows).to(dev)].cpu().numpy()
+    for r, v in zip(rows, gs):
+        assert O.db_unrank(int(r), 10, 40, f) == v.tolist()
+    s = g.to(torch.int32).sum(1)
+    assert int(s.min()) == 40 and int(s.max()) == 40
+    assert bool((g[:, 0].to(torch.int32) == g[:, 1:].to(torch.int32).max(1).values).all())
+
+
+@pytest.mark.parametrize("T,label,scale_nominal", [(8, 0, False), (12, 3, False), (12, 7, True)])
+def test_certify_image_matches_oracle(T, label, scale_nominal):
+    from fiode_amd import ops
+    dev = _dev()
+    P = make_params(seed=40 + T)
+    x = np.random.default_rng(T).normal(size=10).astype(np.float32)
+    grid_v = O.db_grid_rows(10, T)
+    cfg = O.DynConfig(scale_nominal=scale_nominal)
+    cc = O.CertifyConst(T=T, batches=10)
+    vmax, vtmax = O.certify_image(x, label, grid_v, P, cfg, cc)
+    w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
+    grid = ops.certify_grid(T, device=dev)
+    out, it = ops.certify_image(torch.from_numpy(x).to(dev), label, grid, w,
+                                ops.DynCfg(scale_nominal=scale_nominal, dropout=0.0), T=T, batches=10)
+    o = out.cpu().numpy()
+    assert o.shape == (len(vmax), 2)
+    err = float(np.abs(o[:, 0] - vmax).max()), float(np.abs(o[:, 1] - vtmax).max())
+    assert max(err) <= 2e-3, err
+
+
+def test_certify_driver_through_module():
+    """certify_lipschitz over a few synthetic images with the bench module (T=12 grid)."""
+    import bench
+    from fiode_amd.certify import certify_lipschitz
+    dev = _dev()
+    mod = bench.build_module(dev)
+    x = torch.rand(3, 3, 32, 32, device=dev)
+    y = torch.tensor([1, 4, 9], device=dev)
+    res = certify_lipschitz(mod, x, y, T=12, batches=10)
+    assert res.n_images == 3 and len(res.max_violations) == 3
+    assert all(np.isfinite(res.max_violations))

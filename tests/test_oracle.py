@@ -244,3 +244,28 @@ def test_dopri5_on_dynamics_matches_fine_reference():
     yf, _ = O.rk4_fixed_grid(func, h0, 0.0, 1.0, 0.002)
     assert np.allclose(y.sum(1), 1.0, atol=1e-3)
     assert np.abs(y - yf).max() < 2e-2
+
+
+# -- certification grid (eval_utils.py:31-89) -------------------------------------------------------
+
+def test_grid_count_G_10_40():
+    assert O.db_count_table(10, 40)[40][10] == 41_320_837
+
+
+@pytest.mark.parametrize("n,T", [(3, 6), (4, 8), (5, 10), (10, 4)])
+def test_grid_order_and_unrank(n, T):
+    import itertools
+    g = O.db_grid_rows(n, T)
+    f = O.db_count_table(n, T)
+    assert g.shape[0] == f[T][n]
+    brute = {v for v in itertools.product(range(T + 1), repeat=n) if sum(v) == T and v[0] == max(v[1:])}
+    assert set(map(tuple, g.tolist())) == brute
+    assert len(brute) == g.shape[0]                 # no duplicates
+    for r in range(g.shape[0]):
+        assert O.db_unrank(r, n, T, f) == g[r].tolist()
+
+
+def test_certify_batches_rule():
+    assert O.certify_batches(41_320_837, 10)[-1] == (41_320_830, 41_320_837)
+    assert len(O.certify_batches(41_320_837, 10)) == 11
+    assert O.certify_batches(20, 10) == [(2 * i, 2 * i + 2) for i in range(10)]
