@@ -190,3 +190,23 @@ def test_dyn_eval_matches_oracle(scale_nominal):
     assert abs(int(it.item()) - ref.qp.iters) <= 1
     err = float(np.abs(f.cpu().numpy() - ref.f).max())
     assert err <= 1e-3, err
+
+
+def test_barrier_projection_function_autograd():
+    """FastBarrierProjectionNoUpper drop-in: forward bit-exact, backward = oracle closed form."""
+    dev = _dev()
+    from fiode_amd.barrier_projection import FastBarrierProjectionNoUpper
+    rng = np.random.default_rng(11)
+    h = O.uniform_simplex(rng.exponential(1, (700, 10)).astype(np.float32))
+    lower = O.barrier_lower(h, O.DynConfig())
+    nominal = rng.normal(0, 20, (700, 10)).astype(np.float32)
+    proj = FastBarrierProjectionNoUpper(max_iter=30, tol=1e-4)
+    lt = torch.from_numpy(lower).to(dev).requires_grad_(True)
+    nt = torch.from_numpy(nominal).to(dev).requires_grad_(True)
+    v = proj(lt, nt)
+    g = rng.normal(size=(700, 10)).astype(np.float32)
+    v.backward(torch.from_numpy(g).to(dev))
+    r = O.qp_forward(lower, nominal)
+    assert np.array_equal(v.detach().cpu().numpy(), r.v)
+    gl, gn = O.qp_backward(g, r.v, r.mu, lower, nominal)
+    assert np.array_equal(nt.grad.cpu().numpy(), gn) and np.array_equal(lt.grad.cpu().numpy(), gl)
