@@ -138,24 +138,20 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
     x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
-    metrics = torch.zeros(4, device=dev)
+    from fiode_amd.distributed import GradAllReducer, MetricReducer, broadcast_parameters
+    broadcast_parameters(mod)                   # DDP's construction-time broadcast
+    reducer = GradAllReducer(params)            # p.grad are views into one flat bucket
+    metrics = MetricReducer(["training_loss", "effective_batch_size", "mean_active_constraints"], dev)
 
     def step():
         opt.zero_grad(set_to_none=False)
         loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
         loss.backward()
         if world > 1:
-            flat = torch.cat([p.grad.reshape(-1) for p in params])
-            dist.all_reduce(flat)                 # one RCCL all-reduce of the whole gradient
-            flat /= world
-            o = 0
-            for p in params:
-                n = p.numel()
-                p.grad.copy_(flat[o:o + n].view_as(p))
-                o += n
+            reducer.allreduce(world)              # one RCCL all-reduce of the whole gradient
             sc = mod.last_plan["scalars"]
-            metrics[0] = sc[0]; metrics[1] = sc[1]; metrics[2] = sc[2]; metrics[3] = 1.0
-            dist.all_reduce(metrics)              # fused sync_dist of the logged scalars
+            metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
+                            "mean_active_constraints": sc[2]}, world)   # fused sync_dist
         opt.step()
         mod.global_step += 1
 
