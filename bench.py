@@ -121,6 +121,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--prof-reps", type=int, default=20)
+    ap.add_argument("--eager", action="store_true", help="dispatch the step op by op (no hipGraph replay)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,7 +134,7 @@ def main():
 
     mod = build_module(dev, seed=0)
     mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
-    opt = mod.configure_optimizers()[0][0]
+    opt = mod.configure_optimizers(capturable=not args.eager)[0][0]
     params = [p for p in mod.parameters() if p.requires_grad]
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
     x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
@@ -143,17 +144,29 @@ def main():
     reducer = GradAllReducer(params)            # p.grad are views into one flat bucket
     metrics = MetricReducer(["training_loss", "effective_batch_size", "mean_active_constraints"], dev)
 
-    def step():
-        opt.zero_grad(set_to_none=False)
-        loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
-        loss.backward()
-        if world > 1:
-            reducer.allreduce(world)              # one RCCL all-reduce of the whole gradient
-            sc = mod.last_plan["scalars"]
-            metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
-                            "mean_active_constraints": sc[2]}, world)   # fused sync_dist
-        opt.step()
-        mod.global_step += 1
+    def sync_metrics():
+        sc = mod.last_plan["scalars"]
+        metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
+                        "mean_active_constraints": sc[2]}, world)   # fused sync_dist
+
+    if args.eager:
+        def step():
+            opt.zero_grad(set_to_none=False)
+            loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
+            loss.backward()
+            if world > 1:
+                reducer.allreduce(world)              # one RCCL all-reduce of the whole gradient
+                sync_metrics()
+            opt.step()
+            mod.global_step += 1
+    else:
+        from fiode_amd.graph_step import GraphTrainStep
+        gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world)
+
+        def step():
+            gstep.step()                              # hipGraph replay (+ eager RCCL between graphs)
+            if world > 1:
+                sync_metrics()
 
     for _ in range(args.warmup):
         step()
@@ -203,7 +216,7 @@ def main():
     out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic (x~U[0,1) 128x3x32x32 per rank, y~randint(10))",
-           "config": {"workload": "Lyapunov train step of README.md:27 at epoch 20 (configs[1] shape: B=128, "
+           "config": {"workload": ("hipGraph replay" if not args.eager else "eager") + ": Lyapunov train step of README.md:27 at epoch 20 (configs[1] shape: B=128, "
                                   "h_sample_size=256 -> 204 uniform + 52 correct-cone rows/image), KWLarge-Cayley "
                                   "backbone + fused HIP fan-out + Adam",
                       "global_batch": world * B_PER_RANK, "h_sample_size": H_SAMPLE,

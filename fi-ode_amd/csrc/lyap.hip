@@ -42,6 +42,7 @@ struct LyapArgs {
   uint32_t thr8;
   float drop_scale;
   Rng rng;
+  const uint64_t* offset_dev;   // optional device-resident addend of the Philox offset
   DynScalars d;
   float kappa, invN;
   int parts, chunk;
@@ -181,6 +182,11 @@ __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
 __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= a.N) return;
+  if (a.offset_dev) {            // graph replay: the step counter lives in device memory
+    const uint64_t o = (((uint64_t)a.rng.off_hi << 32) | a.rng.off_lo) + *a.offset_dev;
+    a.rng.off_lo = (uint32_t)o;
+    a.rng.off_hi = (uint32_t)(o >> 32);
+  }
   if (a.sampler != FIODE_SAMPLER_GIVEN || a.h_out) {
     const int label = (int)a.y[row / a.S];
     float h[C];
@@ -600,6 +606,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.drop_scale = (a.dropout_mode == FIODE_DROPOUT_OFF) ? 1.0f : 1.0f / (1.0f - p);
   a.rng.key = make_uint2((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32));
   a.rng.off_lo = (uint32_t)cfg->offset; a.rng.off_hi = (uint32_t)(cfg->offset >> 32);
+  a.offset_dev = io->offset_dev;
   a.d.alpha_1 = dyn->alpha_1; a.d.alpha_2 = dyn->alpha_2; a.d.sigma_1 = dyn->sigma_1;
   a.d.tol = dyn->qp_tol; a.d.scale_nominal = dyn->scale_nominal; a.d.max_iter = dyn->qp_max_iter;
   a.kappa = cfg->kappa;

@@ -47,7 +47,7 @@ class LyapConfig(ct.Structure):
 class LyapIO(ct.Structure):
     _fields_ = [(n, ct.c_void_p) for n in ("x_feat", "y", "h", "masks", "scalars", "h_out", "V", "Vdot",
                                            "f", "f_log", "qp_lower", "qp_nominal", "g_ftilde", "events")] + \
-        [("n_events", ct.c_int32)]
+        [("n_events", ct.c_int32), ("offset_dev", ct.c_void_p)]
 
 
 LYAP_KERNELS = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_wgrad", "k_lyap_reduce",
@@ -59,6 +59,8 @@ class LyapGrads(ct.Structure):
 
 
 FIODE_ODE_RK4, FIODE_ODE_DOPRI5 = 0, 1
+FIODE_DTYPE_F32, FIODE_DTYPE_C64 = 0, 1
+FIODE_INV_MAX_N = 128
 FIODE_ODE_MAX_BATCH = 4096
 
 
@@ -99,6 +101,8 @@ def _load():
         "fiode_certify_workspace_bytes": (ct.c_size_t, [ct.c_int64, ct.c_int32]),
         "fiode_certify": (ct.c_int, [_vp, ct.POINTER(CertifyConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
                                      _vp, _vp, ct.c_int64, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,
+                                             ct.c_int64]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

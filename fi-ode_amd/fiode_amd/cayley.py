@@ -19,9 +19,52 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+_BLOCK = 128
+
+
+def _block_inverse(M: torch.Tensor) -> torch.Tensor:
+    """Inverse of (..., n, n) on the device: the HIP Gauss-Jordan kernel for n <= 128, else
+    block Gauss-Jordan in natural order over 128-wide panels (pivot blocks inverted by the
+    kernel, the rank-128 updates as batched GEMMs).  Valid for positive-real matrices (every
+    Schur complement of one is positive-real), which all Cayley systems I + A are."""
+    from . import ops
+    n = M.shape[-1]
+    if n <= _BLOCK:
+        return ops.batched_inverse(M)
+    X = M.clone()
+    for k0 in range(0, n, _BLOCK):
+        K = slice(k0, min(n, k0 + _BLOCK))
+        P = ops.batched_inverse(X[..., K, K])
+        R = P @ X[..., K, :]                     # pivot block row, scaled
+        Cm = X[..., :, K].clone()                # pivot block column (old)
+        X -= Cm @ R
+        X[..., K, :] = R
+        X[..., :, K] = -(Cm @ P)
+        X[..., K, K] = P
+    return X
+
+
+class _CayleyInverse(torch.autograd.Function):
+    """(I + A)^-1 with torch.linalg.inv's gradient, d(M^-1) = -M^-H dM M^-H -- computed by the
+    fiode_batched_inverse kernel instead of getrf/getrs (no pivot search, no info sync)."""
+
+    @staticmethod
+    def forward(ctx, M):
+        inv = _block_inverse(M.contiguous())
+        ctx.save_for_backward(inv)
+        return inv
+
+    @staticmethod
+    def backward(ctx, g):
+        inv, = ctx.saved_tensors
+        ih = inv.mH
+        return -(ih @ g @ ih)
+
+
 def cayley(W: torch.Tensor) -> torch.Tensor:
     """Orthogonal (or orthonormal-column) matrix from an unconstrained W [.., cout, cin]:
-    with U = W[:cin], V = W[cin:], A = U - U^H + V^H V:  Q = [(I+A)^-1 (I-A); -2 V (I+A)^-1].
+    with U = W[:cin], V = W[cin:], A = U - U^H + V^H V:
+        Q = [(I+A)^-1 (I-A); -2 V (I+A)^-1] = [2 (I+A)^-1 - I; -2 V (I+A)^-1].
     Wide matrices (cin > cout) are handled through the transpose."""
     if W.dim() == 2:
         return cayley(W.unsqueeze(0)).squeeze(0)
@@ -29,11 +72,15 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
     if cin > cout:
         return cayley(W.transpose(-2, -1)).transpose(-2, -1)
     U, V = W[..., :cin, :], W[..., cin:, :]
-    eye = torch.eye(cin, dtype=W.dtype, device=W.device).expand(W.shape[:-2] + (cin, cin))
-    Uh = U.conj().transpose(-2, -1)
-    A = U - Uh + V.conj().transpose(-2, -1) @ V
-    inv = torch.linalg.inv(eye + A)
-    return torch.cat([inv @ (eye - A), -2.0 * (V @ inv)], dim=-2)
+    eye = torch.eye(cin, dtype=W.dtype, device=W.device)
+    A = U - U.mH
+    if cout > cin:
+        A = A + V.mH @ V
+    inv = _CayleyInverse.apply(eye + A)
+    top = 2.0 * inv - eye
+    if cout == cin:
+        return top
+    return torch.cat([top, -2.0 * (V @ inv)], dim=-2)
 
 
 class CayleyLinear(nn.Linear):
@@ -82,6 +129,10 @@ class CayleyConv(nn.Conv2d):
         self.alpha = nn.Parameter(torch.ones(1))
         self._alpha_init = False
         self._shift = {}
+
+    def _load_from_state_dict(self, *args, **kw):
+        super()._load_from_state_dict(*args, **kw)
+        self._alpha_init = True          # a loaded alpha is kept (no data-dependent re-init)
 
     def _shift_matrix(self, n: int, device) -> torch.Tensor:
         key = (n, str(device))

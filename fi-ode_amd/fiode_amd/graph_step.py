@@ -1,0 +1,100 @@
+"""The training step as replayable hipGraphs (torch.cuda.CUDAGraph = hipGraph on ROCm).
+
+One eager step of the README model launches ~1,000 kernels from Python (backbone FFT convs,
+Cayley maps, autograd, Adam); at B=128 the GPU work is a few ms, so the eager step is bound by
+host dispatch.  The whole step has no host synchronisation (the fused fan-out, the QP exit and
+the Cayley inverses are all device-side), so it is captured once and replayed:
+
+* ``fwd_bwd`` graph: zero grads -> compute_loss (backbone, Cayley maps, fused fan-out kernels)
+  -> backward, accumulating into the persistent ``p.grad`` tensors (with a GradAllReducer these
+  are views into its flat bucket) -> advance the device Philox counter, so every replay draws
+  fresh samples and dropout masks;
+* ``opt`` graph: the Adam step (``capturable=True``: step counts on the device).
+For one rank both are captured into a single graph; for N ranks the RCCL gradient all-reduce
+and the metric reduce run eagerly between the two replays.
+
+Static inputs: ``step(x, y)`` copies the batch into the captured input buffers.  What the
+captured step bakes in (and ``GraphTrainStep`` checks on every call): the sampler plan of the
+current epoch (S1/S2 split, ``scale_nominal``), kappa (needs ``global_step >= kappa_length``),
+batch shape.  Recapture (construct a new GraphTrainStep) at an epoch boundary.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+class GraphTrainStep:
+    def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
+                 warmup: int = 3, act: str = "relu"):
+        dev = x.device
+        if dev.type != "cuda":
+            raise ValueError("GraphTrainStep needs ROCm device tensors")
+        self.module, self.opt, self.reducer, self.world, self.act = module, optimizer, reducer, world, act
+        dyn = module.dyn_fun
+        if module.global_step < dyn.kappa_length:
+            raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
+        self.epoch = module.current_epoch
+        self.static_x = x.detach().clone()
+        self.static_y = y.detach().clone()
+        if module.rng_counter is None:
+            module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        for p in self.params:            # persistent grads: autograd accumulates into them in place
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self._grad_ptrs = [p.grad.data_ptr() for p in self.params]
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._fwd_bwd()
+                self._between()
+                self.opt.step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+
+        self.single = world == 1
+        self.g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fb):
+            self.loss = self._fwd_bwd()
+            if self.single:
+                self.opt.step()
+        self.g_opt = None
+        if not self.single:
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt):
+                self.opt.step()
+        if [p.grad.data_ptr() for p in self.params] != self._grad_ptrs:
+            raise RuntimeError("autograd re-allocated .grad during capture; cannot replay into the bucket")
+        self.scalars = module.last_plan["scalars"]
+
+    def _fwd_bwd(self):
+        m = self.module
+        for p in self.params:
+            p.grad.zero_()
+        loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
+        loss.backward()
+        m.rng_counter.add_(1)
+        return loss
+
+    def _between(self):
+        if self.reducer is not None and self.world > 1:
+            self.reducer.allreduce(self.world)
+
+    def step(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None):
+        m = self.module
+        if m.current_epoch != self.epoch:
+            raise RuntimeError("epoch changed: the captured sampler plan is stale, recapture the step")
+        if x is not None:
+            self.static_x.copy_(x, non_blocking=True)
+        if y is not None:
+            self.static_y.copy_(y, non_blocking=True)
+        self.g_fb.replay()
+        if not self.single:
+            self._between()
+            self.g_opt.replay()
+        m.global_step += 1
+        return self.loss

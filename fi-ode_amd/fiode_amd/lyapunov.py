@@ -37,7 +37,7 @@ class LyapunovLossFn(torch.autograd.Function):
             x_feat.detach().contiguous(), y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"],
             sampler=plan["sampler"], dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"],
             offset=plan["offset"], h=plan.get("h"), masks=plan.get("masks"), debug=plan.get("debug", False),
-            out=plan.get("out"))
+            out=plan.get("out"), offset_dev=plan.get("offset_dev"))
         plan["scalars"] = sc
         plan["debug_out"] = dbg
         g = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
@@ -121,6 +121,7 @@ class LyapunovLearning(nn.Module):
         self.global_step = 0
         self.seed = seed
         self._rng_offset = 0
+        self.rng_counter: Optional[torch.Tensor] = None   # device step counter (graph replay)
         self.logged: Dict[str, float] = {}
         self._out = None
 
@@ -164,15 +165,20 @@ class LyapunovLearning(nn.Module):
     def log(self, name, value, **kw):
         self.logged[name] = value
 
-    def configure_optimizers(self):
-        """pl_modules.py:97-147 (Adam/AdamW/SGD; cosine or step schedule; warm-up Adam)."""
+    def configure_optimizers(self, capturable: bool = False):
+        """pl_modules.py:97-147 (Adam/AdamW/SGD; cosine or step schedule; warm-up Adam).
+        ``capturable``: Adam/AdamW keep their step counts on the device so the optimizer step
+        can be captured in a hipGraph (fiode_amd.graph_step)."""
         params = self.parameters()
         if self.current_epoch < self.warmup:
-            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas)]
+            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas,
+                                     capturable=capturable)]
         if self.opt_name == "Adam":
-            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas)
+            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas,
+                                   capturable=capturable)
         elif self.opt_name == "AdamW":
-            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas)
+            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas,
+                                    capturable=capturable)
         elif self.opt_name == "SGD":
             opt = torch.optim.SGD(params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
         else:
@@ -211,8 +217,9 @@ class LyapunovLearning(nn.Module):
         if h is not None:
             kind = L.FIODE_SAMPLER_GIVEN
         plan = dict(dyn=self.dyn_fun.dyn_cfg(), S=self.h_sample_size, S1=s1, sampler=kind, dropout_mode=drop,
-                    kappa=self.current_kappa(), seed=self.seed, offset=self._rng_offset, h=h, masks=masks,
-                    debug=debug, out=None)
+                    kappa=self.current_kappa(), seed=self.seed,
+                    offset=self._rng_offset if self.rng_counter is None else 0, h=h, masks=masks,
+                    debug=debug, out=None, offset_dev=self.rng_counter)
         self._rng_offset += 1
         return plan
 

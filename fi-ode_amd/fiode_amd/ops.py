@@ -79,10 +79,12 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
               sample_size: int, n_uniform: int, sampler: int = L.FIODE_SAMPLER_COMPOSITE,
               dropout_mode: int = L.FIODE_DROPOUT_PHILOX, kappa: float = 2.0, seed: int = 0, offset: int = 0,
               h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None, debug: bool = False,
-              out: Optional[dict] = None, events=None):
+              out: Optional[dict] = None, events=None, offset_dev: Optional[torch.Tensor] = None):
     """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict).
     ``events``: optional list of len(_lib.LYAP_KERNELS)+1 torch.cuda.Event(enable_timing=True),
-    recorded by the library around each of its kernels on the current stream."""
+    recorded by the library around each of its kernels on the current stream.
+    ``offset_dev``: optional int64 [1] device tensor added to ``offset`` by the kernels (a captured
+    graph of the step advances it on every replay)."""
     dev = x_feat.device
     B = x_feat.shape[0]
     S = int(sample_size)
@@ -99,6 +101,8 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
         if masks is None:
             raise ValueError("dropout GIVEN needs masks")
         masks = _need(masks, "masks", (4, N, M), torch.uint8, dev)
+    if offset_dev is not None:
+        offset_dev = _need(offset_dev, "offset_dev", (1,), torch.int64, dev)
     ws_w, cw = _weights_c(weights, dev)
     if out is None:
         out = {}
@@ -133,7 +137,8 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
     io = L.LyapIO(x_feat.data_ptr(), y.data_ptr(), _ptr(h), _ptr(masks), scalars.data_ptr(),
                   _ptr(dbg.get("h")), _ptr(dbg.get("V")), _ptr(dbg.get("Vdot")), _ptr(dbg.get("f")),
                   _ptr(dbg.get("f_log")), _ptr(dbg.get("qp_lower")), _ptr(dbg.get("qp_nominal")),
-                  _ptr(dbg.get("g_ftilde")), ct.cast(ev_arr, ct.c_void_p) if ev_arr is not None else None, n_ev)
+                  _ptr(dbg.get("g_ftilde")), ct.cast(ev_arr, ct.c_void_p) if ev_arr is not None else None, n_ev,
+                  _ptr(offset_dev))
     cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
     lib = L.lib()
     nbytes = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dc))
@@ -269,3 +274,23 @@ def certify_image(x_feat: torch.Tensor, label: int, grid: torch.Tensor, weights:
     L.check(rc, "fiode_certify")
     del ws_w
     return out, it
+
+
+def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(..., n, n) -> inverse, n <= 128, float32 or complex64 (fiode_batched_inverse).
+    Valid for matrices with positive-definite Hermitian part (the Cayley I + A)."""
+    if M.device.type != "cuda":
+        raise ValueError(f"batched_inverse: must be on a ROCm device; got {M.device}")
+    if M.dtype not in (torch.float32, torch.complex64):
+        raise TypeError(f"batched_inverse: dtype {M.dtype} (float32 / complex64 only)")
+    n = M.shape[-1]
+    if M.dim() < 2 or M.shape[-2] != n or n > L.FIODE_INV_MAX_N:
+        raise ValueError(f"batched_inverse: shape {tuple(M.shape)} (square, n <= {L.FIODE_INV_MAX_N})")
+    M = M.contiguous()
+    if out is None:
+        out = torch.empty_like(M)
+    batch = M.numel() // (n * n)
+    dt = L.FIODE_DTYPE_F32 if M.dtype == torch.float32 else L.FIODE_DTYPE_C64
+    L.check(L.lib().fiode_batched_inverse(_stream(M.device), dt, batch, n, M.data_ptr(), n * n, out.data_ptr(),
+                                          n * n), "fiode_batched_inverse")
+    return out

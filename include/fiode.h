@@ -96,6 +96,10 @@ typedef struct fiode_lyap_io {
    * after each of the FIODE_LYAP_NKERNELS kernels (needs n_events >= FIODE_LYAP_NKERNELS + 1) */
   void* const* events;
   int32_t n_events;
+  /* optional device-resident Philox offset addend (NULL = 0): offset = cfg.offset + *offset_dev,
+   * so a captured hipGraph of the step draws fresh samples / dropout masks on every replay when
+   * the graph also advances the counter */
+  const uint64_t* offset_dev;
 } fiode_lyap_io;
 
 /* kernels of one fiode_lyap_step, in launch order (for the profiling events) */
@@ -188,6 +192,17 @@ FIODE_API size_t fiode_certify_workspace_bytes(int64_t G, int32_t batches);
 FIODE_API int fiode_certify(void* stream, const fiode_certify_config* cfg, const fiode_dyn_config* dyn,
                             const fiode_dyn_weights* w, const float* x_feat, const uint8_t* grid, int64_t G,
                             float* out, int32_t* exit_iters, void* workspace, size_t workspace_bytes);
+
+/* ---- Batched inverse of the Cayley maps (classification.py:282-293 convert_cayley ->
+ * cayley(): (I + A)^-1 with A = U - U^H + V^H V; replaces torch.inverse / torch.linalg.inv) ---- */
+#define FIODE_DTYPE_F32 0
+#define FIODE_DTYPE_C64 1   /* complex64, interleaved (re, im) */
+#define FIODE_INV_MAX_N 128
+/* out[b] = in[b]^-1 for b < batch, n x n row-major matrices at element strides in_stride /
+ * out_stride (in == out allowed).  Gauss-Jordan in natural pivot order: valid for matrices whose
+ * Hermitian part is positive definite (every I + A above); no pivoting, no host sync. */
+FIODE_API int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch, int32_t n, const void* in,
+                                    int64_t in_stride, void* out, int64_t out_stride);
 
 /* Error text for a return code. */
 FIODE_API const char* fiode_error_string(int code);

@@ -50,3 +50,15 @@ def test_bad_shapes_rejected_before_launch():
     assert lib.fiode_qp_forward(None, 5, 11, None, None, 30, 1e-4, None, None, None, None, 0) == 2
     dyn = _lib.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 40, 1e-4)     # qp_max_iter > 32
     assert lib.fiode_lyap_step(None, ct.byref(cfg), ct.byref(dyn), None, None, None, None, 0) == 1
+
+
+def test_batched_inverse_argument_checks():
+    """fiode_batched_inverse validates before launching: n <= 128, known dtype, strides >= n*n;
+    an empty batch is a no-op."""
+    from fiode_amd import _lib
+    lib = _lib.lib()
+    assert lib.fiode_batched_inverse(None, 0, 0, 4, None, 16, None, 16) == 0
+    assert lib.fiode_batched_inverse(None, 0, 1, 129, None, 0, None, 0) == 1
+    assert lib.fiode_batched_inverse(None, 7, 1, 4, None, 16, None, 16) == 1
+    buf = ct.create_string_buffer(64)
+    assert lib.fiode_batched_inverse(None, 0, 1, 4, buf, 15, buf, 16) == 2

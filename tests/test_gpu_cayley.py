@@ -1,0 +1,110 @@
+"""GPU tests of the Cayley inverse (fiode_batched_inverse + block Gauss-Jordan) against
+torch.linalg.inv in float64 on the same positive-real systems I + A, A = U - U^H + V^H V.
+
+Tolerance: max |inv - inv64| <= 2e-5 * n^0.5 (||inv||_2 <= 1 for these systems, so absolute
+error is the meaningful scale; fp32 Gauss-Jordan error grows ~ sqrt(n) eps ||M||)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _system(batch, n, dtype, dev, scale=1.0, tall=16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    W = torch.randn(batch, n + tall, n, generator=g, dtype=torch.float64 if dtype == torch.float32 else torch.complex128)
+    W = W * scale / (n ** 0.5)
+    U, V = W[:, :n], W[:, n:]
+    M = torch.eye(n, dtype=W.dtype) + U - U.mH + V.mH @ V
+    return M.to(dev)
+
+
+@pytest.mark.parametrize("n", [1, 3, 10, 16, 17, 32, 64, 100, 128])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.complex64])
+def test_batched_inverse_matches_float64(n, dtype):
+    from fiode_amd import ops
+    dev = _dev()
+    M64 = _system(7, n, dtype, dev, scale=3.0, seed=n)
+    ref = torch.linalg.inv(M64)
+    inv = ops.batched_inverse(M64.to(dtype))
+    err = float((inv.to(ref.dtype) - ref).abs().max())
+    assert err <= 2e-5 * n ** 0.5, err
+
+
+@pytest.mark.parametrize("n", [200, 512])
+def test_block_inverse_large(n):
+    from fiode_amd.cayley import _block_inverse
+    dev = _dev()
+    M64 = _system(2, n, torch.float32, dev, scale=2.0, seed=n)
+    ref = torch.linalg.inv(M64)
+    inv = _block_inverse(M64.float())
+    err = float((inv.double() - ref).abs().max())
+    assert err <= 2e-5 * n ** 0.5, err
+
+
+def test_inverse_in_place_and_strided_batch():
+    from fiode_amd import ops
+    dev = _dev()
+    M = _system(5, 24, torch.float32, dev, seed=3).float()
+    ref = torch.linalg.inv(M.double())
+    out = M.clone()
+    ops.batched_inverse(out, out=out)
+    assert float((out.double() - ref).abs().max()) < 2e-4
+
+
+@pytest.mark.parametrize("shape", [(32, 3), (512, 4096), (512, 512), (10, 512), (128, 10), (128, 128)])
+def test_cayley_orthogonal(shape):
+    from fiode_amd.cayley import cayley
+    dev = _dev()
+    W = torch.randn(*shape, device=dev)
+    Q = cayley(W / W.norm() * 3.0)
+    if shape[0] >= shape[1]:
+        G = Q.T @ Q
+    else:
+        G = Q @ Q.T
+    err = float((G - torch.eye(G.shape[0], device=dev)).abs().max())
+    assert err < 5e-5, err
+
+
+def test_cayley_complex_batch_orthogonal():
+    from fiode_amd.cayley import cayley
+    dev = _dev()
+    W = torch.randn(144, 32, 128, dtype=torch.complex64, device=dev)
+    Q = cayley(W * 0.2)                 # wide: through the transpose
+    G = Q @ Q.mH
+    err = float((G - torch.eye(32, device=dev)).abs().max())
+    assert err < 5e-5, err
+
+
+@pytest.mark.parametrize("dtype,n", [(torch.float32, 20), (torch.float32, 300), (torch.complex64, 24)])
+def test_cayley_inverse_gradient_matches_linalg_inv(dtype, n):
+    from fiode_amd.cayley import _CayleyInverse
+    dev = _dev()
+    M = _system(3, n, dtype, dev, scale=1.5, seed=11).to(dtype)
+    G = torch.randn(M.shape, dtype=dtype, device=dev)
+    a = M.clone().requires_grad_(True)
+    (_CayleyInverse.apply(a) * G.conj()).real.sum().backward() if dtype.is_complex else \
+        (_CayleyInverse.apply(a) * G).sum().backward()
+    b = M.clone().double() if not dtype.is_complex else M.clone().to(torch.complex128)
+    b.requires_grad_(True)
+    Gb = G.to(b.dtype)
+    (torch.linalg.inv(b) * Gb.conj()).real.sum().backward() if dtype.is_complex else \
+        (torch.linalg.inv(b) * Gb).sum().backward()
+    err = float((a.grad.to(b.dtype) - b.grad).abs().max())
+    assert err < 1e-4 * n ** 0.5, err
+
+
+def test_inverse_rejects_bad_inputs():
+    from fiode_amd import ops
+    dev = _dev()
+    with pytest.raises(ValueError):
+        ops.batched_inverse(torch.eye(129, device=dev))
+    with pytest.raises(TypeError):
+        ops.batched_inverse(torch.eye(4, device=dev, dtype=torch.float64))
+    with pytest.raises(ValueError):
+        ops.batched_inverse(torch.eye(4))
