@@ -39,6 +39,7 @@ METRIC = "CIFAR-10 train-step images/sec (B=128, h_sample=256) at 1/2/4/8 MI355X
 B_PER_RANK = 128
 H_SAMPLE = 256
 EPOCH = 20
+TRAIN_ODE_EPOCH = 10          # train_ode branch active at EPOCH (loss_ode portion 0.2)
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
 HBM_PEAK_GBS = 8000.0
 # algorithmic FLOP per (image, sample) row
@@ -48,7 +49,7 @@ FLOP_ROW = {"k_lyap_fwd": 2 * FLOP_ROW_FWD_PASS,                   # loss pass +
             "k_lyap_wgrad": FLOP_ROW_FWD_PASS}                     # weight grads dQ3, dQ2, dQ1
 
 
-def build_module(dev, seed=0):
+def build_module(dev, seed=0, train_ode=False):
     from fiode_amd.dynamics import OrthoClassDynProjectSimplexLips
     from fiode_amd.lyapunov import LyapunovLearning, UniformInitFun, DecisionBoundary
     from fiode_amd.models import make_ortho_KWLarge_Concat
@@ -66,7 +67,9 @@ def build_module(dev, seed=0):
     mod = LyapunovLearning(order=1, h_sample_size=H_SAMPLE, h_dist_lim=15.0, sampler=sampler,
                            sampler_scheduler=sched, dynamics=dyn, init_fun=UniformInitFun((10,), backbone),
                            lya_cand=DecisionBoundary(on_simplex=True), t_max=1.0, opt_name="Adam", lr=5e-3,
-                           train_ode_tol=1e-3, val_ode_solver="dopri5", val_ode_tol=1e-3,
+                           train_ode=train_ode, train_ode_epoch=TRAIN_ODE_EPOCH,
+                           train_ode_solver="rk4" if train_ode else "dopri5", train_ode_tol=0.1 if train_ode else 1e-3,
+                           val_ode_solver="dopri5", val_ode_tol=1e-3,
                            weight_decay=0.0, warmup=-1, max_epochs=300, simplex=True, act="relu", val_adv=False,
                            seed=seed)
     mod.current_epoch = EPOCH
@@ -122,6 +125,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--prof-reps", type=int, default=20)
     ap.add_argument("--eager", action="store_true", help="dispatch the step op by op (no hipGraph replay)")
+    ap.add_argument("--workload", choices=("rk4", "lyap"), default="rk4",
+                    help="rk4: BASELINE configs[1] (Lyapunov loss + differentiable RK4 train_ode solve); "
+                         "lyap: the Lyapunov-only step")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the Lyapunov-only companion measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,59 +139,69 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
-    mod = build_module(dev, seed=0)
-    mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
-    opt = mod.configure_optimizers(capturable=not args.eager)[0][0]
-    params = [p for p in mod.parameters() if p.requires_grad]
-    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
-    y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
-    from fiode_amd.distributed import GradAllReducer, MetricReducer, broadcast_parameters
-    broadcast_parameters(mod)                   # DDP's construction-time broadcast
-    reducer = GradAllReducer(params)            # p.grad are views into one flat bucket
-    metrics = MetricReducer(["training_loss", "effective_batch_size", "mean_active_constraints"], dev)
+    def timed_run(train_ode: bool, steps: int, warmup: int):
+        """Build the module, capture (or not) the step, run warmup + timed steps; max over ranks."""
+        mod = build_module(dev, seed=0, train_ode=train_ode)
+        mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
+        opt = mod.configure_optimizers(capturable=not args.eager)[0][0]
+        params = [p for p in mod.parameters() if p.requires_grad]
+        g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+        x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
+        from fiode_amd.distributed import GradAllReducer, MetricReducer, broadcast_parameters
+        broadcast_parameters(mod)                   # DDP's construction-time broadcast
+        reducer = GradAllReducer(params)            # p.grad are views into one flat bucket
+        metrics = MetricReducer(["training_loss", "effective_batch_size", "mean_active_constraints"], dev)
 
-    def sync_metrics():
-        sc = mod.last_plan["scalars"]
-        metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
-                        "mean_active_constraints": sc[2]}, world)   # fused sync_dist
+        def sync_metrics():
+            sc = mod.last_plan["scalars"]
+            metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
+                            "mean_active_constraints": sc[2]}, world)   # fused sync_dist
 
-    if args.eager:
-        def step():
-            opt.zero_grad(set_to_none=False)
-            loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
-            loss.backward()
-            if world > 1:
-                reducer.allreduce(world)              # one RCCL all-reduce of the whole gradient
-                sync_metrics()
-            opt.step()
-            mod.global_step += 1
-    else:
-        from fiode_amd.graph_step import GraphTrainStep
-        gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world)
+        if args.eager:
+            def step():
+                opt.zero_grad(set_to_none=False)
+                loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
+                loss.backward()
+                if world > 1:
+                    reducer.allreduce(world)          # one RCCL all-reduce of the whole gradient
+                    sync_metrics()
+                opt.step()
+                mod.global_step += 1
+        else:
+            from fiode_amd.graph_step import GraphTrainStep
+            gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world)
 
-        def step():
-            gstep.step()                              # hipGraph replay (+ eager RCCL between graphs)
-            if world > 1:
-                sync_metrics()
+            def step():
+                gstep.step()                          # hipGraph replay (+ eager RCCL between graphs)
+                if world > 1:
+                    sync_metrics()
 
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    elapsed = float(dt.item())
+        for _ in range(warmup):
+            step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item()), mod, x, y
+
+    train_ode = args.workload == "rk4"
+    elapsed, mod, x, y = timed_run(train_ode, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B_PER_RANK * args.steps / elapsed
+    lyap_only = None
+    if train_ode and not args.no_secondary:
+        e2, _, _, _ = timed_run(False, args.steps, args.warmup)
+        lyap_only = {"images_per_s": round(world * B_PER_RANK * args.steps / e2, 2),
+                     "ms_per_step": round(e2 / args.steps * 1e3, 4)}
 
     # ---- per-kernel timing of the fused hot path with HIP events (same inputs as a step) ----
     from fiode_amd import _lib as L, ops
@@ -203,26 +220,55 @@ def main():
             for i in range(nk):
                 tot[i] += evs[i].elapsed_time(evs[i + 1])
     kern_ms = {L.LYAP_KERNELS[i]: tot[i] / args.prof_reps for i in range(nk)}
-    hot_ms = sum(kern_ms.values())
     rows = B_PER_RANK * H_SAMPLE
-    dom = max(FLOP_ROW, key=lambda k: kern_ms[k])
-    ach = FLOP_ROW[dom] * rows / (kern_ms[dom] * 1e-3) / 1e12
+    kern_flop = {k: FLOP_ROW[k] * rows for k in FLOP_ROW}
+    if train_ode:
+        # the differentiable RK4 solve: k_ot_fwd (one kernel) and k_ot_bwd + its wgrad chain
+        oplan = mod.ode_plan(B_PER_RANK)
+        h0 = torch.full((B_PER_RANK, 10), 0.1, device=dev)
+        E = ops.odetrain_evals(oplan["cfg"])
+        t_f = t_b = 0.0
+        for r in range(args.prof_reps + 2):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record()
+            yo, _, ws = ops.odetrain_forward(feat, h0, w, oplan["dyn"], oplan["cfg"], offset_dev=oplan["offset_dev"])
+            e1.record()
+            ops.odetrain_backward(torch.ones_like(yo), feat, w, oplan["dyn"], oplan["cfg"], ws)
+            e2.record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                t_f += e0.elapsed_time(e1)
+                t_b += e1.elapsed_time(e2)
+        kern_ms["k_ot_fwd"] = t_f / args.prof_reps
+        kern_ms["k_ot_bwd+wgrad"] = t_b / args.prof_reps
+        kern_flop["k_ot_fwd"] = FLOP_ROW_FWD_PASS * E * B_PER_RANK
+        kern_flop["k_ot_bwd+wgrad"] = (2 * (10 * 128 + 128 * 128 + 128 * 10) + FLOP_ROW_FWD_PASS) * E * B_PER_RANK
+    hot_ms = sum(kern_ms.values())
+    dom = max(kern_flop, key=lambda k: kern_ms[k])
+    ach = kern_flop[dom] / (kern_ms[dom] * 1e-3) / 1e12
     traffic = load_pmc_traffic(dom)
     roofline = {"bound": "mfma", "achieved": round(ach, 3), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic, "kernel": dom,
-                "kernel_ms": round(kern_ms[dom], 4), "flop_per_launch": FLOP_ROW[dom] * rows,
+                "kernel_ms": round(kern_ms[dom], 4), "flop_per_launch": kern_flop[dom],
                 "per_kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
-                "hot_path_tflops": round(sum(FLOP_ROW.values()) * rows / (hot_ms * 1e-3) / 1e12, 3)}
+                "per_kernel_tflops": {k: round(kern_flop[k] / (kern_ms[k] * 1e-3) / 1e12, 3)
+                                      for k in kern_flop},
+                "hot_path_tflops": round(sum(kern_flop.values()) / (hot_ms * 1e-3) / 1e12, 3)}
     out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic (x~U[0,1) 128x3x32x32 per rank, y~randint(10))",
-           "config": {"workload": ("hipGraph replay" if not args.eager else "eager") + ": Lyapunov train step of README.md:27 at epoch 20 (configs[1] shape: B=128, "
-                                  "h_sample_size=256 -> 204 uniform + 52 correct-cone rows/image), KWLarge-Cayley "
-                                  "backbone + fused HIP fan-out + Adam",
+           "config": {"workload": ("hipGraph replay" if not args.eager else "eager") + ": " + (
+                          "BASELINE configs[1]: train step of README.md:27 at epoch 20 with train_ode (rk4, step_size "
+                          "0.1, t_max=1: 10 steps / 40 train-mode f-evals, backprop through the stages; loss_ode "
+                          "portion 0.2) + the Lyapunov loss (B=128, h_sample_size=256 -> 204 uniform + 52 "
+                          "correct-cone rows/image), KWLarge-Cayley backbone + Adam" if train_ode else
+                          "Lyapunov-only train step of README.md:27 at epoch 20 (B=128, h_sample_size=256 -> 204 "
+                          "uniform + 52 correct-cone rows/image), KWLarge-Cayley backbone + Adam"),
                       "global_batch": world * B_PER_RANK, "h_sample_size": H_SAMPLE,
                       "rows_per_rank": rows, "parallelism": f"dp{world}"},
            "roofline": roofline,
-           "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)}}
+           "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)},
+           "lyapunov_only_step": lyap_only}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     else:

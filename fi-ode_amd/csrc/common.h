@@ -59,6 +59,54 @@ struct Rng {
 #define RNG_STREAM_DB 0x300u          // + call, index = row
 #define RNG_STREAM_DROP 0x1000u       // + (mask_set << 4) + call, index = row
 
+#define RNG_STREAM_ODE_DROP 0x20000u  // + (eval << 5) + (mask_set << 4) + call, index = batch row
+
+// ---- dropout keep words: bit t of kw[mb] = keep hidden unit 32*mb + t -------------------------
+// mode OFF: all kept.  GIVEN: from a uint8 0/1 mask row [M].  PHILOX: p = 0.5 (bit_mode) one
+// Philox bit per unit; general p: keep iff a random byte < thr8 = round(256 (1 - p)).
+__device__ __forceinline__ void dropout_keep_words(int mode, int bit_mode, uint32_t thr8, const Rng& rng,
+                                                   const uint8_t* mask_row, uint32_t index, uint32_t stream,
+                                                   uint32_t (&kw)[4]) {
+  if (mode == 0) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) kw[mb] = 0xFFFFFFFFu;
+  } else if (mode == 1) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      uint32_t w = 0;
+      const uint4* q = reinterpret_cast<const uint4*>(mask_row + 32 * mb);
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const uint4 t = q[v];
+        const uint32_t ww[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) ? 1u : 0u) << (16 * v + 4 * e + by);
+      }
+      kw[mb] = w;
+    }
+  } else if (bit_mode) {
+    const uint4 r = rng.draw(index, stream);
+    kw[0] = r.x; kw[1] = r.y; kw[2] = r.z; kw[3] = r.w;
+  } else {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int call = 0; call < 2; ++call) {
+        const uint4 r = rng.draw(index, stream + 1 + 2 * mb + call);
+        const uint32_t ww[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) < thr8 ? 1u : 0u) << (16 * call + 4 * e + by);
+      }
+      kw[mb] = w;
+    }
+  }
+}
+
 // Exp(1) variate from 24 random bits: -log(u), u in (0, 1].
 __device__ __forceinline__ float exp1_from_bits(uint32_t x) {
   const float u = (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);

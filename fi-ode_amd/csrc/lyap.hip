@@ -28,6 +28,7 @@
 #include "common.h"
 #include "tile.h"
 #include "../../include/fiode.h"
+#include "wgrad.h"
 
 namespace {
 using namespace fiode_tile;
@@ -123,47 +124,10 @@ __device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C])
   }
 }
 
-// ---- dropout keep words: bit t of kw[mb] = keep hidden unit 32*mb + t --------------------------
 __device__ __forceinline__ void keep_words(const LyapArgs& a, int row, int set, uint32_t (&kw)[4]) {
-  if (a.dropout_mode == FIODE_DROPOUT_OFF) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) kw[mb] = 0xFFFFFFFFu;
-  } else if (a.dropout_mode == FIODE_DROPOUT_GIVEN) {
-    const uint8_t* m = a.masks + ((size_t)set * a.N + row) * M;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      uint32_t w = 0;
-      const uint4* q = reinterpret_cast<const uint4*>(m + 32 * mb);
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const uint4 t = q[v];
-        const uint32_t ww[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) ? 1u : 0u) << (16 * v + 4 * e + by);
-      }
-      kw[mb] = w;
-    }
-  } else if (a.bit_mode) {               // p = 0.5: one Philox bit per unit
-    const uint4 r = a.rng.draw((uint32_t)row, RNG_STREAM_DROP + ((uint32_t)set << 4));
-    kw[0] = r.x; kw[1] = r.y; kw[2] = r.z; kw[3] = r.w;
-  } else {                               // general p: keep iff random byte < round(256 (1-p))
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int call = 0; call < 2; ++call) {
-        const uint4 r = a.rng.draw((uint32_t)row, RNG_STREAM_DROP + ((uint32_t)set << 4) + 1 + 2 * mb + call);
-        const uint32_t ww[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) < a.thr8 ? 1u : 0u) << (16 * call + 4 * e + by);
-      }
-      kw[mb] = w;
-    }
-  }
+  const uint8_t* m = a.dropout_mode == FIODE_DROPOUT_GIVEN ? a.masks + ((size_t)set * a.N + row) * M : nullptr;
+  dropout_keep_words(a.dropout_mode, a.bit_mode, a.thr8, a.rng, m, (uint32_t)row,
+                     RNG_STREAM_DROP + ((uint32_t)set << 4), kw);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -473,7 +437,7 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
       for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
       a.g_u[q] = s;
     }
-  } else {                                                          // scalars
+  } else if (a.tile_sc) {                                           // scalars
     const int ntiles = (a.N + 31) / 32;
     double v = 0.0, ef = 0.0, ac = 0.0;
     for (int t = threadIdx.x; t < ntiles; t += 256) {
@@ -672,3 +636,36 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   if ((rc = mark())) return rc;
   return FIODE_OK;
 }
+
+// ---- shared with the ODE training path (odetrain.hip): weight gradients of rows (b, s) ------
+namespace fiode_internal {
+size_t wgrad_bytes(int B, int S) {
+  int parts, chunk;
+  parts_for(B, S, parts, chunk);
+  return al((size_t)B * parts * SLAB * 4) + al((size_t)B * M * 4);
+}
+
+int launch_wgrad(hipStream_t st, const WgradIO& io) {
+  LyapArgs a{};
+  a.B = io.B; a.S = io.S; a.N = io.B * io.S;
+  parts_for(a.B, a.S, a.parts, a.chunk);
+  a.sampler = FIODE_SAMPLER_GIVEN;
+  a.h_in = io.h; a.x_feat = io.x_feat; a.Qx = io.Qx;
+  a.a1 = const_cast<float*>(io.a1); a.a2 = const_cast<float*>(io.a2);
+  a.gz2 = const_cast<float*>(io.gz2); a.gz1 = const_cast<float*>(io.gz1); a.gft = const_cast<float*>(io.gft);
+  char* ws = static_cast<char*>(io.workspace);
+  a.slabs = reinterpret_cast<float*>(ws);
+  a.g_u = reinterpret_cast<float*>(ws + al((size_t)a.B * a.parts * SLAB * 4));
+  a.tile_sc = nullptr;
+  a.grads = io.grads;
+  hipLaunchKernelGGL(k_lyap_wgrad, dim3(a.B * a.parts), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (a.B * M + RED_COLS - 1) / RED_COLS;
+  hipLaunchKernelGGL(k_lyap_reduce, dim3(red_blocks), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  const int sg_items = M * FIODE_X + M + a.B * FIODE_X;
+  hipLaunchKernelGGL(k_lyap_static_grads, dim3((sg_items + 255) / 256), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
+}  // namespace fiode_internal

@@ -69,6 +69,11 @@ class OdeConfig(ct.Structure):
                 ("rtol", ct.c_double), ("atol", ct.c_double), ("step_size", ct.c_double)]
 
 
+class OdeTrainConfig(ct.Structure):
+    _fields_ = [("batch", ct.c_int32), ("dropout_mode", ct.c_int32), ("seed", ct.c_uint64), ("offset", ct.c_uint64),
+                ("t0", ct.c_double), ("t1", ct.c_double), ("step_size", ct.c_double)]
+
+
 class CertifyConfig(ct.Structure):
     _fields_ = [("n_classes", ct.c_int32), ("T", ct.c_int32), ("batches", ct.c_int32), ("label", ct.c_int32),
                 ("eps", ct.c_float), ("min_std", ct.c_float)]
@@ -101,6 +106,14 @@ def _load():
         "fiode_certify_workspace_bytes": (ct.c_size_t, [ct.c_int64, ct.c_int32]),
         "fiode_certify": (ct.c_int, [_vp, ct.POINTER(CertifyConfig), ct.POINTER(DynConfig), ct.POINTER(DynWeights),
                                      _vp, _vp, ct.c_int64, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_odetrain_evals": (ct.c_int32, [ct.POINTER(OdeTrainConfig)]),
+        "fiode_odetrain_saved_offsets": (ct.c_int, [ct.POINTER(OdeTrainConfig), _vp]),
+        "fiode_odetrain_workspace_bytes": (ct.c_size_t, [ct.POINTER(OdeTrainConfig)]),
+        "fiode_odetrain_forward": (ct.c_int, [_vp, ct.POINTER(OdeTrainConfig), ct.POINTER(DynConfig),
+                                              ct.POINTER(DynWeights), _vp, _vp, _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_odetrain_backward": (ct.c_int, [_vp, ct.POINTER(OdeTrainConfig), ct.POINTER(DynConfig),
+                                               ct.POINTER(DynWeights), _vp, _vp, ct.POINTER(LyapGrads), _vp, _vp,
+                                               ct.c_size_t]),
         "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,
                                              ct.c_int64]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),

@@ -50,6 +50,28 @@ class LyapunovLossFn(torch.autograd.Function):
         return tuple(t * go for t in g) + (None, None)
 
 
+class ODETrainFn(torch.autograd.Function):
+    """y_hat = odeint(h_dot, h0, [0, t_max], method='rk4') in train mode, differentiable
+    (fiode_odetrain_forward / _backward); the train_ode branch of pl_modules.py:490-493."""
+
+    @staticmethod
+    def forward(ctx, x_feat, Q1, b1, Qx, bx, Q2, b2, Q3, b3, h0, plan: dict):
+        w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
+        w = {k: v.detach().contiguous() for k, v in w.items()}
+        xf = x_feat.detach().contiguous()
+        y, stats, ws = ops.odetrain_forward(xf, h0.detach().float().contiguous(), w, plan["dyn"], plan["cfg"],
+                                            masks=plan.get("masks"), offset_dev=plan.get("offset_dev"))
+        plan["stats"] = stats
+        ctx.plan, ctx.w, ctx.xf, ctx.ws = plan, w, xf, ws
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        grads, _ = ops.odetrain_backward(g_y.contiguous(), ctx.xf, ctx.w, ctx.plan["dyn"], ctx.plan["cfg"], ctx.ws)
+        ctx.ws = None
+        return tuple(grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")) + (None, None)
+
+
 class DecisionBoundary(nn.Module):
     """lya_cands.py:72-94 (kept for the validation/ODE path; the training step fuses it)."""
 
@@ -98,9 +120,10 @@ class LyapunovLearning(nn.Module):
             raise NotImplementedError("order=1 (the reference raises for order 0; higher orders are unused)")
         if act != "relu":
             raise NotImplementedError("act='relu' is the README configuration")
-        if barrier_loss or lips_train or relax_exp_stable or adv_train or train_ode:
-            raise NotImplementedError("barrier_loss / lips_train / relax_exp_stable / adv_train / train_ode are off "
+        if barrier_loss or lips_train or relax_exp_stable or adv_train:
+            raise NotImplementedError("barrier_loss / lips_train / relax_exp_stable / adv_train are off "
                                       "in the north-star configuration and not fused")
+        self.train_ode, self.train_ode_epoch = bool(train_ode), int(train_ode_epoch)
         self.order, self.h_sample_size, self.h_dist_lim = order, h_sample_size, h_dist_lim
         self.sampler, self.sampler_scheduler = sampler, sampler_scheduler
         # same module tree as the reference (state_dict keys model.dyn_fun.*, model.init_coordinates.*)
@@ -237,4 +260,37 @@ class LyapunovLearning(nn.Module):
         self.log("effective_batch_size", sc[1])
         self.log("mean_active_constraints", sc[2])
         self.last_plan = plan
+        if self.train_ode and self.current_epoch > self.train_ode_epoch:
+            return self._ode_loss(loss, static_state.float(), w, y)
         return loss
+
+    def ode_plan(self, batch: int, masks: Optional[torch.Tensor] = None) -> dict:
+        """Solver plan of the train_ode solve (make_solver_params(train_ode_solver, train_ode_tol))."""
+        if self.use_adjoint:
+            raise NotImplementedError("odeint_adjoint (SURVEY.md section 8f row 3)")
+        if self.train_ode_solver != "rk4":
+            raise NotImplementedError(f"train_ode with {self.train_ode_solver!r}: the differentiable HIP solve is the "
+                                      "fixed-grid rk4 (BASELINE config 2); adaptive backprop is section 8f row 3")
+        step = make_solver_params("rk4", self.train_ode_tol)["options"]["step_size"]
+        mode = L.FIODE_DROPOUT_PHILOX if self.training else L.FIODE_DROPOUT_OFF
+        if masks is not None:
+            mode = L.FIODE_DROPOUT_GIVEN
+        cfg = ops.odetrain_config(batch, 0.0, float(self.t_max), float(step), mode, seed=self.seed,
+                                  offset=self._rng_offset if self.rng_counter is None else 0)
+        return dict(dyn=self.dyn_fun.dyn_cfg(), cfg=cfg, masks=masks, offset_dev=self.rng_counter)
+
+    def _ode_loss(self, loss, static_state, w, y, masks=None):
+        """pl_modules.py:490-500.  The reference re-runs the backbone inside self.model(x); the
+        backbone is deterministic (no dropout / batch norm), so static_state is reused."""
+        h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
+        plan = self.ode_plan(static_state.shape[0], masks)
+        y_hat = ODETrainFn.apply(static_state, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
+                                 w["b3"], h0, plan)
+        self.last_ode_plan = plan
+        if self.simplex:
+            loss_ode = F.nll_loss(torch.log(y_hat), y)
+        else:
+            loss_ode = F.cross_entropy(y_hat, y)
+        self.log("loss_ode", loss_ode)
+        p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
+        return loss * (1.0 - p) + loss_ode * p

@@ -241,6 +241,85 @@ def odeint_dyn(x_feat: torch.Tensor, h0: torch.Tensor, times: torch.Tensor, weig
     return sol, stats, dstats
 
 
+def odetrain_config(B: int, t0: float, t1: float, step_size: float, dropout_mode: int, seed: int = 0,
+                    offset: int = 0) -> L.OdeTrainConfig:
+    return L.OdeTrainConfig(int(B), int(dropout_mode), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+                            float(t0), float(t1), float(step_size))
+
+
+def odetrain_evals(cfg: L.OdeTrainConfig) -> int:
+    E = L.lib().fiode_odetrain_evals(ct.byref(cfg))
+    if E < 0:
+        raise ValueError("odetrain: invalid time grid (need t1 > t0, step_size > 0, <= 1024 steps)")
+    return E
+
+
+def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
+                     cfg: L.OdeTrainConfig, masks: Optional[torch.Tensor] = None,
+                     offset_dev: Optional[torch.Tensor] = None):
+    """fiode_odetrain_forward: y(t1) of the train-mode RK4 solve.  Returns (y [B,C], stats int32[8],
+    workspace) -- the workspace carries the saved activations to ``odetrain_backward``."""
+    dev = h0.device
+    B = int(cfg.batch)
+    if B > L.FIODE_ODE_MAX_BATCH:
+        raise ValueError(f"batch {B} > FIODE_ODE_MAX_BATCH")
+    h0 = _need(h0, "h0", (B, C), torch.float32, dev)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    E = odetrain_evals(cfg)
+    if cfg.dropout_mode == L.FIODE_DROPOUT_GIVEN:
+        if masks is None:
+            raise ValueError("dropout GIVEN needs masks [E,2,B,M]")
+        masks = _need(masks, "masks", (E, 2, B, M), torch.uint8, dev)
+    if offset_dev is not None:
+        offset_dev = _need(offset_dev, "offset_dev", (1,), torch.int64, dev)
+    lib = L.lib()
+    ws = torch.empty(lib.fiode_odetrain_workspace_bytes(ct.byref(cfg)), dtype=torch.uint8, device=dev)
+    ws_w, cw = _weights_c(weights, dev)
+    y = torch.empty((B, C), dtype=torch.float32, device=dev)
+    stats = torch.zeros(8, dtype=torch.int32, device=dev)
+    dc = dyn.to_c()
+    rc = lib.fiode_odetrain_forward(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(),
+                                    h0.data_ptr(), _ptr(masks), _ptr(offset_dev), y.data_ptr(), stats.data_ptr(),
+                                    ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_odetrain_forward")
+    del ws_w
+    return y, stats, ws
+
+
+def odetrain_saved(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> Dict[str, torch.Tensor]:
+    """Views of the forward's saved arrays in an odetrain workspace (for checkers)."""
+    B, E = int(cfg.batch), odetrain_evals(cfg)
+    off = (ct.c_int64 * 8)()
+    L.check(L.lib().fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)),
+            "fiode_odetrain_saved_offsets")
+    f = lambda i, n: ws[off[i]:off[i] + 4 * n].view(torch.float32)
+    R = B * E
+    return dict(h=f(0, R * C).view(B, E, C), ftilde=f(1, R * C).view(B, E, C), v=f(2, R * C).view(B, E, C),
+                mu=f(3, R).view(B, E), nominal=f(4, R * C).view(B, E, C), a1=f(5, R * M).view(B, E, M),
+                a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C))
+
+
+def odetrain_backward(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
+                      cfg: L.OdeTrainConfig, ws: torch.Tensor, debug: bool = False):
+    """fiode_odetrain_backward: dL/d(weights, x_feat) from dL/dy(t1).  Returns (grads, dbg_gft)."""
+    dev = g_y.device
+    B = int(cfg.batch)
+    g_y = _need(g_y.float(), "g_y", (B, C), torch.float32, dev)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    E = odetrain_evals(cfg)
+    ws_w, cw = _weights_c(weights, dev)
+    grads = {k: torch.empty(WEIGHT_SHAPES[k], dtype=torch.float32, device=dev) for k in WEIGHT_KEYS}
+    grads["x_feat"] = torch.empty((B, X), dtype=torch.float32, device=dev)
+    cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
+    dbg = torch.empty((B, E, C), dtype=torch.float32, device=dev) if debug else None
+    dc = dyn.to_c()
+    rc = L.lib().fiode_odetrain_backward(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(),
+                                         g_y.data_ptr(), ct.byref(cg), _ptr(dbg), ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_odetrain_backward")
+    del ws_w
+    return grads, dbg
+
+
 def certify_grid(T: int = 40, n: int = C, device="cuda") -> torch.Tensor:
     """grid_label_0 of sample_decision_boundary(n, T) as uint8 counts [G][n] (eta = v/T)."""
     lib = L.lib()

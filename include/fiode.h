@@ -170,6 +170,40 @@ FIODE_API int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fiod
                            const double* times, float* solution, int32_t* stats, double* dstats,
                            void* workspace, size_t workspace_bytes);
 
+/* ---- Differentiable RK4 solve for train_ode (pl_modules.py:490-500; models.py:235-241) -------
+ * y_hat = odeint(IVP.h_dot, (h0,), [t0, t1], method='rk4', options.step_size) with the dynamics in
+ * TRAIN mode (fresh dropout masks per func() call), backpropagated through every stage.
+ * evals E = 4 * (niters - 1), niters = ceil((t1 - t0) / step_size + 1) in float32. */
+typedef struct fiode_odetrain_config {
+  int32_t batch;         /* B (<= FIODE_ODE_MAX_BATCH)                                          */
+  int32_t dropout_mode;  /* FIODE_DROPOUT_*; GIVEN: masks [E][2][B][M] uint8 0/1               */
+  uint64_t seed;         /* Philox key                                                          */
+  uint64_t offset;       /* Philox counter offset                                               */
+  double t0, t1;         /* ts = [t0, t1] (linspace(0, t_max, 2))                               */
+  double step_size;      /* make_solver_params('rk4', tol): options.step_size = tol             */
+} fiode_odetrain_config;
+
+FIODE_API int32_t fiode_odetrain_evals(const fiode_odetrain_config* cfg);
+/* The workspace also carries the forward's saved activations to the backward. */
+FIODE_API size_t fiode_odetrain_workspace_bytes(const fiode_odetrain_config* cfg);
+/* y_out [B][C] = y(t1); stats (device int32[8]): nfe, steps, last QP exit iteration.
+ * offset_dev: optional device addend of the Philox offset (graph replay). */
+FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
+                                     const fiode_dyn_weights* w, const float* x_feat, const float* h0,
+                                     const uint8_t* masks, const uint64_t* offset_dev, float* y_out,
+                                     int32_t* stats, void* workspace, size_t workspace_bytes);
+/* Byte offsets inside the workspace of the forward's saved arrays, for checkers:
+ * [0] stage inputs [B][E][C], [1] MLP outputs [B][E][C], [2] QP outputs v [B][E][C], [3] QP mu
+ * [B][E], [4] QP nominal [B][E][C], [5] a1 [B][E][M], [6] a2 [B][E][M], [7] dL/d mlp output
+ * [B][E][C] (after the backward).  Row (b, e) = b*E + e. */
+FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets);
+/* Given g_y = dL/dy(t1) [B][C]: all weight gradients and dL/dx_feat (overwritten).  Must follow
+ * fiode_odetrain_forward on the same workspace.  dbg_gft: optional [B][E][C] dL/d mlp output. */
+FIODE_API int fiode_odetrain_backward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
+                                      const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
+                                      fiode_lyap_grads* grads, float* dbg_gft, void* workspace,
+                                      size_t workspace_bytes);
+
 /* ---- Certification grid (robustness/eval_utils.py:31-89, certify_lipschitz.py:37-143) ------ */
 typedef struct fiode_certify_config {
   int32_t n_classes;     /* 10                                                                   */

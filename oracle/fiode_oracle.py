@@ -631,6 +631,25 @@ def rk4_fixed_grid(func, y0: np.ndarray, t0: float, t1: float, step_size: float,
     return np.stack(sol), len(grid) - 1
 
 
+def rk4_train(x_feat: np.ndarray, h0: np.ndarray, P: DynParams, cfg: DynConfig, t0: float, t1: float,
+              step_size: float, masks: Optional[np.ndarray] = None, p: Optional[float] = None):
+    """The train_ode forward (pl_modules.py:490-493): odeint with method='rk4' and the dynamics in
+    TRAIN mode -- every func() call is eval_dot with its own dropout masks ``masks[e]`` =
+    (layer-1, layer-2) keep masks of eval e, [E,2,B,M] uint8 (None = eval mode).  Returns
+    (y(t1), records) with records[e] = (stage input h, EvalDotResult)."""
+    u = static_projection(x_feat, P)
+    recs = []
+
+    def func(t, h):
+        e = len(recs)
+        m1, m2 = (masks[e, 0], masks[e, 1]) if masks is not None else (None, None)
+        r = eval_dot(h, u, P, cfg, m1, m2, p)
+        recs.append((np.asarray(h, F32).copy(), r))
+        return r.f
+    y, _ = rk4_fixed_grid(func, h0, t0, t1, step_size)
+    return y, recs
+
+
 DOPRI5_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1.0, 1.0]
 DOPRI5_BETA = [
     [1 / 5],

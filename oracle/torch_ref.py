@@ -69,8 +69,29 @@ class _NoUpperProjection(Function):
         return (g[:, None, :] @ jl)[:, 0, :], (g[:, None, :] @ jn)[:, 0, :]
 
 
+class _PinnedActiveSet(Function):
+    """The same projection whose backward takes its active set from another implementation's
+    (v, mu, nominal) -- the QP active-set test ``(v - nominal) + mu > 0`` is float32 rounding
+    noise for inactive coordinates (see fiode_oracle.eval_dot), so chained checks pin it."""
+
+    @staticmethod
+    def forward(ctx, lower, nominal, act):
+        v = _NoUpperProjection.forward(ctx, lower, nominal)
+        ctx.act = act
+        return v
+
+    @staticmethod
+    def backward(ctx, g):
+        act = ctx.act
+        na = ~act
+        cnt = na.sum(dim=-1, keepdim=True).to(g.dtype)
+        corr = torch.where(cnt > 0, (g * na).sum(dim=-1, keepdim=True) / cnt.clamp(min=1), torch.zeros_like(cnt))
+        d = g - corr
+        return torch.where(act, d, torch.zeros_like(d)), torch.where(act, torch.zeros_like(d), d), None
+
+
 def eval_dot(h, x_rows, W: Dict[str, torch.Tensor], alpha_1, alpha_2, sigma_1, scale_nominal,
-             mask1=None, mask2=None, p=0.5, stash=None):
+             mask1=None, mask2=None, p=0.5, stash=None, act=None):
     """classification.py:96-115 (eval_dot) with dropout masks injected.  ``stash`` (a dict)
     receives the QP inputs (lower, nominal) so a checker can pin the QP's active-set test."""
     z = F.linear(h, W["Q1"], W["b1"]) + F.linear(x_rows, W["Qx"], W["bx"])
@@ -89,6 +110,8 @@ def eval_dot(h, x_rows, W: Dict[str, torch.Tensor], alpha_1, alpha_2, sigma_1, s
     if stash is not None:
         stash["lower"] = lower.detach().clone()
         stash["nominal"] = ft.detach().clone()
+    if act is not None:
+        return _PinnedActiveSet.apply(lower, ft, act)
     return _NoUpperProjection.apply(lower, ft)
 
 
@@ -148,3 +171,42 @@ def correct_cone(draws, y):
     h[oh[:, None, :].expand(-1, S2, -1)] = mo.values.flatten()
     h.scatter_(2, mo.indices[:, :, None], lab.unflatten(0, mo.indices.shape)[:, :, None])
     return h
+
+
+def rk4_grid32(t0: float, t1: float, step_size: float):
+    """FixedGridODESolver's float32 grid: niters = ceil((t1-t0)/h + 1), t_k = k h + t0, last = t1."""
+    import math
+    t0f, t1f, hf = torch.tensor(t0, dtype=torch.float32), torch.tensor(t1, dtype=torch.float32), \
+        torch.tensor(step_size, dtype=torch.float32)
+    n = int(math.ceil(float((t1f - t0f) / hf + 1)))
+    g = torch.arange(n, dtype=torch.float32) * hf + t0f
+    g[-1] = t1f
+    return g
+
+
+def ode_train_loss(x_feat, h0, y, W: Dict[str, torch.Tensor], masks, t0=0.0, t1=1.0, step_size=0.1, *,
+                   alpha_1=100.0, alpha_2=20.0, sigma_1=0.02, scale_nominal=True, p=0.5, acts=None):
+    """pl_modules.py:490-497: y_hat = odeint(h_dot, h0, [t0, t1], method='rk4', step_size) in train
+    mode (torchdiffeq 0.2.2 rk4_alt_step_func op order), loss_ode = nll_loss(log(y_hat), y).
+    masks: [E,2,B,M] uint8 keep masks per func() call; acts: optional per-eval pinned QP active
+    sets [E][B,C] bool.  Returns (loss_ode, y_hat)."""
+    grid = rk4_grid32(t0, t1, step_size)
+    third = 1.0 / 3.0
+    e = [0]
+
+    def f(hh):
+        i = e[0]
+        e[0] += 1
+        m1 = masks[i, 0] if masks is not None else None
+        m2 = masks[i, 1] if masks is not None else None
+        return eval_dot(hh, x_feat, W, alpha_1, alpha_2, sigma_1, scale_nominal, m1, m2, p,
+                        act=None if acts is None else acts[i])
+    yy = h0
+    for a, b in zip(grid[:-1], grid[1:]):
+        dt = b - a
+        k1 = f(yy)
+        k2 = f(yy + dt * k1 * third)
+        k3 = f(yy + dt * (k2 - k1 * third))
+        k4 = f(yy + dt * (k1 - k2 + k3))
+        yy = yy + (k1 + 3 * (k2 + k3) + k4) * dt * 0.125
+    return F.nll_loss(torch.log(yy), y), yy

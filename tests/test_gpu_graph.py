@@ -12,17 +12,18 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def test_graph_replay_matches_eager_step():
+@pytest.mark.parametrize("train_ode", [False, True])
+def test_graph_replay_matches_eager_step(train_ode):
     import bench
     from fiode_amd.graph_step import GraphTrainStep
     dev = _dev()
-    mod = bench.build_module(dev, seed=0)
+    mod = bench.build_module(dev, seed=0, train_ode=train_ode)
     g = torch.Generator(device="cpu").manual_seed(5)
     x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (32,), generator=g).to(dev)
     opt = mod.configure_optimizers(capturable=True)[0][0]
     gs = GraphTrainStep(mod, opt, x, y, warmup=2)
-    twin = bench.build_module(dev, seed=1)          # same parameters / counter as before the replay
+    twin = bench.build_module(dev, seed=1, train_ode=train_ode)          # same parameters / counter as before the replay
     twin.load_state_dict(mod.state_dict())
     twin.rng_counter = mod.rng_counter.clone()
     twin.seed = mod.seed

@@ -1,0 +1,121 @@
+"""GPU parity of the differentiable train-mode RK4 solve (fiode_odetrain_forward / _backward,
+the train_ode branch of pl_modules.py:490-500) against the oracle (numpy forward,
+oracle.fiode_oracle.rk4_train) and torch autograd through the reference-order RK4 stages
+(oracle.torch_ref.ode_train_loss) with the same dropout masks.
+
+Tolerances: forward 2e-4 absolute on the simplex state (MLP accumulation order can move a
+stage's batch-global QP exit by one bisection step, as in test_gpu_ode).  Gradients: relative
+2e-3 of each tensor's max-abs (float32 chains of 40 stage VJPs, MFMA vs torch accumulation
+order); the QP active sets of the torch autograd are pinned to the device's (v, mu, nominal),
+because the reference's active-set test is float32 rounding noise on inactive coordinates."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fiode_oracle as O
+from tests._util import make_params
+
+pytestmark = pytest.mark.gpu
+KEYS = ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _case(B, step, scale_nominal, seed, p=0.5):
+    from fiode_amd import _lib as L, ops
+    dev = _dev()
+    P = make_params(seed=seed)
+    rng = np.random.default_rng(seed + 7)
+    x = rng.normal(size=(B, 10)).astype(np.float32)
+    h0 = np.full((B, 10), 0.1, np.float32)
+    labels = rng.integers(0, 10, B)
+    cfg = ops.odetrain_config(B, 0.0, 1.0, step, L.FIODE_DROPOUT_GIVEN if p > 0 else L.FIODE_DROPOUT_OFF)
+    E = ops.odetrain_evals(cfg)
+    masks = (rng.random((E, 2, B, 128)) >= p).astype(np.uint8) if p > 0 else None
+    w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in KEYS}
+    dyn = ops.DynCfg(scale_nominal=scale_nominal, dropout=p)
+    return ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn
+
+
+@pytest.mark.parametrize("B,step,scale_nominal", [(64, 0.25, True), (128, 0.1, False), (37, 0.3, True)])
+def test_forward_matches_oracle(B, step, scale_nominal):
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(B, step, scale_nominal, 100 + B)
+    ref, recs = O.rk4_train(x, h0, P, O.DynConfig(scale_nominal=scale_nominal), 0.0, 1.0, step, masks, 0.5)
+    assert len(recs) == E
+    y, st, ws = ops.odetrain_forward(torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev), w, dyn, cfg,
+                                     masks=torch.from_numpy(masks).to(dev))
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[0] == E and s[1] == E // 4
+    err = float(np.abs(y.cpu().numpy() - ref).max())
+    assert err <= 2e-4, err
+    sv = ops.odetrain_saved(ws, cfg)
+    herr = max(float(np.abs(sv["h"][:, e].cpu().numpy() - recs[e][0]).max()) for e in range(E))
+    assert herr <= 2e-4, herr
+
+
+@pytest.mark.parametrize("B,step,scale_nominal", [(64, 0.25, True), (128, 0.1, False), (48, 0.5, False)])
+def test_backward_matches_torch_autograd(B, step, scale_nominal):
+    from oracle import torch_ref as T
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(B, step, scale_nominal, 200 + B)
+    xt, h0t = torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev)
+    y, st, ws = ops.odetrain_forward(xt, h0t, w, dyn, cfg, masks=torch.from_numpy(masks).to(dev))
+    yd = y.detach().clone().requires_grad_(True)
+    lab = torch.from_numpy(labels).to(dev)
+    torch.nn.functional.nll_loss(torch.log(yd), lab).backward()
+    grads, _ = ops.odetrain_backward(yd.grad, xt, w, dyn, cfg, ws)
+    sv = ops.odetrain_saved(ws, cfg)
+    act = ((sv["v"] - sv["nominal"]) + sv["mu"][..., None] > 0).cpu()          # [B,E,C]
+    acts = [act[:, e] for e in range(E)]
+    leaves = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).clone().requires_grad_(True) for k in KEYS}
+    xf = torch.from_numpy(x).clone().requires_grad_(True)
+    loss, yy = T.ode_train_loss(xf, torch.from_numpy(h0), torch.from_numpy(labels), leaves, torch.from_numpy(masks),
+                                0.0, 1.0, step, scale_nominal=scale_nominal, p=0.5, acts=acts)
+    loss.backward()
+    ref = {k: leaves[k].grad for k in KEYS}
+    ref["x_feat"] = xf.grad
+    for k in KEYS + ("x_feat",):
+        g = grads[k].cpu()
+        r = ref[k]
+        scale = float(r.abs().max()) + 1e-12
+        err = float((g - r).abs().max()) / scale
+        assert err <= 2e-3, (k, err, scale)
+
+
+def test_philox_masks_fresh_per_offset():
+    from fiode_amd import _lib as L
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(64, 0.25, True, 5)
+    xt, h0t = torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev)
+    outs = []
+    for off in (0, 0, 1):
+        c = ops.odetrain_config(64, 0.0, 1.0, 0.25, L.FIODE_DROPOUT_PHILOX, seed=9, offset=off)
+        y, _, _ = ops.odetrain_forward(xt, h0t, w, dyn, c)
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1]) and not torch.equal(outs[0], outs[2])
+    assert torch.isfinite(outs[2]).all()
+    assert torch.allclose(outs[2].sum(-1), torch.ones(64), atol=1e-3)
+
+
+def test_module_train_ode_loss_mix():
+    """compute_loss with train_ode: loss = (1-p) lyapunov + p nll(log y_hat), p = min(.98, (epoch -
+    train_ode_epoch)/50) (pl_modules.py:490-500); gradients reach the backbone and the dynamics."""
+    import bench
+    dev = _dev()
+    mod = bench.build_module(dev, seed=0, train_ode=True)
+    x = torch.rand(16, 3, 32, 32, device=dev)
+    y = torch.randint(0, 10, (16,), device=dev)
+    loss = mod.compute_loss(x, y, 16, "relu")
+    lyap = float(mod.last_plan["scalars"][0])
+    lode = float(mod.logged["loss_ode"])
+    p = min(0.98, (bench.EPOCH - bench.TRAIN_ODE_EPOCH) / 50.0)
+    assert abs(float(loss) - ((1 - p) * lyap + p * lode)) < 1e-5
+    loss.backward()
+    for name, prm in mod.named_parameters():
+        if prm.requires_grad:
+            assert prm.grad is not None and torch.isfinite(prm.grad).all(), name
+    s = mod.last_ode_plan["stats"].cpu()
+    assert int(s[0]) == 40 and int(s[1]) == 10

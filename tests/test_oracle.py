@@ -269,3 +269,44 @@ def test_certify_batches_rule():
     assert O.certify_batches(41_320_837, 10)[-1] == (41_320_830, 41_320_837)
     assert len(O.certify_batches(41_320_837, 10)) == 11
     assert O.certify_batches(20, 10) == [(2 * i, 2 * i + 2) for i in range(10)]
+
+
+def test_rk4_train_oracle_matches_torch_ref_forward():
+    """The numpy train-mode RK4 (fiode_oracle.rk4_train) and the autograd restatement
+    (torch_ref.ode_train_loss) agree on y(t1) with the same dropout masks."""
+    import torch
+    from oracle import torch_ref as T
+    P = make_params(3)
+    cfg = O.DynConfig(scale_nominal=True)
+    rng = np.random.default_rng(0)
+    B = 16
+    x = rng.normal(size=(B, 10)).astype(np.float32)
+    h0 = np.full((B, 10), 0.1, np.float32)
+    masks = (rng.random((16, 2, B, 128)) < 0.5).astype(np.uint8)
+    y, recs = O.rk4_train(x, h0, P, cfg, 0.0, 1.0, 0.25, masks, 0.5)
+    assert len(recs) == 16
+    W = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))) for k in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")}
+    loss, yy = T.ode_train_loss(torch.from_numpy(x), torch.from_numpy(h0), torch.from_numpy(rng.integers(0, 10, B)),
+                                W, torch.from_numpy(masks), 0.0, 1.0, 0.25)
+    assert np.abs(yy.numpy() - y).max() < 1e-4
+    assert np.allclose(y.sum(-1), 1.0, atol=1e-3)
+
+
+def test_pinned_active_set_backward_equals_reference_backward():
+    """torch_ref._PinnedActiveSet with the projection's own active set = _NoUpperProjection."""
+    import torch
+    from oracle import torch_ref as T
+    rng = np.random.default_rng(4)
+    h = O.uniform_simplex(rng.exponential(1, (50, 10)).astype(np.float32))
+    lower = torch.from_numpy(O.barrier_lower(h, O.DynConfig()))
+    nom = torch.from_numpy(rng.normal(0, 10, (50, 10)).astype(np.float32))
+    g = torch.from_numpy(rng.normal(size=(50, 10)).astype(np.float32))
+    a1, n1 = lower.clone().requires_grad_(True), nom.clone().requires_grad_(True)
+    v = T._NoUpperProjection.apply(a1, n1)
+    (v * g).sum().backward()
+    r = O.qp_forward(lower.numpy(), nom.numpy())
+    act = torch.from_numpy(((r.v - nom.numpy()) + r.mu[:, None]) > 0)
+    a2, n2 = lower.clone().requires_grad_(True), nom.clone().requires_grad_(True)
+    v2 = T._PinnedActiveSet.apply(a2, n2, act)
+    (v2 * g).sum().backward()
+    assert torch.allclose(a1.grad, a2.grad, atol=1e-6) and torch.allclose(n1.grad, n2.grad, atol=1e-6)
