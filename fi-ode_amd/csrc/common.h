@@ -107,6 +107,42 @@ __device__ __forceinline__ void dropout_keep_words(int mode, int bit_mode, uint3
   }
 }
 
+// One word (hidden units 32*mb .. 32*mb+31) of dropout_keep_words, same draws.
+__device__ __forceinline__ uint32_t dropout_keep_word(int mode, int bit_mode, uint32_t thr8, const Rng& rng,
+                                                      const uint8_t* mask_row, uint32_t index, uint32_t stream,
+                                                      int mb) {
+  if (mode == 0) return 0xFFFFFFFFu;
+  if (mode == 1) {
+    uint32_t w = 0;
+    const uint4* q = reinterpret_cast<const uint4*>(mask_row + 32 * mb);
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const uint4 t = q[v];
+      const uint32_t ww[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) ? 1u : 0u) << (16 * v + 4 * e + by);
+    }
+    return w;
+  }
+  if (bit_mode) {
+    const uint4 r = rng.draw(index, stream);
+    return mb == 0 ? r.x : mb == 1 ? r.y : mb == 2 ? r.z : r.w;
+  }
+  uint32_t w = 0;
+#pragma unroll
+  for (int call = 0; call < 2; ++call) {
+    const uint4 r = rng.draw(index, stream + 1 + 2 * mb + call);
+    const uint32_t ww[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int by = 0; by < 4; ++by) w |= (((ww[e] >> (8 * by)) & 0xFFu) < thr8 ? 1u : 0u) << (16 * call + 4 * e + by);
+  }
+  return w;
+}
+
 // Exp(1) variate from 24 random bits: -log(u), u in (0, 1].
 __device__ __forceinline__ float exp1_from_bits(uint32_t x) {
   const float u = (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);

@@ -5,14 +5,15 @@
 // (torchdiffeq 0.2.2 FixedGridODESolver + rk4_alt_step_func, the 3/8 rule; every func() call is
 // eval_dot with fresh dropout masks and the QP's batch-global exit over the B rows).
 //
-// Forward  (k_ot_fwd, one persistent workgroup: each stage's QP exit is a batch-wide AND):
-//   for each step, stage i = 1..4 (eval e = 4*step + i - 1):
-//     Y_i = y + dt * sum_j beta_ij k_j      -> hs[b][e]        thread per element
-//     MLP (MFMA wave tiles), a1/a2 saved    -> a1/a2[b][e], ft[b][e]
-//     QP to the global exit                 -> k_i = v[b][e], mu[b][e]
+// Forward  (k_ot_fwd, one persistent workgroup per 32-row tile, all tiles co-resident; each
+//   stage's QP exit is a batch-wide AND exchanged through tagged granules, see below):
+//   for each step, stage i = 1..4 (eval e = 4*step + i - 1), per row in registers:
+//     Y_i = y + dt * sum_j beta_ij k_j      -> hs[b][e]
+//     MLP (MFMA, hidden split over 4 waves), a1/a2 saved -> a1/a2[b][e], ft[b][e]
+//     QP bisection recording mu per iteration; exit K from all tiles; k_i = v(mu_K)
 //   y += (k1 + 3 (k2 + k3) + k4) dt / 8
-// Backward (k_ot_bwd, one wave per 32 rows; rows never interact in the backward, so there are
-//   no barriers): the reverse sweep of the 3/8 rule; every stage VJP is the QP backward
+// Backward (k_ot_bwd, one workgroup per 32 rows; rows never interact in the backward, so tiles
+//   need no grid-wide synchronisation): the reverse sweep of the 3/8 rule; every stage VJP is the QP backward
 //   (closed form), the sigmoid rescale, the barrier bounds' h-dependence, and the MLP input
 //   gradients (Q3^T, Q2^T via LDS images, Q1^T via a zero-padded LDS image), writing the per-
 //   (row, eval) activation gradients gft / gz2 / gz1.
@@ -25,8 +26,6 @@
 namespace {
 using namespace fiode_tile;
 
-constexpr int OT_THREADS = 256;
-constexpr int OT_WAVES = OT_THREADS / 64;
 
 struct OTArgs {
   int B, E, niters;
@@ -59,6 +58,11 @@ struct OTArgs {
   float* gz2;               // [B][E][M]
   float* gz1;               // [B][E][M]
   float* gft;               // [B][E][C]
+  unsigned long long* xslots;  // [E][ntiles] {epoch, mask} granules of the QP exit exchange
+  uint32_t* kw;                // [E][2][B] uint4 dropout keep words
+#ifdef OT_PROFILE
+  unsigned long long* prof;    // [8] wall-clock ticks per phase (workgroup 0, lane 0)
+#endif
 };
 
 // float32 grid of FixedGridODESolver: t_k = k*h + t0, last point = t1
@@ -79,142 +83,293 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// forward: one eval (stage) over all B rows; stage input already in hs[:, e]
-__device__ void ot_eval(const OTArgs& a, const Rng& rng, const float* Q2s, const float* Q3s,
-                        const float (&q1)[4][5], int e, float* kout, uint32_t* word, int* last_exit) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
-  const int ntiles = (a.B + 31) / 32;
-  for (int tile = wave; tile < ntiles; tile += OT_WAVES) {
-    const int b = tile * 32 + col;
-    const bool valid = b < a.B;
-    const int bb = valid ? b : a.B - 1;
-    const size_t r = (size_t)bb * a.E + e;
-    float h[C];
-    load_row10(a.hs + r * C, h);
-    uint32_t kw1[4], kw2[4];
-    const uint8_t* m1 = a.dropout_mode == FIODE_DROPOUT_GIVEN ? a.masks + (((size_t)e * 2 + 0) * a.B + bb) * M : nullptr;
-    const uint8_t* m2 = a.dropout_mode == FIODE_DROPOUT_GIVEN ? a.masks + (((size_t)e * 2 + 1) * a.B + bb) * M : nullptr;
-    dropout_keep_words(a.dropout_mode, a.bit_mode, a.thr8, rng, m1, (uint32_t)bb,
-                       RNG_STREAM_ODE_DROP + ((uint32_t)e << 5), kw1);
-    dropout_keep_words(a.dropout_mode, a.bit_mode, a.thr8, rng, m2, (uint32_t)bb,
-                       RNG_STREAM_ODE_DROP + ((uint32_t)e << 5) + 16u, kw2);
-    f32x16 z1[4], z2[4];
-    const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)bb * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale, col, half,
-                               z1, z2);
-    float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-    gather_ft(z3, half, ft);
-    barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-    uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
-    if (!valid) conv = 0xFFFFFFFFu;
-    conv = wave_and(conv);
-    if (lane == 0) atomicAnd(word, conv);
-    if (valid) {
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        store_acc_rows(a.a1 + r * M, mb, half, z1[mb]);
-        store_acc_rows(a.a2 + r * M, mb, half, z2[mb]);
+// forward: one workgroup per 32-row tile, persistent over all evals; 4 waves = 4 parts of the
+// hidden dimension.  Per eval every wave computes layer 1 in full (20 MFMA), its 32 of the 128
+// layer-2 outputs (64 MFMA) and their layer-3 partial (16 MFMA); the partials meet in LDS and
+// every wave sums them in the same order, so the row state (y, k1..k4, the QP) is replicated in
+// the 4 waves and needs no further exchange.  The only cross-tile coupling -- the QP's exit
+// iteration, the lowest bit of the AND over ALL rows of the per-iteration convergence masks --
+// is exchanged through per-eval {tag, mask} granules: each workgroup publishes its mask with ONE
+// agent-scope 64-bit atomic store, then one wave sweeps the ntiles granules of that eval until
+// every tag matches (relaxed agent-scope loads; the granule IS the flag, so no fence is needed).
+// The spin is bounded: on timeout the status word records it and the solve completes.
+struct OtShared {
+  float zpart[4][64][6];      // [part][lane][valid layer-3 accumulator registers]
+  float mu_rec[4][32][33];    // [wave][row][bisection iteration] (padded)
+  float Q1s[M * C];
+  uint32_t K;
+  int pad[3];
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+
+__device__ __forceinline__ void publish_mask(unsigned long long* slot, unsigned epoch, uint32_t mask) {
+  __hip_atomic_store((gu64_t*)(slot), ((unsigned long long)epoch << 32) | mask, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...)
+__device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int ntiles, unsigned epoch,
+                                                 int32_t* status, int lane) {
+  uint32_t acc = 0xFFFFFFFFu;
+  for (int base = 0; base < ntiles; base += 64) {
+    const int t = base + lane;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      unsigned long long x = 0;
+      if (t < ntiles) {
+        x = __hip_atomic_load((gu64_t*)(slots + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = (unsigned)(x >> 32) == epoch;
       }
-      if (half == 0) store_row10(a.ftw + r * C, ft);
+      if (__all(ok)) {
+        if (t < ntiles) acc &= (uint32_t)x;
+        break;
+      }
+      if (++spins > (1u << 22)) {           // ~0.5 s: a non-resident tile; record and give up
+        if (lane == 0) atomicMax(status, 4);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
   }
-  __syncthreads();
-  const int K = qp_exit_iter(*word, a.d.max_iter);
-  for (int b = threadIdx.x; b < a.B; b += OT_THREADS) {
-    const size_t r = (size_t)b * a.E + e;
-    float h[C], ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-    load_row10(a.hs + r * C, h);
-    load_row10(a.ftw + r * C, ft);
-    barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-    qp_bisect(lower, nominal, K, a.d.tol, v, mu);
-    store_row10(a.vw + r * C, v);
-    store_row10(a.nomw + r * C, nominal);
-    a.muw[r] = mu;
-    store_row10(kout + (size_t)b * C, v);
+  return wave_and(acc);
+}
+
+__device__ __forceinline__ uint32_t qp_bisect_record(const float (&lower)[C], const float (&nom)[C], int last,
+                                                     float tol, float* mu_rec, bool rec) {
+  float hi = nom[0] - lower[0], lo = nom[0];
+#pragma unroll
+  for (int j = 1; j < C; ++j) {
+    hi = fmaxf(hi, nom[j] - lower[j]);
+    lo = fminf(lo, nom[j]);
   }
-  __syncthreads();              // every thread has read the word; k_i complete
-  if (threadIdx.x == 0) {      // reset for the next eval (whose first atomicAnd follows the
-    *last_exit = K;            // caller's stage-input barrier)
-    *word = 0xFFFFFFFFu;
+  uint32_t conv = 0;
+  for (int it = 0; it <= last; ++it) {
+    const float mu = (hi - lo) / 2.0f + lo;
+    float eps = 0.f;
+#pragma unroll
+    for (int j = 0; j < C; ++j) eps = eps + fmaxf(nom[j] - mu, lower[j]);
+    if (rec) mu_rec[it] = mu;
+    conv |= (fabsf(eps) < tol ? 1u : 0u) << it;
+    lo = eps > 0.f ? mu : lo;
+    hi = eps < 0.f ? mu : hi;
+  }
+  return conv;
+}
+
+#ifdef OT_PROFILE
+#define OT_MARK(i) do { const uint64_t t_ = wall_clock64(); if (blockIdx.x == 0 && threadIdx.x == 0) \
+    atomicAdd((unsigned long long*)&a.prof[i], (unsigned long long)(t_ - t_prev)); t_prev = t_; } while (0)
+#else
+#define OT_MARK(i) do { } while (0)
+#endif
+
+// one eval for this workgroup's tile: stage input h (per lane, its row) -> k (per lane)
+__device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtShared& sh, int e, int p, int b,
+                        bool valid, int lane, int half, int col, const f32x16 (&uacc)[4], const uint32_t (&kw1)[4],
+                        uint32_t kw2p, const float (&h)[C], float (&k)[C]) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + e;
+#ifdef OT_PROFILE
+  uint64_t t_prev = wall_clock64();
+#endif
+  if (p == 0 && valid && half == 0) store_row10(a.hs + r * C, h);
+  // layer 1 (full): z1 = u[b] + Q1 h
+  f32x16 z1[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) z1[mb] = uacc[mb];
+#pragma unroll
+  for (int s = 0; s < 5; ++s) {
+    const float bs = half ? h[2 * s + 1] : h[2 * s];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) z1[mb] = mfma32(sh.Q1s[(32 * mb + col) * C + 2 * s + half], bs, z1[mb]);
+  }
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) dropout_relu(z1[mb], kw1[mb], half, a.drop_scale);
+  OT_MARK(0);
+  if (valid) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+      if (mb == p) store_acc_rows(a.a1 + r * M, mb, half, z1[mb]);
+  }
+  // layer 2, output block p: z2 = b2 + Q2[32p.., :] a1
+  f32x16 z2;
+  load_acc_rows(a.b2, p, half, z2);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(Q2s + (32 * p + col) * LDQ + 32 * kb + 8 * g + 4 * half);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) z2 = mfma32(q[t], z1[kb][4 * g + t], z2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  dropout_relu(z2, kw2p, half, a.drop_scale);
+  if (valid) store_acc_rows(a.a2 + r * M, p, half, z2);
+  // layer-3 partial over hidden block p (bias on part 0)
+  f32x16 z3 = f16_zero();
+  if (p == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = acc_row(q, half);
+      z3[q] = i < C ? a.b3[i] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(Q3s + col * LDQ + 32 * p + 8 * g + 4 * half);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) z3 = mfma32(q[t], z2[4 * g + t], z3);
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) sh.zpart[p][lane][q] = z3[q];
+  OT_MARK(1);
+  __syncthreads();
+  f32x16 zs = f16_zero();
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    zs[q] = ((sh.zpart[0][lane][q] + sh.zpart[1][lane][q]) + sh.zpart[2][lane][q]) + sh.zpart[3][lane][q];
+  float ft[C], lower[C], nominal[C], sig[C], span[C];
+  gather_ft(zs, half, ft);
+  barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+  uint32_t conv = qp_bisect_record(lower, nominal, a.d.max_iter - 1, a.d.tol, &sh.mu_rec[p][col][0], half == 0);
+  if (!valid) conv = 0xFFFFFFFFu;
+  conv = wave_and(conv);
+  OT_MARK(2);
+  const int ntiles = gridDim.x;
+  unsigned long long* slots = a.xslots + (size_t)e * ntiles;
+  if (p == 0 && lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, conv);
+  if (p == 0) {
+    const uint32_t all = gather_masks(slots, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
+    if (lane == 0) sh.K = (uint32_t)qp_exit_iter(all, a.d.max_iter);
+  }
+  __syncthreads();
+  OT_MARK(3);
+  const int K = (int)sh.K;
+  const float mu = sh.mu_rec[p][col][K];
+#pragma unroll
+  for (int j = 0; j < C; ++j) k[j] = fmaxf(nominal[j] - mu, lower[j]);
+  if (p == 0 && valid && half == 0) {
+    store_row10(a.ftw + r * C, ft);
+    store_row10(a.nomw + r * C, nominal);
+    store_row10(a.vw + r * C, k);
+    a.muw[r] = mu;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.stats[2] = K;
+  __syncthreads();            // zpart / mu_rec / K reused by the next eval
+  OT_MARK(4);
+}
+
+// dropout keep words of every (eval, set, row): kw[e][set][b] (uint4 = the 4 words of the 128 units)
+__global__ __launch_bounds__(256) void k_ot_masks(OTArgs a) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.E * a.B) return;
+  const int e = q / a.B, b = q - e * a.B;
+  const Rng rng = rng_of(a);
+#pragma unroll
+  for (int set = 0; set < 2; ++set) {
+    const uint8_t* m = a.dropout_mode == FIODE_DROPOUT_GIVEN ? a.masks + (((size_t)e * 2 + set) * a.B + b) * M : nullptr;
+    uint32_t w[4];
+    dropout_keep_words(a.dropout_mode, a.bit_mode, a.thr8, rng, m, (uint32_t)b,
+                       RNG_STREAM_ODE_DROP + ((uint32_t)e << 5) + ((uint32_t)set << 4), w);
+    reinterpret_cast<uint4*>(a.kw)[((size_t)e * 2 + set) * a.B + b] = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
-__global__ __launch_bounds__(OT_THREADS) void k_ot_fwd(OTArgs a) {
+__global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
-  uint32_t* word = reinterpret_cast<uint32_t*>(smem + (M + 32) * LDQ);
-  int* last_exit = reinterpret_cast<int*>(word + 1);
+  OtShared& sh = *reinterpret_cast<OtShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
-  if (threadIdx.x == 0) *word = 0xFFFFFFFFu;
-  for (int e = threadIdx.x; e < a.B * M; e += OT_THREADS) {      // u[b] = U_x x_b + bx + b1
-    const int b = e / M, i = e - b * M;
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < FIODE_X; ++c) s = __fmaf_rn(a.Qx[i * FIODE_X + c], a.x_feat[(size_t)b * FIODE_X + c], s);
-    a.u[e] = (s + a.bx[i]) + a.b1[i];
-  }
-  for (int e = threadIdx.x; e < a.B * C; e += OT_THREADS) a.y[e] = a.h0[e];
-  __syncthreads();
-  const Rng rng = rng_of(a);
+  for (int q = threadIdx.x; q < M * C; q += blockDim.x) sh.Q1s[q] = a.Q1[q];
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
-  float q1[4][5];
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x * 32 + col;
+  const bool valid = b < a.B;
+  const int bb = valid ? b : a.B - 1;
+  // u[b] = U_x x_b + bx + b1 for this tile's rows (part p computes hidden block p)
+  for (int q = threadIdx.x; q < 32 * M; q += blockDim.x) {
+    const int rb = blockIdx.x * 32 + q / M, i = q % M;
+    if (rb < a.B) {
+      float s = 0.f;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+      for (int c = 0; c < FIODE_X; ++c) s = __fmaf_rn(a.Qx[i * FIODE_X + c], a.x_feat[(size_t)rb * FIODE_X + c], s);
+      a.u[(size_t)rb * M + i] = (s + a.bx[i]) + a.b1[i];
+    }
+  }
+  __syncthreads();
+  f32x16 uacc[4];
 #pragma unroll
-    for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
-  const size_t BC = (size_t)a.B * C;
-  float* k1 = a.k;
-  float* k2 = a.k + BC;
-  float* k3 = a.k + 2 * BC;
-  float* k4 = a.k + 3 * BC;
+  for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)bb * M, mb, half, uacc[mb]);
+  // dropout keep words of eval e (k_ot_masks), prefetched one eval ahead
+  const uint4* kwp = reinterpret_cast<const uint4*>(a.kw);
+  auto fetch = [&](int e, uint32_t (&w1)[4], uint32_t& w2) {
+    if (a.dropout_mode == FIODE_DROPOUT_OFF) {
+      w1[0] = w1[1] = w1[2] = w1[3] = w2 = 0xFFFFFFFFu;
+      return;
+    }
+    const uint4 q1 = kwp[((size_t)e * 2 + 0) * a.B + bb];
+    const uint4 q2 = kwp[((size_t)e * 2 + 1) * a.B + bb];
+    w1[0] = q1.x; w1[1] = q1.y; w1[2] = q1.z; w1[3] = q1.w;
+    w2 = p == 0 ? q2.x : p == 1 ? q2.y : p == 2 ? q2.z : q2.w;
+  };
+  uint32_t kc1[4], kc2, kn1[4], kn2;
+  fetch(0, kc1, kc2);
+  float y[C], k1[C], k2[C], k3[C], k4[C], hin[C];
+  load_row10(a.h0 + (size_t)bb * C, y);
   const float third = 1.0f / 3.0f;
   for (int it = 0; it + 1 < a.niters; ++it) {
     float ta, dt;
     step_times(a, it, ta, dt);
     const int e0 = 4 * it;
-    for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) {
-      const int b = q / C, j = q - b * C;
-      a.hs[((size_t)b * a.E + e0) * C + j] = a.y[q];
+    const int eN = 4 * (a.niters - 1);
+#define OT_STAGE(E_, H_, K_)                                                       \
+    {                                                                              \
+      if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                \
+      ot_eval(a, Q2s, Q3s, sh, (E_), p, b, valid, lane, half, col, uacc, kc1, kc2, H_, K_); \
+      kc1[0] = kn1[0]; kc1[1] = kn1[1]; kc1[2] = kn1[2]; kc1[3] = kn1[3]; kc2 = kn2; \
     }
-    __syncthreads();
-    ot_eval(a, rng, Q2s, Q3s, q1, e0, k1, word, last_exit);
-    for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) {
-      const int b = q / C, j = q - b * C;
-      a.hs[((size_t)b * a.E + e0 + 1) * C + j] = a.y[q] + (dt * k1[q]) * third;
+    OT_STAGE(e0, y, k1)
+#pragma unroll
+    for (int j = 0; j < C; ++j) hin[j] = y[j] + (dt * k1[j]) * third;
+    OT_STAGE(e0 + 1, hin, k2)
+#pragma unroll
+    for (int j = 0; j < C; ++j) hin[j] = y[j] + dt * (k2[j] - k1[j] * third);
+    OT_STAGE(e0 + 2, hin, k3)
+#pragma unroll
+    for (int j = 0; j < C; ++j) hin[j] = y[j] + dt * ((k1[j] - k2[j]) + k3[j]);
+    OT_STAGE(e0 + 3, hin, k4)
+#undef OT_STAGE
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const float dy = (((k1[j] + 3.0f * (k2[j] + k3[j])) + k4[j]) * dt) * 0.125f;
+      y[j] = y[j] + dy;
     }
-    __syncthreads();
-    ot_eval(a, rng, Q2s, Q3s, q1, e0 + 1, k2, word, last_exit);
-    for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) {
-      const int b = q / C, j = q - b * C;
-      a.hs[((size_t)b * a.E + e0 + 2) * C + j] = a.y[q] + dt * (k2[q] - k1[q] * third);
-    }
-    __syncthreads();
-    ot_eval(a, rng, Q2s, Q3s, q1, e0 + 2, k3, word, last_exit);
-    for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) {
-      const int b = q / C, j = q - b * C;
-      a.hs[((size_t)b * a.E + e0 + 3) * C + j] = a.y[q] + dt * ((k1[q] - k2[q]) + k3[q]);
-    }
-    __syncthreads();
-    ot_eval(a, rng, Q2s, Q3s, q1, e0 + 3, k4, word, last_exit);
-    for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) {
-      const float dy = (((k1[q] + 3.0f * (k2[q] + k3[q])) + k4[q]) * dt) * 0.125f;
-      a.y[q] = a.y[q] + dy;
-    }
-    __syncthreads();
   }
-  for (int q = threadIdx.x; q < (int)BC; q += OT_THREADS) a.y_out[q] = a.y[q];
-  if (threadIdx.x == 0) {
+  if (p == 0 && valid && half == 0) store_row10(a.y_out + (size_t)b * C, y);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.stats[0] = 4 * (a.niters - 1);
     a.stats[1] = a.niters - 1;
-    a.stats[2] = *last_exit;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// backward: VJP of one eval for the wave's 32 rows.  g: dL/dk (per lane, its row); returns
-// dL/d(stage input) in gy_out.
-__device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[4][5], int e,
-                       int b, bool valid, int half, int col, const float (&g)[C], float (&gy_out)[C]) {
+// backward: one workgroup per 32-row tile, 4 waves = 4 parts of the hidden dimension.  Every
+// wave runs the row math (QP backward, rescale, barrier terms) and g_a2 = Q3^T g_ft in full
+// (identical values in all 4 waves), then its 32 of the 128 rows of g_a1 = Q2^T g_z2 (64 MFMA)
+// and their Q1^T partial; the 4 partials of g_h meet in LDS (double-buffered, one barrier per
+// VJP) and every wave sums them in the same order, so the adjoint state stays replicated.
+struct OtBwdShared {
+  float gpart[2][4][64][6];
+};
+
+__device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[4][5],
+                       OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int half, int col,
+                       const float (&g)[C], float (&gy_out)[C]) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
   float h[C], ft[C], v[C], lower[C], nominal[C], sig[C], span[C];
@@ -243,11 +398,11 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
     // lower = -a1 (exp(s1 h) - 1), upper = a2 (1 - h)
     ghb[j] = ((g_lo * -a.d.alpha_1) * expf(a.d.sigma_1 * h[j])) * a.d.sigma_1 + g_up * -a.d.alpha_2;
   }
-  if (valid && half == 0) {
+  if (p == 0 && valid && half == 0) {
     store_row10(a.gft + r * C, gft);
     if (a.dbg_gft) store_row10(a.dbg_gft + r * C, gft);
   }
-  // g_a2^T = Q3^T g_ft^T, masked by the saved post-activation a2 (> 0 <=> kept and positive)
+  // g_a2^T = Q3^T g_ft^T (all 128 rows), masked by the saved post-activation a2
   f32x16 ga[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) ga[mb] = f16_zero();
@@ -263,52 +418,54 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
     load_acc_rows(a.a2 + r * M, mb, half, act);
 #pragma unroll
     for (int q = 0; q < 16; ++q) ga[mb][q] = act[q] > 0.f ? ga[mb][q] * a.drop_scale : 0.f;
-    if (valid) store_acc_rows(a.gz2 + r * M, mb, half, ga[mb]);
+    if (valid && mb == p) store_acc_rows(a.gz2 + r * M, mb, half, ga[mb]);
   }
-  // g_a1^T = Q2^T g_z2^T
-  f32x16 gb[4];
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb) gb[mb] = f16_zero();
+  // rows 32p.. of g_a1^T = Q2^T g_z2^T
+  f32x16 gb = f16_zero();
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg)
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(Q2Ts + (32 * p + col) * LDQ + 32 * kb + 8 * gg + 4 * half);
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        const f32x4 q = *reinterpret_cast<const f32x4*>(Q2Ts + (32 * mb + col) * LDQ + 32 * kb + 8 * gg + 4 * half);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) gb[mb] = mfma32(q[t], ga[kb][4 * gg + t], gb[mb]);
-      }
+      for (int t = 0; t < 4; ++t) gb = mfma32(q[t], ga[kb][4 * gg + t], gb);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  {
     f32x16 act;
-    load_acc_rows(a.a1 + r * M, mb, half, act);
+    load_acc_rows(a.a1 + r * M, p, half, act);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) gb[mb][q] = act[q] > 0.f ? gb[mb][q] * a.drop_scale : 0.f;
-    if (valid) store_acc_rows(a.gz1 + r * M, mb, half, gb[mb]);
+    for (int q = 0; q < 16; ++q) gb[q] = act[q] > 0.f ? gb[q] * a.drop_scale : 0.f;
+    if (valid) store_acc_rows(a.gz1 + r * M, p, half, gb);
   }
-  // g_h^T (10 x 32, padded to 32 rows) = Q1^T g_z1^T
+  // partial g_h^T over hidden rows 32p.. (Q1^T image padded to 32 output rows)
   f32x16 gh = f16_zero();
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
+  for (int gg = 0; gg < 4; ++gg) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(Q1Ts + col * LDQ + 32 * p + 8 * gg + 4 * half);
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const f32x4 q = *reinterpret_cast<const f32x4*>(Q1Ts + col * LDQ + 32 * kb + 8 * gg + 4 * half);
+    for (int t = 0; t < 4; ++t) gh = mfma32(q[t], gb[4 * gg + t], gh);
+  }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) gh = mfma32(q[t], gb[kb][4 * gg + t], gh);
-    }
+  for (int q = 0; q < 6; ++q) sh.gpart[buf][p][lane][q] = gh[q];
+  __syncthreads();
+  f32x16 gs = f16_zero();
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    gs[q] = ((sh.gpart[buf][0][lane][q] + sh.gpart[buf][1][lane][q]) + sh.gpart[buf][2][lane][q]) +
+            sh.gpart[buf][3][lane][q];
   float ghm[C];
-  gather_ft(gh, half, ghm);
+  gather_ft(gs, half, ghm);
 #pragma unroll
   for (int j = 0; j < C; ++j) gy_out[j] = ghm[j] + ghb[j];
 }
 
-__global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
+__global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2Ts = smem;                 // Q2^T image [128][LDQ]
   float* Q1Ts = smem + M * LDQ;       // Q1^T image [32][LDQ] (rows >= 10 zero)
+  OtBwdShared& sh = *reinterpret_cast<OtBwdShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
   for (int q = threadIdx.x; q < 32 * M; q += blockDim.x) {
     const int c = q >> 7, i = q & 127;
@@ -316,6 +473,7 @@ __global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float q3t[4][5];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
@@ -329,6 +487,7 @@ __global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
 #pragma unroll
     for (int j = 0; j < C; ++j) gy[j] = 0.f;
   const float third = 1.0f / 3.0f;
+  int buf = 0;
   for (int it = a.niters - 2; it >= 0; --it) {
     float ta, dt;
     step_times(a, it, ta, dt);
@@ -343,7 +502,8 @@ __global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
       gk4[j] = gy[j] * c8;
     }
     const int e0 = 4 * it;
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, e0 + 3, b, valid, half, col, gk4, gY);   // Y4 = y + dt (k1 - k2 + k3)
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 3, b, valid, lane, half, col, gk4, gY);  // Y4 = y + dt (k1 - k2 + k3)
+    buf ^= 1;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       acc[j] += gY[j];
@@ -352,7 +512,8 @@ __global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
       gk2[j] -= d;
       gk3[j] += d;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, e0 + 2, b, valid, half, col, gk3, gY);   // Y3 = y + dt (k2 - k1/3)
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 2, b, valid, lane, half, col, gk3, gY);  // Y3 = y + dt (k2 - k1/3)
+    buf ^= 1;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       acc[j] += gY[j];
@@ -360,13 +521,15 @@ __global__ __launch_bounds__(64) void k_ot_bwd(OTArgs a) {
       gk2[j] += d;
       gk1[j] -= d * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, e0 + 1, b, valid, half, col, gk2, gY);   // Y2 = y + (dt k1) / 3
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 1, b, valid, lane, half, col, gk2, gY);  // Y2 = y + (dt k1) / 3
+    buf ^= 1;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       acc[j] += gY[j];
       gk1[j] += (dt * gY[j]) * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, e0, b, valid, half, col, gk1, gY);       // Y1 = y
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0, b, valid, lane, half, col, gk1, gY);      // Y1 = y
+    buf ^= 1;
 #pragma unroll
     for (int j = 0; j < C; ++j) gy[j] = acc[j] + gY[j];
   }
@@ -383,7 +546,7 @@ int grid_iters(const fiode_odetrain_config* cfg) {
 }
 
 struct OtLayout {
-  size_t u, y, k, hs, ftw, vw, muw, nomw, a1, a2, gz2, gz1, gft, wg, total;
+  size_t u, y, k, hs, ftw, vw, muw, nomw, a1, a2, gz2, gz1, gft, xs, kw, wg, total;
 };
 OtLayout ot_layout(int B, int E) {
   OtLayout L;
@@ -402,6 +565,8 @@ OtLayout ot_layout(int B, int E) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
+  L.xs = o; o += al((size_t)E * ((B + 31) / 32) * 8 + 256);
+  L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
   L.total = o;
   return L;
@@ -446,6 +611,11 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.gz2 = reinterpret_cast<float*>(ws + L.gz2);
   a.gz1 = reinterpret_cast<float*>(ws + L.gz1);
   a.gft = reinterpret_cast<float*>(ws + L.gft);
+  a.xslots = reinterpret_cast<unsigned long long*>(ws + L.xs);
+  a.kw = reinterpret_cast<uint32_t*>(ws + L.kw);
+#ifdef OT_PROFILE
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * ((a.B + 31) / 32) + 8;
+#endif
   return FIODE_OK;
 }
 
@@ -485,8 +655,16 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   if (a.dropout_mode == FIODE_DROPOUT_GIVEN && !masks) return FIODE_EINVAL;
   a.h0 = h0; a.masks = masks; a.offset_dev = offset_dev; a.y_out = y_out; a.stats = stats;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + 16;
-  hipLaunchKernelGGL(k_ot_fwd, dim3(1), dim3(OT_THREADS), lds, st, a);
+  const int ntiles = (a.B + 31) / 32;
+  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);
+  // zero the exchange granules (tags) and the status word before every launch
+  FIODE_HIP_CHECK(hipMemsetAsync(a.xslots, 0, (size_t)a.E * ntiles * 8 + 256, st));
+  FIODE_HIP_CHECK(hipMemsetAsync(stats, 0, 8 * sizeof(int32_t), st));
+  if (a.dropout_mode != FIODE_DROPOUT_OFF) {
+    hipLaunchKernelGGL(k_ot_masks, dim3((a.E * a.B + 255) / 256), dim3(256), 0, st, a);
+    FIODE_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_ot_fwd, dim3(ntiles), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }
@@ -503,8 +681,8 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
     return FIODE_EINVAL;
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float);
-  hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + 31) / 32), dim3(64), lds, st, a);
+  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtBwdShared);
+  hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + 31) / 32), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const OtLayout L = ot_layout(a.B, a.E);
   fiode_internal::WgradIO io{};

@@ -50,7 +50,7 @@ def test_forward_matches_oracle(B, step, scale_nominal):
                                      masks=torch.from_numpy(masks).to(dev))
     torch.cuda.synchronize()
     s = st.cpu().numpy()
-    assert s[0] == E and s[1] == E // 4
+    assert s[0] == E and s[1] == E // 4 and s[3] == 0
     err = float(np.abs(y.cpu().numpy() - ref).max())
     assert err <= 2e-4, err
     sv = ops.odetrain_saved(ws, cfg)

@@ -1,0 +1,32 @@
+"""Phase timing of k_ot_fwd (needs tools/libfiode_prof.so built with -DOT_PROFILE; not a test)."""
+import ctypes as ct, os, sys, pathlib
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+os.environ["FIODE_LIB"] = str(ROOT / "tools" / "libfiode_prof.so")
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import numpy as np, torch
+from fiode_amd import _lib as L, ops
+from tests._util import make_params
+dev = torch.device("cuda:0")
+P = make_params(1)
+w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
+for B in (128, 1024):
+    x = torch.randn(B, 10, device=dev); h0 = torch.full((B, 10), 0.1, device=dev)
+    cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=3)
+    dyn = ops.DynCfg(scale_nominal=False, dropout=0.5)
+    for rep in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(); y, st, ws = ops.odetrain_forward(x, h0, w, dyn, cfg); e1.record(); torch.cuda.synchronize()
+    E = ops.odetrain_evals(cfg); nt = (B + 31) // 32
+    off = ct.c_int64 * 8
+    # prof array sits after the exchange granules
+    lib = L.lib()
+    offs = (ct.c_int64 * 8)()
+    # xslots offset = gft offset + al(R*C*4)
+    lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
+    al = lambda v: (v + 255) & ~255
+    xs = offs[7] + al(B * E * 10 * 4)
+    prof = ws[xs + (E * nt + 8) * 8: xs + (E * nt + 16) * 8].view(torch.int64).cpu().numpy()
+    ticks = prof[:5] / E          # 100 MHz wall clock -> 10 ns per tick
+    print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): layer1 {ticks[0]*0.01:.2f} "
+          f"layer2+3 {ticks[1]*0.01:.2f} sum+QP {ticks[2]*0.01:.2f} exchange {ticks[3]*0.01:.2f} "
+          f"final {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
