@@ -61,6 +61,85 @@ class _CayleyInverse(torch.autograd.Function):
         return -(ih @ g @ ih)
 
 
+class _CayleyScaledFn(torch.autograd.Function):
+    """Q = cayley(alpha * W / ||W||) with an analytic backward (one autograd node instead of the
+    ~40 of the op-by-op graph).  W: [..., cout, cin] real or complex; the norm is over the whole
+    tensor (``per_matrix`` False: CayleyConv's one alpha for all frequencies) or over each matrix
+    (True: several same-shape linears batched, alpha [batch]).  Wide maps go through the transpose.
+
+    Forward, with X = s W (s = alpha / ||W||), U = X[:cin], V = X[cin:]:
+        M = I + U - U^H + V^H V,  inv = M^-1,  Q = [2 inv - I ; -2 V inv].
+    Backward, G = dL/dQ = [Gt ; Gb]:
+        G_inv = 2 Gt - 2 V^H Gb,  G_M = -inv^H G_inv inv^H,
+        dL/dU = G_M - G_M^H,      dL/dV = V (G_M + G_M^H) - 2 Gb inv^H,
+        D = Re<dL/dX, W>,  dL/dW = s dL/dX - alpha D / ||W||^3 W,  dL/dalpha = D / ||W||."""
+
+    @staticmethod
+    def forward(ctx, W, alpha, per_matrix: bool):
+        Wd = W.detach()
+        if per_matrix:
+            n = torch.linalg.vector_norm(Wd, dim=(-2, -1), keepdim=True)
+            s = alpha.detach().reshape(n.shape) / n
+        else:
+            n = torch.linalg.vector_norm(Wd)
+            s = alpha.detach().reshape(()) / n
+        X = Wd * s
+        wide = X.shape[-1] > X.shape[-2]
+        if wide:
+            X = X.mT
+        cin = X.shape[-1]
+        tall = X.shape[-2] > cin
+        U, V = X[..., :cin, :], X[..., cin:, :]
+        M = U - U.mH
+        if tall:
+            M = M + V.mH @ V
+        M.diagonal(dim1=-2, dim2=-1).add_(1.0)
+        inv = _block_inverse(M.contiguous())
+        top = inv * 2.0
+        top.diagonal(dim1=-2, dim2=-1).sub_(1.0)
+        Q = torch.cat([top, (V @ inv).mul_(-2.0)], dim=-2) if tall else top
+        ctx.save_for_backward(Wd, alpha, n, s, inv, V if tall else None)
+        ctx.flags = (wide, tall, per_matrix, cin)
+        return Q.mT if wide else Q
+
+    @staticmethod
+    def backward(ctx, G):
+        Wd, alpha, n, s, inv, V = ctx.saved_tensors
+        wide, tall, per_matrix, cin = ctx.flags
+        if wide:
+            G = G.mT
+        ih = inv.mH
+        Gt = G[..., :cin, :]
+        if tall:
+            Gb = G[..., cin:, :]
+            Ginv = 2.0 * Gt - 2.0 * (V.mH @ Gb)
+        else:
+            Ginv = 2.0 * Gt
+        GM = -(ih @ Ginv @ ih)
+        gU = GM - GM.mH
+        if tall:
+            gV = V @ (GM + GM.mH) - 2.0 * (Gb @ ih)
+            gX = torch.cat([gU, gV], dim=-2)
+        else:
+            gX = gU
+        if wide:
+            gX = gX.mT
+        prod = gX.conj() * Wd if gX.is_complex() else gX * Wd
+        if per_matrix:
+            D = prod.real.sum(dim=(-2, -1), keepdim=True) if prod.is_complex() else prod.sum(dim=(-2, -1), keepdim=True)
+        else:
+            D = prod.real.sum() if prod.is_complex() else prod.sum()
+        a = alpha.reshape(n.shape)
+        gW = s * gX - (a * D / (n * n * n)) * Wd
+        galpha = (D / n).reshape(alpha.shape)
+        return gW, galpha, None
+
+
+def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False) -> torch.Tensor:
+    """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293)."""
+    return _CayleyScaledFn.apply(W, alpha, per_matrix)
+
+
 def cayley(W: torch.Tensor) -> torch.Tensor:
     """Orthogonal (or orthonormal-column) matrix from an unconstrained W [.., cout, cin]:
     with U = W[:cin], V = W[cin:], A = U - U^H + V^H V:
@@ -100,7 +179,7 @@ class CayleyLinear(nn.Linear):
         self._Q = None
 
     def effective_weight(self) -> torch.Tensor:
-        return cayley(self.alpha * self.weight / self.weight.norm())
+        return cayley_scaled(self.weight, self.alpha)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.training or self._Q is None:
@@ -108,10 +187,29 @@ class CayleyLinear(nn.Linear):
         return F.linear(x, self._Q if self.training else self._Q.detach(), self.bias)
 
 
+class _GroupSortFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        from . import ops
+        y = ops.groupsort_forward(x)
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import ops
+        x, = ctx.saved_tensors
+        return ops.groupsort_backward(x, g)
+
+
 class GroupSort(nn.Module):
-    """Sort pairs of channel halves: [max(a, b), min(a, b)] along dim 1."""
+    """Sort pairs of channel halves: [max(a, b), min(a, b)] along dim 1.  On ROCm tensors one HIP
+    kernel each way (fiode_groupsort_*; ties split the gradient like torch.maximum); host tensors
+    take the torch ops."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            return _GroupSortFn.apply(x)
         a, b = x.split(x.size(1) // 2, 1)
         return torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=1)
 
@@ -158,7 +256,7 @@ class CayleyConv(nn.Conv2d):
             with torch.no_grad():
                 self.alpha.fill_(float(wf.norm()))
             self._alpha_init = True
-        yf = (cayley(self.alpha * wf / wf.norm()) @ xf).reshape(n, n // 2 + 1, cout, B)
+        yf = (cayley_scaled(wf, self.alpha) @ xf).reshape(n, n // 2 + 1, cout, B)
         y = torch.fft.irfft2(yf.permute(3, 2, 0, 1), s=(n, n))
         if self.bias is not None:
             y = y + self.bias[:, None, None]

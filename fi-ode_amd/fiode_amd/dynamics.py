@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .cayley import CayleyLinear
+from .cayley import CayleyLinear, cayley_scaled
 
 
 class LipsLinear(nn.Linear):
@@ -62,7 +62,17 @@ class OrthoClassDynProjectSimplexLips(nn.Module):
 
     # -- parameters as the kernels take them ---------------------------------------------------
     def effective_weights(self) -> Dict[str, torch.Tensor]:
-        """Q = cayley(alpha W / ||W||) for each layer (differentiable), with the biases."""
+        """Q = cayley(alpha W / ||W||) for each layer (differentiable), with the biases.  The three
+        128x10-shaped maps (hidden_to_mlp, U_x and the transpose of mlp_to_hidden) run as one
+        batched Cayley map (per-matrix norms and alphas); mlp_to_mlp on its own."""
+        if self.cayley:
+            l1, lx, l3 = self.hidden_to_mlp, self.U_x, self.mlp_to_hidden
+            Wb = torch.stack([l1.weight, lx.weight, l3.weight.t()])
+            ab = torch.cat([l1.alpha, lx.alpha, l3.alpha])
+            Qb = cayley_scaled(Wb, ab, per_matrix=True)
+            return {"Q1": Qb[0], "b1": l1.bias, "Qx": Qb[1], "bx": lx.bias,
+                    "Q2": self.mlp_to_mlp.effective_weight(), "b2": self.mlp_to_mlp.bias,
+                    "Q3": Qb[2].t(), "b3": l3.bias}
         return {"Q1": self.hidden_to_mlp.effective_weight(), "b1": self.hidden_to_mlp.bias,
                 "Qx": self.U_x.effective_weight(), "bx": self.U_x.bias,
                 "Q2": self.mlp_to_mlp.effective_weight(), "b2": self.mlp_to_mlp.bias,

@@ -373,3 +373,31 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     L.check(L.lib().fiode_batched_inverse(_stream(M.device), dt, batch, n, M.data_ptr(), n * n, out.data_ptr(),
                                           n * n), "fiode_batched_inverse")
     return out
+
+
+def _gs_shape(x: torch.Tensor):
+    if x.device.type != "cuda" or x.dtype != torch.float32:
+        raise ValueError(f"groupsort: float32 ROCm tensor expected, got {x.dtype} on {x.device}")
+    B, Cc = x.shape[0], x.shape[1]
+    S = x[0, 0].numel() if x.dim() > 2 else 1
+    if Cc % 2 or ((Cc // 2) * S) % 4:
+        raise ValueError(f"groupsort: shape {tuple(x.shape)} needs even C and (C/2)*S % 4 == 0")
+    return B, Cc, S
+
+
+def groupsort_forward(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    B, Cc, S = _gs_shape(x)
+    y = torch.empty_like(x)
+    L.check(L.lib().fiode_groupsort_forward(_stream(x.device), B, Cc, S, x.data_ptr(), y.data_ptr()),
+            "fiode_groupsort_forward")
+    return y
+
+
+def groupsort_backward(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    x, g = x.contiguous(), g.contiguous()
+    B, Cc, S = _gs_shape(x)
+    gx = torch.empty_like(x)
+    L.check(L.lib().fiode_groupsort_backward(_stream(x.device), B, Cc, S, x.data_ptr(), g.data_ptr(), gx.data_ptr()),
+            "fiode_groupsort_backward")
+    return gx

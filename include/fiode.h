@@ -238,6 +238,13 @@ FIODE_API int fiode_certify(void* stream, const fiode_certify_config* cfg, const
 FIODE_API int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch, int32_t n, const void* in,
                                     int64_t in_stride, void* out, int64_t out_stride);
 
+/* ---- Backbone GroupSort (KWLarge_Concat activation; absent libs/ortho_conv, restated) --------
+ * x, y: [B][C][S] float32 (S = spatial size, 1 for linear layers); C even, (C/2)*S % 4 == 0.
+ * y = cat(max(x[:, :C/2], x[:, C/2:]), min(...)); backward splits ties in half (torch.maximum). */
+FIODE_API int fiode_groupsort_forward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, float* y);
+FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, const float* g,
+                                       float* gx);
+
 /* Error text for a return code. */
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);

@@ -108,3 +108,67 @@ def test_inverse_rejects_bad_inputs():
         ops.batched_inverse(torch.eye(4, device=dev, dtype=torch.float64))
     with pytest.raises(ValueError):
         ops.batched_inverse(torch.eye(4))
+
+
+@pytest.mark.parametrize("shape", [(128, 32, 32, 32), (5, 64, 8, 8), (128, 512), (3, 8)])
+def test_groupsort_matches_torch_ops(shape):
+    """fiode_groupsort_* vs torch.maximum/minimum + cat and their autograd (ties included)."""
+    from fiode_amd.cayley import GroupSort
+    dev = _dev()
+    x = torch.randn(*shape, device=dev)
+    x = torch.where(torch.rand_like(x) < 0.05, torch.zeros_like(x), x)      # ties between halves
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    y = GroupSort()(xa)
+    a, b = xb.split(shape[1] // 2, 1)
+    ref = torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=1)
+    assert torch.equal(y, ref)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref.backward(g)
+    assert torch.equal(xa.grad, xb.grad)
+
+
+def _cayley_autograd_reference(W, alpha, per_matrix):
+    """The op-by-op formula through torch.linalg.inv (float64), differentiated by autograd."""
+    if per_matrix:
+        n = torch.linalg.vector_norm(W, dim=(-2, -1), keepdim=True)
+        X = alpha.reshape(n.shape) * W / n
+    else:
+        X = alpha * W / W.norm()
+    wide = X.shape[-1] > X.shape[-2]
+    if wide:
+        X = X.mT
+    cin = X.shape[-1]
+    U, V = X[..., :cin, :], X[..., cin:, :]
+    eye = torch.eye(cin, dtype=X.dtype, device=X.device)
+    inv = torch.linalg.inv(eye + U - U.mH + V.mH @ V)
+    Q = torch.cat([inv @ (eye - (U - U.mH + V.mH @ V)), -2.0 * (V @ inv)], dim=-2)
+    return Q.mT if wide else Q
+
+
+@pytest.mark.parametrize("shape,dtype,per_matrix", [
+    ((128, 10), torch.float32, False), ((10, 128), torch.float32, False), ((128, 128), torch.float32, False),
+    ((512, 4096), torch.float32, False), ((3, 128, 10), torch.float32, True),
+    ((144, 32, 128), torch.complex64, False), ((40, 64, 64), torch.complex64, False),
+    ((544, 32, 3), torch.complex64, False)])
+def test_cayley_scaled_forward_backward(shape, dtype, per_matrix):
+    """_CayleyScaledFn (one node, analytic backward) vs autograd of the plain formula in float64."""
+    from fiode_amd.cayley import cayley_scaled
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    W = torch.randn(shape, generator=g, dtype=torch.complex64 if dtype.is_complex else torch.float32).to(dev)
+    nb = shape[0] if per_matrix else 1
+    alpha = (torch.rand(nb, generator=g) * 3 + 0.5).to(dev)
+    Wa, aa = W.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+    Q = cayley_scaled(Wa, aa, per_matrix)
+    wdt = torch.complex128 if dtype.is_complex else torch.float64
+    Wb, ab = W.to(wdt).requires_grad_(True), alpha.double().requires_grad_(True)
+    Qr = _cayley_autograd_reference(Wb, ab, per_matrix)
+    assert float((Q.to(wdt) - Qr).abs().max()) < 2e-5
+    G = torch.randn(Q.shape, generator=g, dtype=Q.dtype).to(dev)
+    (Q * G.conj()).real.sum().backward() if dtype.is_complex else (Q * G).sum().backward()
+    (Qr * G.to(wdt).conj()).real.sum().backward() if dtype.is_complex else (Qr * G.to(wdt)).sum().backward()
+    for got, ref in ((Wa.grad, Wb.grad), (aa.grad, ab.grad)):
+        scale = float(ref.abs().max()) + 1e-12
+        assert float((got.to(ref.dtype) - ref).abs().max()) / scale < 1e-4
