@@ -162,6 +162,28 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
     return torch.cat([top, -2.0 * (V @ inv)], dim=-2)
 
 
+def _prefetch(stream: torch.cuda.Stream, fn):
+    """Run fn() on `stream` (forked from the current stream); returns (result, done event)."""
+    main = torch.cuda.current_stream(stream.device)
+    stream.wait_stream(main)
+    with torch.cuda.stream(stream):
+        out = fn()
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return out, ev
+
+
+def _take(pre):
+    """Join a prefetched result into the current stream."""
+    out, ev = pre
+    main = torch.cuda.current_stream()
+    main.wait_event(ev)
+    for t in (out.values() if isinstance(out, dict) else (out,)):
+        if isinstance(t, torch.Tensor):
+            t.record_stream(main)
+    return out
+
+
 class CayleyLinear(nn.Linear):
     """nn.Linear whose effective weight is cayley(alpha * W / ||W||_F) (state_dict keys
     ``weight``, ``bias``, ``alpha``, as the reference's checkpoints carry)."""
@@ -170,6 +192,7 @@ class CayleyLinear(nn.Linear):
         super().__init__(in_features, out_features, bias)
         self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
         self._Q = None
+        self._pre = None
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -181,8 +204,16 @@ class CayleyLinear(nn.Linear):
     def effective_weight(self) -> torch.Tensor:
         return cayley_scaled(self.weight, self.alpha)
 
+    def prefetch(self, stream: torch.cuda.Stream) -> None:
+        """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
+        the layers before it); the next training forward joins it."""
+        self._pre = _prefetch(stream, self.effective_weight)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.training or self._Q is None:
+        if self._pre is not None and self.training:
+            self._Q = _take(self._pre)
+            self._pre = None
+        elif self.training or self._Q is None:
             self._Q = self.effective_weight()
         return F.linear(x, self._Q if self.training else self._Q.detach(), self.bias)
 
@@ -227,6 +258,8 @@ class CayleyConv(nn.Conv2d):
         self.alpha = nn.Parameter(torch.ones(1))
         self._alpha_init = False
         self._shift = {}
+        self._n = None
+        self._pre = None
 
     def _load_from_state_dict(self, *args, **kw):
         super()._load_from_state_dict(*args, **kw)
@@ -242,6 +275,25 @@ class CayleyConv(nn.Conv2d):
             self._shift[key] = sh.reshape(n * (n // 2 + 1), 1, 1).to(torch.complex64)
         return self._shift[key]
 
+    def spectral_weight(self, n: int, device) -> torch.Tensor:
+        """The per-frequency orthogonal channel matrices Q [n (n/2+1), cout, cin] for n x n inputs."""
+        cout, cin = self.weight.shape[:2]
+        nf = n * (n // 2 + 1)
+        wf = torch.fft.rfft2(self.weight, (n, n)).reshape(cout, cin, nf).permute(2, 0, 1).conj()
+        wf = self._shift_matrix(n, device) * wf
+        if not self._alpha_init:
+            with torch.no_grad():
+                self.alpha.fill_(float(wf.norm()))
+            self._alpha_init = True
+        return cayley_scaled(wf, self.alpha)
+
+    def prefetch(self, stream: torch.cuda.Stream) -> None:
+        """Compute this step's spectral Cayley maps on a side stream (needs one forward first, to
+        know the input size and initialise alpha)."""
+        if self._n is not None and self._alpha_init:
+            n = self._n
+            self._pre = _prefetch(stream, lambda: self.spectral_weight(n, self.weight.device))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.downsample:
             b, c, h, w = x.shape
@@ -250,13 +302,13 @@ class CayleyConv(nn.Conv2d):
         B, _, n, _ = x.shape
         nf = n * (n // 2 + 1)
         xf = torch.fft.rfft2(x).permute(2, 3, 1, 0).reshape(nf, cin, B)
-        wf = torch.fft.rfft2(self.weight, (n, n)).reshape(cout, cin, nf).permute(2, 0, 1).conj()
-        wf = self._shift_matrix(n, x.device) * wf
-        if not self._alpha_init:
-            with torch.no_grad():
-                self.alpha.fill_(float(wf.norm()))
-            self._alpha_init = True
-        yf = (cayley_scaled(wf, self.alpha) @ xf).reshape(n, n // 2 + 1, cout, B)
+        if self._pre is not None and self.training and self._n == n:
+            Q = _take(self._pre)
+        else:
+            Q = self.spectral_weight(n, x.device)
+        self._pre = None
+        self._n = n
+        yf = (Q @ xf).reshape(n, n // 2 + 1, cout, B)
         y = torch.fft.irfft2(yf.permute(3, 2, 0, 1), s=(n, n))
         if self.bias is not None:
             y = y + self.bias[:, None, None]

@@ -61,7 +61,20 @@ class OrthoClassDynProjectSimplexLips(nn.Module):
         self.U_x = lin(x_dim, mlp_size)
 
     # -- parameters as the kernels take them ---------------------------------------------------
+    def prefetch(self, stream) -> None:
+        """Compute the next effective_weights() on a side stream (joined at the next call)."""
+        from .cayley import _prefetch
+        self._pre = _prefetch(stream, self._effective_weights)
+
     def effective_weights(self) -> Dict[str, torch.Tensor]:
+        pre = getattr(self, "_pre", None)
+        if pre is not None:
+            from .cayley import _take
+            self._pre = None
+            return _take(pre)
+        return self._effective_weights()
+
+    def _effective_weights(self) -> Dict[str, torch.Tensor]:
         """Q = cayley(alpha W / ||W||) for each layer (differentiable), with the biases.  The three
         128x10-shaped maps (hidden_to_mlp, U_x and the transpose of mlp_to_hidden) run as one
         batched Cayley map (per-matrix norms and alphas); mlp_to_mlp on its own."""

@@ -145,6 +145,8 @@ class LyapunovLearning(nn.Module):
         self.seed = seed
         self._rng_offset = 0
         self.rng_counter: Optional[torch.Tensor] = None   # device step counter (graph replay)
+        self.parallel_cayley = True     # Cayley maps of the step on side streams (training, ROCm)
+        self._side_streams = None
         self.logged: Dict[str, float] = {}
         self._out = None
 
@@ -246,10 +248,30 @@ class LyapunovLearning(nn.Module):
         self._rng_offset += 1
         return plan
 
+    def _prefetch_weights(self, device):
+        """Launch every Cayley map of the step (backbone convs / linears, dynamics) on side streams
+        before the backbone runs: they depend only on the weights, and their inverses are
+        latency-bound single-workgroup kernels, so they overlap each other and the convolutions.
+        Layers join them when they reach them (autograd runs their backward on the same streams)."""
+        if self._side_streams is None:
+            self._side_streams = [torch.cuda.Stream(device) for _ in range(4)]
+        s = self._side_streams
+        convs, lins = [], []
+        for m in self.init_coordinates.modules():
+            if hasattr(m, "prefetch") and m is not self.dyn_fun:
+                (convs if hasattr(m, "spectral_weight") else lins).append(m)
+        for c in convs:
+            c.prefetch(s[0])
+        for i, l in enumerate(lins):
+            l.prefetch(s[1 + min(i, 2)])
+        self.dyn_fun.prefetch(s[3])
+
     def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
         """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""
         if self.current_epoch == self.epoch_off_scale:
             self.dyn_fun.scale_nominal = False
+        if self.parallel_cayley and self.training and x.is_cuda and self.dyn_fun.cayley:
+            self._prefetch_weights(x.device)
         static_state, _ = self.init_coordinates(x, self.dyn_fun)
         plan = self.step_plan(y, h=h, masks=masks, debug=debug)
         w = self.dyn_fun.effective_weights()
