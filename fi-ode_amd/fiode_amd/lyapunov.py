@@ -275,6 +275,9 @@ class LyapunovLearning(nn.Module):
         static_state, _ = self.init_coordinates(x, self.dyn_fun)
         plan = self.step_plan(y, h=h, masks=masks, debug=debug)
         w = self.dyn_fun.effective_weights()
+        ode_on = self.train_ode and self.current_epoch > self.train_ode_epoch
+        if ode_on:        # launched first: on ROCm it runs on a side stream beside the fan-out kernels
+            y_hat = self._ode_launch(static_state.float(), w)
         loss = LyapunovLossFn.apply(static_state.float(), w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"],
                                     w["Q3"], w["b3"], y, plan)
         sc = plan["scalars"]
@@ -282,8 +285,8 @@ class LyapunovLearning(nn.Module):
         self.log("effective_batch_size", sc[1])
         self.log("mean_active_constraints", sc[2])
         self.last_plan = plan
-        if self.train_ode and self.current_epoch > self.train_ode_epoch:
-            return self._ode_loss(loss, static_state.float(), w, y)
+        if ode_on:
+            return self._ode_loss(loss, y_hat, y)
         return loss
 
     def ode_plan(self, batch: int, masks: Optional[torch.Tensor] = None) -> dict:
@@ -301,14 +304,27 @@ class LyapunovLearning(nn.Module):
                                   offset=self._rng_offset if self.rng_counter is None else 0)
         return dict(dyn=self.dyn_fun.dyn_cfg(), cfg=cfg, masks=masks, offset_dev=self.rng_counter)
 
-    def _ode_loss(self, loss, static_state, w, y, masks=None):
-        """pl_modules.py:490-500.  The reference re-runs the backbone inside self.model(x); the
-        backbone is deterministic (no dropout / batch norm), so static_state is reused."""
+    def _ode_launch(self, static_state, w, masks=None):
+        """The train_ode solve (pl_modules.py:490-493).  The reference re-runs the backbone inside
+        self.model(x); the backbone is deterministic (no dropout / batch norm), so static_state is
+        reused.  Its persistent kernel occupies B/32 CUs for the whole solve, so on ROCm it is
+        launched on a side stream and overlaps the fan-out kernels."""
         h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
         plan = self.ode_plan(static_state.shape[0], masks)
-        y_hat = ODETrainFn.apply(static_state, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
-                                 w["b3"], h0, plan)
+        args = (static_state, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"], w["b3"], h0, plan)
         self.last_ode_plan = plan
+        if static_state.is_cuda and self.parallel_cayley:
+            from .cayley import _prefetch
+            if getattr(self, "_ode_stream", None) is None:
+                self._ode_stream = torch.cuda.Stream(static_state.device)
+            return _prefetch(self._ode_stream, lambda: ODETrainFn.apply(*args))
+        return ODETrainFn.apply(*args)
+
+    def _ode_loss(self, loss, y_hat, y):
+        """pl_modules.py:494-500: loss * (1 - p) + nll(log y_hat) * p."""
+        if isinstance(y_hat, tuple):
+            from .cayley import _take
+            y_hat = _take(y_hat)
         if self.simplex:
             loss_ode = F.nll_loss(torch.log(y_hat), y)
         else:

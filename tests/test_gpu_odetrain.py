@@ -117,5 +117,6 @@ def test_module_train_ode_loss_mix():
     for name, prm in mod.named_parameters():
         if prm.requires_grad:
             assert prm.grad is not None and torch.isfinite(prm.grad).all(), name
+    torch.cuda.synchronize()
     s = mod.last_ode_plan["stats"].cpu()
     assert int(s[0]) == 40 and int(s[1]) == 10
