@@ -150,7 +150,7 @@ def main():
         y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
         from fiode_amd.distributed import GradAllReducer, MetricReducer, broadcast_parameters
         broadcast_parameters(mod)                   # DDP's construction-time broadcast
-        reducer = GradAllReducer(params)            # p.grad are views into one flat bucket
+        reducer = GradAllReducer(params) if world > 1 else None   # p.grad = views into one flat bucket
         metrics = MetricReducer(["training_loss", "effective_batch_size", "mean_active_constraints"], dev)
 
         def sync_metrics():

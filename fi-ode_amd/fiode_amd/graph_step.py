@@ -41,10 +41,16 @@ class GraphTrainStep:
         if module.rng_counter is None:
             module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.params = [p for p in module.parameters() if p.requires_grad]
-        for p in self.params:            # persistent grads: autograd accumulates into them in place
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        self._grad_ptrs = [p.grad.data_ptr() for p in self.params]
+        # N ranks: persistent grads (views into the reducer's flat bucket), zeroed and accumulated
+        # in place.  One rank: grads are set to None before the backward, so autograd hands its
+        # result tensors over (no zero fills, no accumulate adds); inside the graph they come from
+        # the graph's private pool at fixed addresses.
+        self.persistent = world > 1
+        if self.persistent:
+            for p in self.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+        self._grad_ptrs = [p.grad.data_ptr() for p in self.params] if self.persistent else None
 
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -67,14 +73,21 @@ class GraphTrainStep:
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt):
                 self.opt.step()
-        if [p.grad.data_ptr() for p in self.params] != self._grad_ptrs:
+        if self.persistent and [p.grad.data_ptr() for p in self.params] != self._grad_ptrs:
             raise RuntimeError("autograd re-allocated .grad during capture; cannot replay into the bucket")
         self.scalars = module.last_plan["scalars"]
 
     def _fwd_bwd(self):
         m = self.module
-        for p in self.params:
-            p.grad.zero_()
+        if self.persistent:
+            if self.reducer is not None:
+                self.reducer.zero_grad()          # one fill of the flat bucket
+            else:
+                for p in self.params:
+                    p.grad.zero_()
+        else:
+            for p in self.params:
+                p.grad = None
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         loss.backward()
         m.rng_counter.add_(1)

@@ -1,0 +1,28 @@
+"""Busy/idle analysis of one replayed step from a rocprofv3 kernel trace (not a test)."""
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "k_ot_fwd" in r["Kernel_Name"]]
+# step boundaries: consecutive k_ot_fwd dispatches; take a late pair (graph replays)
+k = len(idx) // 2
+a, b = idx[k], idx[k + 1]
+# a step starts a bit before k_ot_fwd; use the window between two k_ot_fwd starts
+win = rows[a:b]
+t0, t1 = int(win[0]["Start_Timestamp"]), int(rows[b]["Start_Timestamp"])
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in win)
+busy, cur_s, cur_e = 0, None, None
+for s, e in iv:
+    if cur_e is None or s > cur_e:
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        cur_s, cur_e = s, e
+    else:
+        cur_e = max(cur_e, e)
+busy += cur_e - cur_s
+kt = sum(e - s for s, e in iv)
+print(f"window {(t1-t0)/1e3:.1f} us, {len(win)} kernels, busy(union) {busy/1e3:.1f} us, "
+      f"sum of kernel times {kt/1e3:.1f} us, queues {sorted(set(r['Queue_Id'] for r in win))}")
+# distribution of gaps on the main queue
+from collections import Counter
+q = Counter(r["Queue_Id"] for r in win)
+print("kernels per queue", dict(q))
