@@ -77,8 +77,10 @@ def build_module(dev, seed=0, train_ode=False):
     return mod.to(dev).train()
 
 
-def cpu_baseline(budget_s: float = 10.0, images: int = 16):
-    """The reference fan-out path restated op-for-op in torch (oracle/torch_ref.py) on host cores."""
+def cpu_baseline(budget_s: float = 10.0, images: int = 16, train_ode: bool = True):
+    """The reference path restated op-for-op in torch (oracle/torch_ref.py) on host cores: the
+    Lyapunov fan-out (jvp(DecisionBoundary, eval_dot) + QP + hinge + logging pass + backward) and,
+    for the configs[1] workload, the train-mode RK4 solve (10 steps, 40 f-evals) + its backward."""
     import numpy as np
     from oracle import torch_ref as T
     from tests._util import make_params, make_step_inputs
@@ -92,15 +94,28 @@ def cpu_baseline(budget_s: float = 10.0, images: int = 16):
     args = (tm(inp.h), tm(inp.x_feat), torch.from_numpy(inp.y), H_SAMPLE, W)
     kw = dict(scale_nominal=False, kappa=2.0, mask1=tm(inp.mask1), mask2=tm(inp.mask2), lmask1=tm(inp.lmask1),
               lmask2=tm(inp.lmask2))
-    T.step_with_grads(*args, **kw)
+    rng = np.random.default_rng(2)
+    ode_masks = torch.from_numpy((rng.random((40, 2, images, 128)) >= 0.5).astype(np.uint8))
+    h0 = torch.full((images, 10), 0.1)
+
+    def one():
+        T.step_with_grads(*args, **kw)
+        if train_ode:
+            leaves = {k: v.clone().requires_grad_(True) for k, v in W.items()}
+            xf = tm(inp.x_feat).clone().requires_grad_(True)
+            loss, _ = T.ode_train_loss(xf, h0, torch.from_numpy(inp.y), leaves, ode_masks, 0.0, 1.0, 0.1,
+                                       scale_nominal=False)
+            loss.backward()
+    one()
     n, t0 = 0, time.perf_counter()
     while n < 3 or time.perf_counter() - t0 < budget_s:
-        T.step_with_grads(*args, **kw)
+        one()
         n += 1
     dt = (time.perf_counter() - t0) / n
+    what = ("the fan-out path (jvp(DecisionBoundary, eval_dot) + QP + hinge + logging pass + backward)" +
+            (" + the train-mode RK4 solve (10 steps / 40 f-evals, autograd through the stages)" if train_ode else ""))
     return {"value": round(images / dt, 2), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps of B={images} x S={H_SAMPLE} rows (S1=204/S2=52) of the fan-out path "
-                      f"(jvp(DecisionBoundary, eval_dot) + QP + hinge + logging pass + backward) in "
+            "sample": f"{n} steps of B={images} images x S={H_SAMPLE} rows (S1=204/S2=52) of {what} in "
                       f"oracle/torch_ref.py, float32, {dt * 1e3:.1f} ms/step; backbone and optimizer excluded"}
 
 
@@ -270,7 +285,7 @@ def main():
            "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)},
            "lyapunov_only_step": lyap_only}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_budget, train_ode=train_ode)
     else:
         out["cpu_baseline"] = None
     if rank == 0:

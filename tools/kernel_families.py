@@ -29,5 +29,6 @@ for r in rows:
     f[0] += float(r["TotalDurationNs"]); f[1] += int(r["Calls"])
 tot = sum(v[0] for v in fam.values())
 for k, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
-    print(f"{t/1e3/steps:9.1f} us/step {c/steps:7.1f} calls/step  {100*t/tot:5.1f}%  {k}")
-print(f"total {tot/1e3/steps:.1f} us/step")
+    unit = "us/step" if steps != 1.0 else "us total"
+    print(f"{t/1e3/steps:9.1f} {unit} {c/steps:7.1f} calls  {100*t/tot:5.1f}%  {k}")
+print(f"total {tot/1e3/steps:.1f} us")

@@ -18,10 +18,15 @@ import sys
 from collections import defaultdict
 
 FUSED = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_wgrad", "k_lyap_reduce",
-         "k_lyap_static_grads", "k_ode", "k_dyn", "k_qp", "k_cert")
+         "k_lyap_static_grads", "k_ot_masks", "k_ot_fwd", "k_ot_bwd", "k_inv_gj", "k_groupsort_fwd",
+         "k_groupsort_bwd", "k_ode", "k_dyn", "k_qp", "k_cert")
 
 
 def short(name: str) -> str:
+    if "k_inv_gj<" in name:          # keep the template: element type and padded size
+        i = name.find("k_inv_gj<")
+        t = name[i:].split(">(")[0].replace("(anonymous namespace)::", "")
+        return t + ">"
     for k in FUSED:
         if k in name:
             i = name.find(k)
@@ -50,7 +55,8 @@ def main(src: str, dst: str):
     total = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"# rocprofv3 --kernel-trace --stats  ({src_p.name})", "",
              "Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python bench.py --steps 10 "
-             "--warmup 3 --no-cpu-baseline` (tools/gpu_profile.sh).", "",
+             "--warmup 3 --no-cpu-baseline --no-secondary` (tools/gpu_profile.sh; the step is a hipGraph replay, "
+             "the fused kernels are also launched once more per rep by bench.py's per-kernel HIP-event timing).", "",
              f"Total kernel time {total / 1e6:.2f} ms over {sum(int(r['Calls']) for r in rows)} dispatches.", "",
              "## Fused FI-ODE kernels (libfiode.so)", "",
              "| kernel | calls | avg us | min us | max us | % of total |", "|---|---|---|---|---|---|"]
@@ -59,6 +65,10 @@ def main(src: str, dst: str):
         if n.startswith("k_"):
             lines.append(f"| {n} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
                          f"{float(r['MaxNs']) / 1e3:.2f} | {float(r['Percentage']):.2f} |")
+    import subprocess
+    fam = subprocess.run([sys.executable, str(pathlib.Path(__file__).with_name("kernel_families.py")), str(stats)],
+                         capture_output=True, text=True).stdout
+    lines += ["", "## Kernel families (all dispatches of the run)", "", "```", fam.rstrip(), "```"]
     lines += ["", "## Top 15 kernels overall", "", "| kernel | calls | avg us | % |", "|---|---|---|---|"]
     for r in rows[:15]:
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
