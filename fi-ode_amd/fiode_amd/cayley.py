@@ -13,6 +13,7 @@ and stay in PyTorch: their gradients come from autograd, fed by the fused HIP st
 from __future__ import annotations
 
 import math
+from typing import Optional
 
 import torch
 import torch.nn as nn
@@ -220,29 +221,36 @@ class CayleyLinear(nn.Linear):
 
 class _GroupSortFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, cdim: int):
         from . import ops
-        y = ops.groupsort_forward(x)
+        y = ops.groupsort_forward(x, cdim)
         ctx.save_for_backward(x)
+        ctx.cdim = cdim
         return y
 
     @staticmethod
     def backward(ctx, g):
         from . import ops
         x, = ctx.saved_tensors
-        return ops.groupsort_backward(x, g)
+        return ops.groupsort_backward(x, g, ctx.cdim), None
 
 
 class GroupSort(nn.Module):
-    """Sort pairs of channel halves: [max(a, b), min(a, b)] along dim 1.  On ROCm tensors one HIP
-    kernel each way (fiode_groupsort_*; ties split the gradient like torch.maximum); host tensors
-    take the torch ops."""
+    """Sort pairs of channel halves: [max(a, b), min(a, b)] along the channel dim (1, or
+    ``channel_dim`` for the spatial-major conv stack).  On ROCm tensors one HIP kernel each way
+    (fiode_groupsort_*; ties split the gradient like torch.maximum); host tensors take the torch
+    ops."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def __init__(self, channel_dim: int = 1):
+        super().__init__()
+        self.channel_dim = channel_dim
+
+    def forward(self, x: torch.Tensor, channel_dim: Optional[int] = None) -> torch.Tensor:
+        cd = self.channel_dim if channel_dim is None else channel_dim
         if x.is_cuda:
-            return _GroupSortFn.apply(x)
-        a, b = x.split(x.size(1) // 2, 1)
-        return torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=1)
+            return _GroupSortFn.apply(x, cd)
+        a, b = x.split(x.size(cd) // 2, cd)
+        return torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=cd)
 
 
 class CayleyConv(nn.Conv2d):
@@ -294,6 +302,15 @@ class CayleyConv(nn.Conv2d):
             n = self._n
             self._pre = _prefetch(stream, lambda: self.spectral_weight(n, self.weight.device))
 
+    def _take_spectral(self, n: int, device) -> torch.Tensor:
+        if self._pre is not None and self.training and self._n == n:
+            Q = _take(self._pre)
+        else:
+            Q = self.spectral_weight(n, device)
+        self._pre = None
+        self._n = n
+        return Q
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.downsample:
             b, c, h, w = x.shape
@@ -302,14 +319,28 @@ class CayleyConv(nn.Conv2d):
         B, _, n, _ = x.shape
         nf = n * (n // 2 + 1)
         xf = torch.fft.rfft2(x).permute(2, 3, 1, 0).reshape(nf, cin, B)
-        if self._pre is not None and self.training and self._n == n:
-            Q = _take(self._pre)
-        else:
-            Q = self.spectral_weight(n, x.device)
-        self._pre = None
-        self._n = n
+        Q = self._take_spectral(n, x.device)
         yf = (Q @ xf).reshape(n, n // 2 + 1, cout, B)
         y = torch.fft.irfft2(yf.permute(3, 2, 0, 1), s=(n, n))
         if self.bias is not None:
             y = y + self.bias[:, None, None]
         return y
+
+    def forward_hwcb(self, x: torch.Tensor) -> torch.Tensor:
+        """The same map on spatial-major activations [n, n, C, B] (the conv stack's HBM layout):
+        the 2-D rFFT over dims (0, 1) yields [n (n/2+1), C, B] = the per-frequency GEMM operand
+        directly, the GEMM output is the inverse FFT's input, and the bias is added on the DC
+        frequency (irfft2's 1/n^2 normalisation: + n^2 b), so no permute copies and no full-size
+        bias pass."""
+        if self.downsample:
+            h, w, c, b = x.shape
+            x = x.reshape(h // 2, 2, w // 2, 2, c, b).permute(0, 2, 4, 1, 3, 5).reshape(h // 2, w // 2, c * 4, b)
+        cout, cin = self.weight.shape[:2]
+        n, _, _, B = x.shape
+        nf = n * (n // 2 + 1)
+        xf = torch.fft.rfft2(x, dim=(0, 1)).reshape(nf, cin, B)
+        Q = self._take_spectral(n, x.device)
+        yf = Q @ xf
+        if self.bias is not None:
+            yf[0] += (float(n * n) * self.bias)[:, None]
+        return torch.fft.irfft2(yf.reshape(n, n // 2 + 1, cout, B), s=(n, n), dim=(0, 1))

@@ -47,8 +47,30 @@ class KWLargeConcat(nn.Module):
             CayleyLinear(512, out_dim),
         )
 
+        self.spatial_major = True
+
     def forward(self, x):
-        return self.model(x)
+        """On ROCm the conv stack runs spatial-major ([h, w, C, B]: FFT and GEMM operands without
+        permute copies, CayleyConv.forward_hwcb); the flatten restores the reference's (C, h, w)
+        feature order.  Host tensors take the module-by-module NCHW path."""
+        if not (self.spatial_major and x.is_cuda):
+            return self.model(x)
+        mods = list(self.model)
+        h = x.permute(2, 3, 1, 0).contiguous()
+        i = 0
+        while not isinstance(mods[i], nn.Flatten):
+            m = mods[i]
+            if isinstance(m, CayleyConv):
+                h = m.forward_hwcb(h)
+            elif isinstance(m, GroupSort):
+                h = m(h, channel_dim=2)
+            else:
+                h = m(h)
+            i += 1
+        h = h.permute(3, 2, 0, 1).reshape(h.shape[3], -1)
+        for m in mods[i + 1:]:
+            h = m(h)
+        return h
 
 
 def make_ortho_KWLarge_Concat(n_in_channels=3, n_outputs=10, mu=(0.485, 0.456, 0.406), std=(0.225, 0.225, 0.225),

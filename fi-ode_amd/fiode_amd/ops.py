@@ -375,28 +375,34 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     return out
 
 
-def _gs_shape(x: torch.Tensor):
+def _gs_shape(x: torch.Tensor, cdim: int = 1):
     if x.device.type != "cuda" or x.dtype != torch.float32:
         raise ValueError(f"groupsort: float32 ROCm tensor expected, got {x.dtype} on {x.device}")
-    B, Cc = x.shape[0], x.shape[1]
-    S = x[0, 0].numel() if x.dim() > 2 else 1
-    if Cc % 2 or ((Cc // 2) * S) % 4:
-        raise ValueError(f"groupsort: shape {tuple(x.shape)} needs even C and (C/2)*S % 4 == 0")
-    return B, Cc, S
+    cdim = cdim % x.dim()
+    outer = 1
+    for d in x.shape[:cdim]:
+        outer *= d
+    Cc = x.shape[cdim]
+    inner = 1
+    for d in x.shape[cdim + 1:]:
+        inner *= d
+    if Cc % 2 or ((Cc // 2) * inner) % 4:
+        raise ValueError(f"groupsort: shape {tuple(x.shape)} needs even C and (C/2)*inner % 4 == 0")
+    return outer, Cc, inner
 
 
-def groupsort_forward(x: torch.Tensor) -> torch.Tensor:
+def groupsort_forward(x: torch.Tensor, cdim: int = 1) -> torch.Tensor:
     x = x.contiguous()
-    B, Cc, S = _gs_shape(x)
+    B, Cc, S = _gs_shape(x, cdim)
     y = torch.empty_like(x)
     L.check(L.lib().fiode_groupsort_forward(_stream(x.device), B, Cc, S, x.data_ptr(), y.data_ptr()),
             "fiode_groupsort_forward")
     return y
 
 
-def groupsort_backward(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+def groupsort_backward(x: torch.Tensor, g: torch.Tensor, cdim: int = 1) -> torch.Tensor:
     x, g = x.contiguous(), g.contiguous()
-    B, Cc, S = _gs_shape(x)
+    B, Cc, S = _gs_shape(x, cdim)
     gx = torch.empty_like(x)
     L.check(L.lib().fiode_groupsort_backward(_stream(x.device), B, Cc, S, x.data_ptr(), g.data_ptr(), gx.data_ptr()),
             "fiode_groupsort_backward")

@@ -172,3 +172,26 @@ def test_cayley_scaled_forward_backward(shape, dtype, per_matrix):
     for got, ref in ((Wa.grad, Wb.grad), (aa.grad, ab.grad)):
         scale = float(ref.abs().max()) + 1e-12
         assert float((got.to(ref.dtype) - ref).abs().max()) / scale < 1e-4
+
+
+def test_spatial_major_backbone_matches_nchw():
+    """KWLargeConcat on the spatial-major path (forward_hwcb, DC-folded bias, groupsort on dim 2)
+    = the module-by-module NCHW path, forward and parameter gradients."""
+    from fiode_amd.models import make_ortho_KWLarge_Concat
+    dev = _dev()
+    torch.manual_seed(0)
+    bb = make_ortho_KWLarge_Concat(out_dim=10, act="GroupSort").to(dev).train()
+    x = torch.rand(8, 3, 32, 32, device=dev)
+    bb[1].spatial_major = False
+    y0 = bb(x)                      # also initialises the conv alphas
+    bb.zero_grad()
+    y0 = bb(x)
+    y0.square().sum().backward()
+    g0 = [p.grad.clone() for p in bb.parameters()]
+    bb.zero_grad()
+    bb[1].spatial_major = True
+    y1 = bb(x)
+    y1.square().sum().backward()
+    assert float((y1 - y0).abs().max()) < 1e-4 * (float(y0.abs().max()) + 1)
+    for a, b in zip(bb.parameters(), g0):
+        assert float((a.grad - b).abs().max()) <= 1e-3 * (float(b.abs().max()) + 1e-6)
