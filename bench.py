@@ -150,8 +150,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://")
-    dev = torch.device(f"cuda:{local}")
+        # RCCL ("nccl") between GPUs; FIODE_BENCH_BACKEND=gloo rehearses the N-rank path with
+        # several ranks sharing the visible GPUs (device = local rank mod device count)
+        dist.init_process_group(backend=os.environ.get("FIODE_BENCH_BACKEND", "nccl"), init_method="env://")
+    dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     torch.cuda.set_device(dev)
 
     def timed_run(train_ode: bool, steps: int, warmup: int):
