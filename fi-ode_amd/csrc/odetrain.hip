@@ -58,7 +58,7 @@ struct OTArgs {
   float* gz2;               // [B][E][M]
   float* gz1;               // [B][E][M]
   float* gft;               // [B][E][C]
-  unsigned long long* xslots;  // [E][ntiles] {epoch, mask} granules of the QP exit exchange
+  unsigned long long* xslots;  // [E][2 phases][ntiles] {epoch, mask} granules of the QP exit exchange
   uint32_t* kw;                // [E][2][B] uint4 dropout keep words
 #ifdef OT_PROFILE
   unsigned long long* prof;    // [8] wall-clock ticks per phase (workgroup 0, lane 0)
@@ -97,8 +97,9 @@ struct OtShared {
   float zpart[4][64][6];      // [part][lane][valid layer-3 accumulator registers]
   float mu_rec[4][32][33];    // [wave][row][bisection iteration] (padded)
   float Q1s[M * C];
-  uint32_t K;
-  int pad[3];
+  int K;
+  int Kprev;                  // previous eval's exit iteration (speculation for the next)
+  int pad[2];
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -137,16 +138,21 @@ __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int 
   return wave_and(acc);
 }
 
-__device__ __forceinline__ uint32_t qp_bisect_record(const float (&lower)[C], const float (&nom)[C], int last,
-                                                     float tol, float* mu_rec, bool rec) {
-  float hi = nom[0] - lower[0], lo = nom[0];
+// The bisection of FastBarrierProjectionNoUpper (qp_bisect, common.h) split so it can stop and
+// resume: iterations [from, to] from the bracket state (lo, hi), recording mu per iteration.
+__device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float (&nom)[C], float& lo, float& hi) {
+  hi = nom[0] - lower[0];
+  lo = nom[0];
 #pragma unroll
   for (int j = 1; j < C; ++j) {
     hi = fmaxf(hi, nom[j] - lower[j]);
     lo = fminf(lo, nom[j]);
   }
+}
+__device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                    float tol, float& lo, float& hi, float* mu_rec, bool rec) {
   uint32_t conv = 0;
-  for (int it = 0; it <= last; ++it) {
+  for (int it = from; it <= to; ++it) {
     const float mu = (hi - lo) / 2.0f + lo;
     float eps = 0.f;
 #pragma unroll
@@ -205,7 +211,6 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
 #pragma unroll
       for (int t = 0; t < 4; ++t) z2 = mfma32(q[t], z1[kb][4 * g + t], z2);
     }
-    __builtin_amdgcn_sched_barrier(0);
   }
   dropout_relu(z2, kw2p, half, a.drop_scale);
   if (valid) store_acc_rows(a.a2 + r * M, p, half, z2);
@@ -235,19 +240,39 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   float ft[C], lower[C], nominal[C], sig[C], span[C];
   gather_ft(zs, half, ft);
   barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-  uint32_t conv = qp_bisect_record(lower, nominal, a.d.max_iter - 1, a.d.tol, &sh.mu_rec[p][col][0], half == 0);
-  if (!valid) conv = 0xFFFFFFFFu;
-  conv = wave_and(conv);
+  // Speculative exit: bisect up to the previous eval's exit + 3 and exchange; only if no iteration
+  // <= that converged on every row of the batch, continue to max_iter - 1 and exchange again.
+  // K is the same as the full sweep's (the lowest all-converged iteration wins either way).
+  const int last = a.d.max_iter - 1;
+  const int kspec = min(last, sh.Kprev + 3);
+  float lo, hi;
+  qp_bracket(lower, nominal, lo, hi);
+  float* rec = &sh.mu_rec[p][col][0];
+  uint32_t conv = qp_bisect_range(lower, nominal, 0, kspec, a.d.tol, lo, hi, rec, half == 0);
+  uint32_t wconv = valid ? conv : 0xFFFFFFFFu;
+  wconv = wave_and(wconv);
   OT_MARK(2);
   const int ntiles = gridDim.x;
-  unsigned long long* slots = a.xslots + (size_t)e * ntiles;
-  if (p == 0 && lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, conv);
+  unsigned long long* slots = a.xslots + (size_t)e * 2 * ntiles;
   if (p == 0) {
+    if (lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, wconv);
     const uint32_t all = gather_masks(slots, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
-    if (lane == 0) sh.K = (uint32_t)qp_exit_iter(all, a.d.max_iter);
+    const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
+    const uint32_t bits = all & lowm;
+    if (lane == 0) sh.K = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
   }
   __syncthreads();
-  OT_MARK(3);
+  if (sh.K < 0) {                       // block-uniform: every tile saw the same masks
+    conv |= qp_bisect_range(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, rec, half == 0);
+    wconv = valid ? conv : 0xFFFFFFFFu;
+    wconv = wave_and(wconv);
+    if (p == 0) {
+      if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, (unsigned)e + 1u, wconv);
+      const uint32_t all = gather_masks(slots + ntiles, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
+      if (lane == 0) sh.K = qp_exit_iter(all, a.d.max_iter);
+    }
+    __syncthreads();
+  }
   const int K = (int)sh.K;
   const float mu = sh.mu_rec[p][col][K];
 #pragma unroll
@@ -259,6 +284,7 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
     a.muw[r] = mu;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) a.stats[2] = K;
+  if (threadIdx.x == 0) sh.Kprev = K;
   __syncthreads();            // zpart / mu_rec / K reused by the next eval
   OT_MARK(4);
 }
@@ -286,6 +312,7 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   OtShared& sh = *reinterpret_cast<OtShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
   for (int q = threadIdx.x; q < M * C; q += blockDim.x) sh.Q1s[q] = a.Q1[q];
+  if (threadIdx.x == 0) sh.Kprev = a.d.max_iter - 1;
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x * 32 + col;
@@ -565,7 +592,7 @@ OtLayout ot_layout(int B, int E) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  L.xs = o; o += al((size_t)E * ((B + 31) / 32) * 8 + 256);
+  L.xs = o; o += al((size_t)E * 2 * ((B + 31) / 32) * 8 + 256);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
   L.total = o;
@@ -614,7 +641,7 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.xslots = reinterpret_cast<unsigned long long*>(ws + L.xs);
   a.kw = reinterpret_cast<uint32_t*>(ws + L.kw);
 #ifdef OT_PROFILE
-  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * ((a.B + 31) / 32) + 8;
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + 31) / 32) + 8;
 #endif
   return FIODE_OK;
 }
@@ -658,7 +685,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   const int ntiles = (a.B + 31) / 32;
   const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);
   // zero the exchange granules (tags) and the status word before every launch
-  FIODE_HIP_CHECK(hipMemsetAsync(a.xslots, 0, (size_t)a.E * ntiles * 8 + 256, st));
+  FIODE_HIP_CHECK(hipMemsetAsync(a.xslots, 0, (size_t)a.E * 2 * ntiles * 8 + 256, st));
   FIODE_HIP_CHECK(hipMemsetAsync(stats, 0, 8 * sizeof(int32_t), st));
   if (a.dropout_mode != FIODE_DROPOUT_OFF) {
     hipLaunchKernelGGL(k_ot_masks, dim3((a.E * a.B + 255) / 256), dim3(256), 0, st, a);

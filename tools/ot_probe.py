@@ -25,7 +25,7 @@ for B in (128, 1024):
     lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
     al = lambda v: (v + 255) & ~255
     xs = offs[7] + al(B * E * 10 * 4)
-    prof = ws[xs + (E * nt + 8) * 8: xs + (E * nt + 16) * 8].view(torch.int64).cpu().numpy()
+    prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 16) * 8].view(torch.int64).cpu().numpy()
     ticks = prof[:5] / E          # 100 MHz wall clock -> 10 ns per tick
     print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): layer1 {ticks[0]*0.01:.2f} "
           f"layer2+3 {ticks[1]*0.01:.2f} sum+QP {ticks[2]*0.01:.2f} exchange {ticks[3]*0.01:.2f} "
