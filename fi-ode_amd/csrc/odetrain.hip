@@ -5,14 +5,14 @@
 // (torchdiffeq 0.2.2 FixedGridODESolver + rk4_alt_step_func, the 3/8 rule; every func() call is
 // eval_dot with fresh dropout masks and the QP's batch-global exit over the B rows).
 //
-// Forward  (k_ot_fwd, one persistent workgroup per 32-row tile, all tiles co-resident; each
+// Forward  (k_ot_fwd, one persistent workgroup per 16-row tile, all tiles co-resident; each
 //   stage's QP exit is a batch-wide AND exchanged through tagged granules, see below):
 //   for each step, stage i = 1..4 (eval e = 4*step + i - 1), per row in registers:
 //     Y_i = y + dt * sum_j beta_ij k_j      -> hs[b][e]
 //     MLP (MFMA, hidden split over 4 waves), a1/a2 saved -> a1/a2[b][e], ft[b][e]
 //     QP bisection recording mu per iteration; exit K from all tiles; k_i = v(mu_K)
 //   y += (k1 + 3 (k2 + k3) + k4) dt / 8
-// Backward (k_ot_bwd, one workgroup per 32 rows; rows never interact in the backward, so tiles
+// Backward (k_ot_bwd, one workgroup per 16 rows; rows never interact in the backward, so tiles
 //   need no grid-wide synchronisation): the reverse sweep of the 3/8 rule; every stage VJP is the QP backward
 //   (closed form), the sigmoid rescale, the barrier bounds' h-dependence, and the MLP input
 //   gradients (Q3^T, Q2^T via LDS images, Q1^T via a zero-padded LDS image), writing the per-
@@ -83,19 +83,56 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// forward: one workgroup per 32-row tile, persistent over all evals; 4 waves = 4 parts of the
-// hidden dimension.  Per eval every wave computes layer 1 in full (20 MFMA), its 32 of the 128
-// layer-2 outputs (64 MFMA) and their layer-3 partial (16 MFMA); the partials meet in LDS and
-// every wave sums them in the same order, so the row state (y, k1..k4, the QP) is replicated in
-// the 4 waves and needs no further exchange.  The only cross-tile coupling -- the QP's exit
-// iteration, the lowest bit of the AND over ALL rows of the per-iteration convergence masks --
-// is exchanged through per-eval {tag, mask} granules: each workgroup publishes its mask with ONE
-// agent-scope 64-bit atomic store, then one wave sweeps the ntiles granules of that eval until
-// every tag matches (relaxed agent-scope loads; the granule IS the flag, so no fence is needed).
-// The spin is bounded: on timeout the status word records it and the solve completes.
+// MFMA layout: v_mfma_f32_16x16x4_f32, "hidden on M, samples on N".  A tile is TR = 16 rows
+// (samples); lane l holds sample j = l & 15 of the tile and q = l >> 4 selects the K slot.
+// A operand A[i = j][k = q], B operand B[k = q][col = j]; accumulator register r holds
+// D[row = 4q + r][col = j].  A layer's accumulator block hb (hidden 16hb + 4q + r) is directly
+// the B operand of the next layer's k-steps (hb, r), whose k index 4q' + r ... is hidden
+// 16hb + 4q + r, so the A operand of that k-step is Q[out][16hb + 4q + r] (r = 0..3): one
+// ds_read_b128 of 4 consecutive weights.  32-cycle issue, 40-cycle dependent latency: every
+// accumulation runs >= 2 independent accumulators except the short layer-3 chain.
+constexpr int TR = 16;
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4v z4() { return f32x4v{0.f, 0.f, 0.f, 0.f}; }
+
+// relu(dropout(z)) on a 16x16 block: hidden 16hb + 4q + r, keep bit from w = kw[hidden >> 5]
+__device__ __forceinline__ void dropout_relu16(f32x4v& z, uint32_t w, int hb, int q, float scale) {
+  const int sh = 16 * (hb & 1) + 4 * q;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool keep = (w >> (sh + r)) & 1u;
+    z[r] = keep ? fmaxf(z[r] * scale, 0.f) : 0.f;
+  }
+}
+__device__ __forceinline__ float sel4(const float (&v)[C], int s, int q) {   // v[4s + q], 0 past C
+  const int k = 4 * s + q;
+  float x = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (4 * s + t < C) x = (q == t) ? v[4 * s + t] : x;
+  return k < C ? x : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward: one workgroup per 16-row tile, persistent over all evals; 4 waves = 4 parts of the
+// hidden dimension.  Per eval every wave computes layer 1 in full (24 MFMA), its 32 of the 128
+// layer-2 outputs (64 MFMA) and their layer-3 partial (8 MFMA); the partials meet in LDS and
+// every lane sums its sample's 10 outputs over the parts in the same order, so the row state
+// (y, k1..k4, the QP) is replicated in all waves and needs no further exchange.  The QP's
+// per-iteration convergence over the tile is a wave ballot (no cross-lane shuffles).  The only
+// cross-tile coupling -- the QP's exit iteration, the lowest bit of the AND over ALL rows of the
+// per-iteration convergence masks -- is exchanged through per-eval {tag, mask} granules: each
+// workgroup publishes its mask with ONE agent-scope 64-bit atomic store, then one wave sweeps the
+// ntiles granules of that eval until every tag matches (relaxed agent-scope loads; the granule
+// IS the flag, so no fence is needed).  The spin is bounded: on timeout the status word records
+// it and the solve completes.
 struct OtShared {
-  float zpart[4][64][6];      // [part][lane][valid layer-3 accumulator registers]
-  float mu_rec[4][32][33];    // [wave][row][bisection iteration] (padded)
+  float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
+  float mu_rec[4][TR][33];    // [wave][row][bisection iteration] (padded)
   float Q1s[M * C];
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
@@ -103,7 +140,6 @@ struct OtShared {
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) unsigned int gu32_t;
 
 __device__ __forceinline__ void publish_mask(unsigned long long* slot, unsigned epoch, uint32_t mask) {
   __hip_atomic_store((gu64_t*)(slot), ((unsigned long long)epoch << 32) | mask, __ATOMIC_RELAXED,
@@ -139,7 +175,8 @@ __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int 
 }
 
 // The bisection of FastBarrierProjectionNoUpper (qp_bisect, common.h) split so it can stop and
-// resume: iterations [from, to] from the bracket state (lo, hi), recording mu per iteration.
+// resume: iterations [from, to] from the bracket state (lo, hi), recording mu per iteration.  The
+// returned mask is the WAVE's: bit it set iff every valid lane converged at iteration it (ballot).
 __device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float (&nom)[C], float& lo, float& hi) {
   hi = nom[0] - lower[0];
   lo = nom[0];
@@ -150,7 +187,8 @@ __device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float 
   }
 }
 __device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], const float (&nom)[C], int from, int to,
-                                                    float tol, float& lo, float& hi, float* mu_rec, bool rec) {
+                                                    float tol, float& lo, float& hi, float* mu_rec, bool rec,
+                                                    bool valid) {
   uint32_t conv = 0;
   for (int it = from; it <= to; ++it) {
     const float mu = (hi - lo) / 2.0f + lo;
@@ -158,7 +196,8 @@ __device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], con
 #pragma unroll
     for (int j = 0; j < C; ++j) eps = eps + fmaxf(nom[j] - mu, lower[j]);
     if (rec) mu_rec[it] = mu;
-    conv |= (fabsf(eps) < tol ? 1u : 0u) << it;
+    const unsigned long long open = __ballot(valid && !(fabsf(eps) < tol));
+    conv |= (open == 0ull ? 1u : 0u) << it;
     lo = eps > 0.f ? mu : lo;
     hi = eps < 0.f ? mu : hi;
   }
@@ -174,72 +213,84 @@ __device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], con
 
 // one eval for this workgroup's tile: stage input h (per lane, its row) -> k (per lane)
 __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtShared& sh, int e, int p, int b,
-                        bool valid, int lane, int half, int col, const f32x16 (&uacc)[4], const uint32_t (&kw1)[4],
+                        bool valid, int lane, int q, int j, const f32x4v (&uacc)[8], const uint32_t (&kw1)[4],
                         uint32_t kw2p, const float (&h)[C], float (&k)[C]) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
 #ifdef OT_PROFILE
   uint64_t t_prev = wall_clock64();
 #endif
-  if (p == 0 && valid && half == 0) store_row10(a.hs + r * C, h);
-  // layer 1 (full): z1 = u[b] + Q1 h
-  f32x16 z1[4];
+  if (p == 0 && valid && q == 0) store_row10(a.hs + r * C, h);
+  // layer 1 (full): z1 = u[b] + Q1 h, 8 hidden blocks, K = 10 in 3 k-steps
+  f32x4v z1[8];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) z1[mb] = uacc[mb];
+  for (int hb = 0; hb < 8; ++hb) z1[hb] = uacc[hb];
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const float bs = half ? h[2 * s + 1] : h[2 * s];
+  for (int s = 0; s < 3; ++s) {
+    const float bs = sel4(h, s, q);
+    const bool kin = 4 * s + q < C;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) z1[mb] = mfma32(sh.Q1s[(32 * mb + col) * C + 2 * s + half], bs, z1[mb]);
-  }
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb) dropout_relu(z1[mb], kw1[mb], half, a.drop_scale);
-  OT_MARK(0);
-  if (valid) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-      if (mb == p) store_acc_rows(a.a1 + r * M, mb, half, z1[mb]);
-  }
-  // layer 2, output block p: z2 = b2 + Q2[32p.., :] a1
-  f32x16 z2;
-  load_acc_rows(a.b2, p, half, z2);
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 q = *reinterpret_cast<const f32x4*>(Q2s + (32 * p + col) * LDQ + 32 * kb + 8 * g + 4 * half);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) z2 = mfma32(q[t], z1[kb][4 * g + t], z2);
+    for (int hb = 0; hb < 8; ++hb) {
+      const float av = kin ? sh.Q1s[(16 * hb + j) * C + 4 * s + q] : 0.f;
+      z1[hb] = mfma16(av, bs, z1[hb]);
     }
   }
-  dropout_relu(z2, kw2p, half, a.drop_scale);
-  if (valid) store_acc_rows(a.a2 + r * M, p, half, z2);
-  // layer-3 partial over hidden block p (bias on part 0)
-  f32x16 z3 = f16_zero();
+#pragma unroll
+  for (int hb = 0; hb < 8; ++hb) dropout_relu16(z1[hb], kw1[hb >> 1], hb, q, a.drop_scale);
+  OT_MARK(0);
+  if (valid) {                 // part p saves a1 blocks 2p, 2p+1
+#pragma unroll
+    for (int hb = 0; hb < 8; ++hb)
+      if ((hb >> 1) == p)
+        *reinterpret_cast<f32x4*>(a.a1 + r * M + 16 * hb + 4 * q) = f32x4{z1[hb][0], z1[hb][1], z1[hb][2], z1[hb][3]};
+  }
+  // layer 2, output blocks 2p, 2p+1: z2 = b2 + Q2[16 ob.., :] a1 (two independent accumulators)
+  f32x4v z2[2];
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.b2 + 16 * (2 * p + o) + 4 * q);
+    z2[o] = f32x4v{bv[0], bv[1], bv[2], bv[3]};
+  }
+#pragma unroll
+  for (int hb = 0; hb < 8; ++hb) {
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(Q2s + (16 * (2 * p + o) + j) * LDQ + 16 * hb + 4 * q);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) z2[o] = mfma16(qv[t], z1[hb][t], z2[o]);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    dropout_relu16(z2[o], kw2p, 2 * p + o, q, a.drop_scale);
+    if (valid)
+      *reinterpret_cast<f32x4*>(a.a2 + r * M + 16 * (2 * p + o) + 4 * q) = f32x4{z2[o][0], z2[o][1], z2[o][2], z2[o][3]};
+  }
+  // layer-3 partial over hidden blocks 2p, 2p+1 (bias on part 0); rows >= 10 of Q3s are zero
+  f32x4v z3 = z4();
   if (p == 0) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = acc_row(q, half);
-      z3[q] = i < C ? a.b3[i] : 0.f;
-    }
+    for (int t = 0; t < 4; ++t) z3[t] = 4 * q + t < C ? a.b3[4 * q + t] : 0.f;
   }
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 q = *reinterpret_cast<const f32x4*>(Q3s + col * LDQ + 32 * p + 8 * g + 4 * half);
+  for (int o = 0; o < 2; ++o) {
+    const f32x4 qv = *reinterpret_cast<const f32x4*>(Q3s + j * LDQ + 16 * (2 * p + o) + 4 * q);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) z3 = mfma32(q[t], z2[4 * g + t], z3);
+    for (int t = 0; t < 4; ++t) z3 = mfma16(qv[t], z2[o][t], z3);
   }
-#pragma unroll
-  for (int q = 0; q < 6; ++q) sh.zpart[p][lane][q] = z3[q];
+  *reinterpret_cast<f32x4*>(&sh.zpart[p][lane][0]) = f32x4{z3[0], z3[1], z3[2], z3[3]};
   OT_MARK(1);
   __syncthreads();
-  f32x16 zs = f16_zero();
+  // this lane's sample j: output i sits in lane 16 (i >> 2) + j, register i & 3, of every part
+  float ft[C];
 #pragma unroll
-  for (int q = 0; q < 6; ++q)
-    zs[q] = ((sh.zpart[0][lane][q] + sh.zpart[1][lane][q]) + sh.zpart[2][lane][q]) + sh.zpart[3][lane][q];
-  float ft[C], lower[C], nominal[C], sig[C], span[C];
-  gather_ft(zs, half, ft);
+  for (int i = 0; i < C; ++i) {
+    const int ln = 16 * (i >> 2) + j, rg = i & 3;
+    ft[i] = ((sh.zpart[0][ln][rg] + sh.zpart[1][ln][rg]) + sh.zpart[2][ln][rg]) + sh.zpart[3][ln][rg];
+  }
+  float lower[C], nominal[C], sig[C], span[C];
   barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+  OT_MARK(5);
   // Speculative exit: bisect up to the previous eval's exit + 3 and exchange; only if no iteration
   // <= that converged on every row of the batch, continue to max_iter - 1 and exchange again.
   // K is the same as the full sweep's (the lowest all-converged iteration wins either way).
@@ -247,15 +298,13 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   const int kspec = min(last, sh.Kprev + 3);
   float lo, hi;
   qp_bracket(lower, nominal, lo, hi);
-  float* rec = &sh.mu_rec[p][col][0];
-  uint32_t conv = qp_bisect_range(lower, nominal, 0, kspec, a.d.tol, lo, hi, rec, half == 0);
-  uint32_t wconv = valid ? conv : 0xFFFFFFFFu;
-  wconv = wave_and(wconv);
+  float* rec = &sh.mu_rec[p][j][0];
+  uint32_t conv = qp_bisect_range(lower, nominal, 0, kspec, a.d.tol, lo, hi, rec, q == 0, valid);
   OT_MARK(2);
   const int ntiles = gridDim.x;
   unsigned long long* slots = a.xslots + (size_t)e * 2 * ntiles;
   if (p == 0) {
-    if (lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, wconv);
+    if (lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, conv);
     const uint32_t all = gather_masks(slots, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
@@ -263,21 +312,20 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   }
   __syncthreads();
   if (sh.K < 0) {                       // block-uniform: every tile saw the same masks
-    conv |= qp_bisect_range(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, rec, half == 0);
-    wconv = valid ? conv : 0xFFFFFFFFu;
-    wconv = wave_and(wconv);
+    conv |= qp_bisect_range(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, rec, q == 0, valid);
     if (p == 0) {
-      if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, (unsigned)e + 1u, wconv);
+      if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, (unsigned)e + 1u, conv);
       const uint32_t all = gather_masks(slots + ntiles, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
       if (lane == 0) sh.K = qp_exit_iter(all, a.d.max_iter);
     }
     __syncthreads();
   }
-  const int K = (int)sh.K;
-  const float mu = sh.mu_rec[p][col][K];
+  OT_MARK(3);
+  const int K = sh.K;
+  const float mu = sh.mu_rec[p][j][K];
 #pragma unroll
-  for (int j = 0; j < C; ++j) k[j] = fmaxf(nominal[j] - mu, lower[j]);
-  if (p == 0 && valid && half == 0) {
+  for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);
+  if (p == 0 && valid && q == 0) {
     store_row10(a.ftw + r * C, ft);
     store_row10(a.nomw + r * C, nominal);
     store_row10(a.vw + r * C, k);
@@ -311,16 +359,16 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   float* Q3s = smem + M * LDQ;
   OtShared& sh = *reinterpret_cast<OtShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
-  for (int q = threadIdx.x; q < M * C; q += blockDim.x) sh.Q1s[q] = a.Q1[q];
+  for (int t = threadIdx.x; t < M * C; t += blockDim.x) sh.Q1s[t] = a.Q1[t];
   if (threadIdx.x == 0) sh.Kprev = a.d.max_iter - 1;
-  const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b = blockIdx.x * 32 + col;
+  const int b = blockIdx.x * TR + j;
   const bool valid = b < a.B;
   const int bb = valid ? b : a.B - 1;
-  // u[b] = U_x x_b + bx + b1 for this tile's rows (part p computes hidden block p)
-  for (int q = threadIdx.x; q < 32 * M; q += blockDim.x) {
-    const int rb = blockIdx.x * 32 + q / M, i = q % M;
+  // u[b] = U_x x_b + bx + b1 for this tile's rows
+  for (int t = threadIdx.x; t < TR * M; t += blockDim.x) {
+    const int rb = blockIdx.x * TR + t / M, i = t % M;
     if (rb < a.B) {
       float s = 0.f;
 #pragma unroll
@@ -329,55 +377,60 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
     }
   }
   __syncthreads();
-  f32x16 uacc[4];
+  f32x4v uacc[8];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)bb * M, mb, half, uacc[mb]);
+  for (int hb = 0; hb < 8; ++hb) {
+    const f32x4 uv = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 16 * hb + 4 * q);
+    uacc[hb] = f32x4v{uv[0], uv[1], uv[2], uv[3]};
+  }
   // dropout keep words of eval e (k_ot_masks), prefetched one eval ahead
   const uint4* kwp = reinterpret_cast<const uint4*>(a.kw);
   auto fetch = [&](int e, uint32_t (&w1)[4], uint32_t& w2) {
     if (a.dropout_mode == FIODE_DROPOUT_OFF) {
-      w1[0] = w1[1] = w1[2] = w1[3] = w2 = 0xFFFFFFFFu;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w1[t] = 0xFFFFFFFFu;
+      w2 = 0xFFFFFFFFu;
       return;
     }
     const uint4 q1 = kwp[((size_t)e * 2 + 0) * a.B + bb];
-    const uint4 q2 = kwp[((size_t)e * 2 + 1) * a.B + bb];
     w1[0] = q1.x; w1[1] = q1.y; w1[2] = q1.z; w1[3] = q1.w;
-    w2 = p == 0 ? q2.x : p == 1 ? q2.y : p == 2 ? q2.z : q2.w;
+    w2 = reinterpret_cast<const uint32_t*>(kwp + ((size_t)e * 2 + 1) * a.B + bb)[p];   // layer-2 word of part p
   };
   uint32_t kc1[4], kc2, kn1[4], kn2;
   fetch(0, kc1, kc2);
   float y[C], k1[C], k2[C], k3[C], k4[C], hin[C];
   load_row10(a.h0 + (size_t)bb * C, y);
   const float third = 1.0f / 3.0f;
+  const int eN = 4 * (a.niters - 1);
   for (int it = 0; it + 1 < a.niters; ++it) {
     float ta, dt;
     step_times(a, it, ta, dt);
     const int e0 = 4 * it;
-    const int eN = 4 * (a.niters - 1);
-#define OT_STAGE(E_, H_, K_)                                                       \
-    {                                                                              \
-      if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                \
-      ot_eval(a, Q2s, Q3s, sh, (E_), p, b, valid, lane, half, col, uacc, kc1, kc2, H_, K_); \
-      kc1[0] = kn1[0]; kc1[1] = kn1[1]; kc1[2] = kn1[2]; kc1[3] = kn1[3]; kc2 = kn2; \
+#define OT_STAGE(E_, H_, K_)                                                             \
+    {                                                                                    \
+      if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                      \
+      ot_eval(a, Q2s, Q3s, sh, (E_), p, b, valid, lane, q, j, uacc, kc1, kc2, H_, K_);   \
+      _Pragma("unroll") for (int t = 0; t < 4; ++t) kc1[t] = kn1[t];                   \
+      kc2 = kn2;                                                                         \
     }
     OT_STAGE(e0, y, k1)
 #pragma unroll
-    for (int j = 0; j < C; ++j) hin[j] = y[j] + (dt * k1[j]) * third;
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + (dt * k1[i]) * third;
     OT_STAGE(e0 + 1, hin, k2)
 #pragma unroll
-    for (int j = 0; j < C; ++j) hin[j] = y[j] + dt * (k2[j] - k1[j] * third);
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + dt * (k2[i] - k1[i] * third);
     OT_STAGE(e0 + 2, hin, k3)
 #pragma unroll
-    for (int j = 0; j < C; ++j) hin[j] = y[j] + dt * ((k1[j] - k2[j]) + k3[j]);
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + dt * ((k1[i] - k2[i]) + k3[i]);
     OT_STAGE(e0 + 3, hin, k4)
 #undef OT_STAGE
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      const float dy = (((k1[j] + 3.0f * (k2[j] + k3[j])) + k4[j]) * dt) * 0.125f;
-      y[j] = y[j] + dy;
+    for (int i = 0; i < C; ++i) {
+      const float dy = (((k1[i] + 3.0f * (k2[i] + k3[i])) + k4[i]) * dt) * 0.125f;
+      y[i] = y[i] + dy;
     }
   }
-  if (p == 0 && valid && half == 0) store_row10(a.y_out + (size_t)b * C, y);
+  if (p == 0 && valid && q == 0) store_row10(a.y_out + (size_t)b * C, y);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.stats[0] = 4 * (a.niters - 1);
     a.stats[1] = a.niters - 1;
@@ -385,17 +438,18 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// backward: one workgroup per 32-row tile, 4 waves = 4 parts of the hidden dimension.  Every
+// backward: one workgroup per 16-row tile, 4 waves = 4 parts of the hidden dimension.  Every
 // wave runs the row math (QP backward, rescale, barrier terms) and g_a2 = Q3^T g_ft in full
-// (identical values in all 4 waves), then its 32 of the 128 rows of g_a1 = Q2^T g_z2 (64 MFMA)
-// and their Q1^T partial; the 4 partials of g_h meet in LDS (double-buffered, one barrier per
-// VJP) and every wave sums them in the same order, so the adjoint state stays replicated.
+// (identical values in all waves), then its 32 of the 128 rows of g_a1 = Q2^T g_z2 (64 MFMA)
+// and their Q1^T partial (8 MFMA); the 4 partials of g_h meet in LDS (double-buffered, one
+// barrier per VJP) and every lane sums its sample's 10 values in the same order, so the adjoint
+// state stays replicated.
 struct OtBwdShared {
-  float gpart[2][4][64][6];
+  float gpart[2][4][64][4];
 };
 
-__device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[4][5],
-                       OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int half, int col,
+__device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[8][3],
+                       OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int q, int j,
                        const float (&g)[C], float (&gy_out)[C]) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
@@ -408,84 +462,81 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
   float g_nom[C], g_low[C], gft[C], ghb[C];
   float gin[C];
 #pragma unroll
-  for (int j = 0; j < C; ++j) gin[j] = valid ? g[j] : 0.f;
+  for (int i = 0; i < C; ++i) gin[i] = valid ? g[i] : 0.f;
   qp_backward_row(gin, v, mu, nominal, g_nom, g_low);
 #pragma unroll
-  for (int j = 0; j < C; ++j) {
-    float g_lo = g_low[j], g_up = 0.f;
+  for (int i = 0; i < C; ++i) {
+    float g_lo = g_low[i], g_up = 0.f;
     if (a.d.scale_nominal) {
       // nominal = span * sig + lower, span = upper - lower
-      gft[j] = ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j];
-      const float g_span = g_nom[j] * sig[j];
-      g_lo = (g_lo + g_nom[j]) - g_span;
+      gft[i] = ((g_nom[i] * span[i]) * (1.0f - sig[i])) * sig[i];
+      const float g_span = g_nom[i] * sig[i];
+      g_lo = (g_lo + g_nom[i]) - g_span;
       g_up = g_span;
     } else {
-      gft[j] = g_nom[j];
+      gft[i] = g_nom[i];
     }
     // lower = -a1 (exp(s1 h) - 1), upper = a2 (1 - h)
-    ghb[j] = ((g_lo * -a.d.alpha_1) * expf(a.d.sigma_1 * h[j])) * a.d.sigma_1 + g_up * -a.d.alpha_2;
+    ghb[i] = ((g_lo * -a.d.alpha_1) * expf(a.d.sigma_1 * h[i])) * a.d.sigma_1 + g_up * -a.d.alpha_2;
   }
-  if (p == 0 && valid && half == 0) {
+  if (p == 0 && valid && q == 0) {
     store_row10(a.gft + r * C, gft);
     if (a.dbg_gft) store_row10(a.dbg_gft + r * C, gft);
   }
-  // g_a2^T = Q3^T g_ft^T (all 128 rows), masked by the saved post-activation a2
-  f32x16 ga[4];
+  // g_a2^T = Q3^T g_ft^T (all 128 hidden, 8 blocks, K = 10 in 3 k-steps), masked by the saved a2
+  f32x4v ga[8];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) ga[mb] = f16_zero();
+  for (int hb = 0; hb < 8; ++hb) ga[hb] = z4();
 #pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const float bs = half ? gft[2 * s + 1] : gft[2 * s];
+  for (int s = 0; s < 3; ++s) {
+    const float bs = sel4(gft, s, q);
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) ga[mb] = mfma32(q3t[mb][s], bs, ga[mb]);
+    for (int hb = 0; hb < 8; ++hb) ga[hb] = mfma16(q3t[hb][s], bs, ga[hb]);
   }
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
-    f32x16 act;
-    load_acc_rows(a.a2 + r * M, mb, half, act);
+  for (int hb = 0; hb < 8; ++hb) {
+    const f32x4 act = *reinterpret_cast<const f32x4*>(a.a2 + r * M + 16 * hb + 4 * q);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ga[mb][q] = act[q] > 0.f ? ga[mb][q] * a.drop_scale : 0.f;
-    if (valid && mb == p) store_acc_rows(a.gz2 + r * M, mb, half, ga[mb]);
+    for (int t = 0; t < 4; ++t) ga[hb][t] = act[t] > 0.f ? ga[hb][t] * a.drop_scale : 0.f;
+    if (valid && (hb >> 1) == p)
+      *reinterpret_cast<f32x4*>(a.gz2 + r * M + 16 * hb + 4 * q) = f32x4{ga[hb][0], ga[hb][1], ga[hb][2], ga[hb][3]};
   }
-  // rows 32p.. of g_a1^T = Q2^T g_z2^T
-  f32x16 gb = f16_zero();
+  // hidden blocks 2p, 2p+1 of g_a1^T = Q2^T g_z2^T (two independent accumulators)
+  f32x4v gb[2] = {z4(), z4()};
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int hb = 0; hb < 8; ++hb) {
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const f32x4 q = *reinterpret_cast<const f32x4*>(Q2Ts + (32 * p + col) * LDQ + 32 * kb + 8 * gg + 4 * half);
+    for (int o = 0; o < 2; ++o) {
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(Q2Ts + (16 * (2 * p + o) + j) * LDQ + 16 * hb + 4 * q);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) gb = mfma32(q[t], ga[kb][4 * gg + t], gb);
+      for (int t = 0; t < 4; ++t) gb[o] = mfma16(qv[t], ga[hb][t], gb[o]);
     }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  {
-    f32x16 act;
-    load_acc_rows(a.a1 + r * M, p, half, act);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) gb[q] = act[q] > 0.f ? gb[q] * a.drop_scale : 0.f;
-    if (valid) store_acc_rows(a.gz1 + r * M, p, half, gb);
-  }
-  // partial g_h^T over hidden rows 32p.. (Q1^T image padded to 32 output rows)
-  f32x16 gh = f16_zero();
-#pragma unroll
-  for (int gg = 0; gg < 4; ++gg) {
-    const f32x4 q = *reinterpret_cast<const f32x4*>(Q1Ts + col * LDQ + 32 * p + 8 * gg + 4 * half);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) gh = mfma32(q[t], gb[4 * gg + t], gh);
   }
 #pragma unroll
-  for (int q = 0; q < 6; ++q) sh.gpart[buf][p][lane][q] = gh[q];
+  for (int o = 0; o < 2; ++o) {
+    const f32x4 act = *reinterpret_cast<const f32x4*>(a.a1 + r * M + 16 * (2 * p + o) + 4 * q);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) gb[o][t] = act[t] > 0.f ? gb[o][t] * a.drop_scale : 0.f;
+    if (valid)
+      *reinterpret_cast<f32x4*>(a.gz1 + r * M + 16 * (2 * p + o) + 4 * q) = f32x4{gb[o][0], gb[o][1], gb[o][2], gb[o][3]};
+  }
+  // partial g_h^T over hidden blocks 2p, 2p+1 (Q1^T image, rows >= 10 zero)
+  f32x4v gh = z4();
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const f32x4 qv = *reinterpret_cast<const f32x4*>(Q1Ts + j * LDQ + 16 * (2 * p + o) + 4 * q);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) gh = mfma16(qv[t], gb[o][t], gh);
+  }
+  *reinterpret_cast<f32x4*>(&sh.gpart[buf][p][lane][0]) = f32x4{gh[0], gh[1], gh[2], gh[3]};
   __syncthreads();
-  f32x16 gs = f16_zero();
 #pragma unroll
-  for (int q = 0; q < 6; ++q)
-    gs[q] = ((sh.gpart[buf][0][lane][q] + sh.gpart[buf][1][lane][q]) + sh.gpart[buf][2][lane][q]) +
-            sh.gpart[buf][3][lane][q];
-  float ghm[C];
-  gather_ft(gs, half, ghm);
-#pragma unroll
-  for (int j = 0; j < C; ++j) gy_out[j] = ghm[j] + ghb[j];
+  for (int i = 0; i < C; ++i) {
+    const int ln = 16 * (i >> 2) + j, rg = i & 3;
+    const float ghm = ((sh.gpart[buf][0][ln][rg] + sh.gpart[buf][1][ln][rg]) + sh.gpart[buf][2][ln][rg]) +
+                      sh.gpart[buf][3][ln][rg];
+    gy_out[i] = ghm + ghb[i];
+  }
 }
 
 __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
@@ -494,25 +545,25 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   float* Q1Ts = smem + M * LDQ;       // Q1^T image [32][LDQ] (rows >= 10 zero)
   OtBwdShared& sh = *reinterpret_cast<OtBwdShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
-  for (int q = threadIdx.x; q < 32 * M; q += blockDim.x) {
-    const int c = q >> 7, i = q & 127;
+  for (int t = threadIdx.x; t < 32 * M; t += blockDim.x) {
+    const int c = t >> 7, i = t & 127;
     Q1Ts[c * LDQ + i] = c < C ? a.Q1[i * C + c] : 0.f;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float q3t[4][5];
+  float q3t[8][3];                    // A operand of g_a2^T: Q3^T[16hb + j][4s + q] = Q3[4s + q][16hb + j]
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int hb = 0; hb < 8; ++hb)
 #pragma unroll
-    for (int s = 0; s < 5; ++s) q3t[mb][s] = a.Q3[(2 * s + half) * M + 32 * mb + col];
-  const int b = blockIdx.x * 32 + col;
+    for (int s = 0; s < 3; ++s) q3t[hb][s] = 4 * s + q < C ? a.Q3[(4 * s + q) * M + 16 * hb + j] : 0.f;
+  const int b = blockIdx.x * TR + j;
   const bool valid = b < a.B;
   float gy[C];
   if (valid) load_row10(a.g_y + (size_t)b * C, gy);
   else
 #pragma unroll
-    for (int j = 0; j < C; ++j) gy[j] = 0.f;
+    for (int i = 0; i < C; ++i) gy[i] = 0.f;
   const float third = 1.0f / 3.0f;
   int buf = 0;
   for (int it = a.niters - 2; it >= 0; --it) {
@@ -521,44 +572,44 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
     const float c8 = dt * 0.125f, c38 = 3.0f * c8;
     float gk1[C], gk2[C], gk3[C], gk4[C], acc[C], gY[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      acc[j] = gy[j];
-      gk1[j] = gy[j] * c8;
-      gk2[j] = gy[j] * c38;
-      gk3[j] = gy[j] * c38;
-      gk4[j] = gy[j] * c8;
+    for (int i = 0; i < C; ++i) {
+      acc[i] = gy[i];
+      gk1[i] = gy[i] * c8;
+      gk2[i] = gy[i] * c38;
+      gk3[i] = gy[i] * c38;
+      gk4[i] = gy[i] * c8;
     }
     const int e0 = 4 * it;
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 3, b, valid, lane, half, col, gk4, gY);  // Y4 = y + dt (k1 - k2 + k3)
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 3, b, valid, lane, q, j, gk4, gY);  // Y4 = y + dt (k1 - k2 + k3)
     buf ^= 1;
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      acc[j] += gY[j];
-      const float d = dt * gY[j];
-      gk1[j] += d;
-      gk2[j] -= d;
-      gk3[j] += d;
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      const float d = dt * gY[i];
+      gk1[i] += d;
+      gk2[i] -= d;
+      gk3[i] += d;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 2, b, valid, lane, half, col, gk3, gY);  // Y3 = y + dt (k2 - k1/3)
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 2, b, valid, lane, q, j, gk3, gY);  // Y3 = y + dt (k2 - k1/3)
     buf ^= 1;
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      acc[j] += gY[j];
-      const float d = dt * gY[j];
-      gk2[j] += d;
-      gk1[j] -= d * third;
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      const float d = dt * gY[i];
+      gk2[i] += d;
+      gk1[i] -= d * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 1, b, valid, lane, half, col, gk2, gY);  // Y2 = y + (dt k1) / 3
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 1, b, valid, lane, q, j, gk2, gY);  // Y2 = y + (dt k1) / 3
     buf ^= 1;
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      acc[j] += gY[j];
-      gk1[j] += (dt * gY[j]) * third;
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      gk1[i] += (dt * gY[i]) * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0, b, valid, lane, half, col, gk1, gY);      // Y1 = y
+    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0, b, valid, lane, q, j, gk1, gY);      // Y1 = y
     buf ^= 1;
 #pragma unroll
-    for (int j = 0; j < C; ++j) gy[j] = acc[j] + gY[j];
+    for (int i = 0; i < C; ++i) gy[i] = acc[i] + gY[i];
   }
 }
 
@@ -592,7 +643,7 @@ OtLayout ot_layout(int B, int E) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  L.xs = o; o += al((size_t)E * 2 * ((B + 31) / 32) * 8 + 256);
+  L.xs = o; o += al((size_t)E * 2 * ((B + TR - 1) / TR) * 8 + 256);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
   L.total = o;
@@ -641,7 +692,7 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.xslots = reinterpret_cast<unsigned long long*>(ws + L.xs);
   a.kw = reinterpret_cast<uint32_t*>(ws + L.kw);
 #ifdef OT_PROFILE
-  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + 31) / 32) + 8;
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + TR - 1) / TR) + 8;
 #endif
   return FIODE_OK;
 }
@@ -682,7 +733,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   if (a.dropout_mode == FIODE_DROPOUT_GIVEN && !masks) return FIODE_EINVAL;
   a.h0 = h0; a.masks = masks; a.offset_dev = offset_dev; a.y_out = y_out; a.stats = stats;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int ntiles = (a.B + 31) / 32;
+  const int ntiles = (a.B + TR - 1) / TR;
   const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);
   // zero the exchange granules (tags) and the status word before every launch
   FIODE_HIP_CHECK(hipMemsetAsync(a.xslots, 0, (size_t)a.E * 2 * ntiles * 8 + 256, st));
@@ -709,7 +760,7 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtBwdShared);
-  hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + 31) / 32), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const OtLayout L = ot_layout(a.B, a.E);
   fiode_internal::WgradIO io{};

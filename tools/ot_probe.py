@@ -16,7 +16,7 @@ for B in (128, 1024):
     for rep in range(3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(); y, st, ws = ops.odetrain_forward(x, h0, w, dyn, cfg); e1.record(); torch.cuda.synchronize()
-    E = ops.odetrain_evals(cfg); nt = (B + 31) // 32
+    E = ops.odetrain_evals(cfg); nt = (B + 15) // 16
     off = ct.c_int64 * 8
     # prof array sits after the exchange granules
     lib = L.lib()
@@ -26,7 +26,7 @@ for B in (128, 1024):
     al = lambda v: (v + 255) & ~255
     xs = offs[7] + al(B * E * 10 * 4)
     prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 16) * 8].view(torch.int64).cpu().numpy()
-    ticks = prof[:5] / E          # 100 MHz wall clock -> 10 ns per tick
+    ticks = prof[:6] / E          # 100 MHz wall clock -> 10 ns per tick
     print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): layer1 {ticks[0]*0.01:.2f} "
-          f"layer2+3 {ticks[1]*0.01:.2f} sum+QP {ticks[2]*0.01:.2f} exchange {ticks[3]*0.01:.2f} "
-          f"final {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
+          f"layer2+3 {ticks[1]*0.01:.2f} barrier+sum+nominal {ticks[5]*0.01:.2f} bisect {ticks[2]*0.01:.2f} "
+          f"exchange {ticks[3]*0.01:.2f} final {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
