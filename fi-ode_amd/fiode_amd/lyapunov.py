@@ -190,20 +190,21 @@ class LyapunovLearning(nn.Module):
     def log(self, name, value, **kw):
         self.logged[name] = value
 
-    def configure_optimizers(self, capturable: bool = False):
+    def configure_optimizers(self, capturable: bool = False, fused: Optional[bool] = None):
         """pl_modules.py:97-147 (Adam/AdamW/SGD; cosine or step schedule; warm-up Adam).
         ``capturable``: Adam/AdamW keep their step counts on the device so the optimizer step
-        can be captured in a hipGraph (fiode_amd.graph_step)."""
-        params = self.parameters()
+        can be captured in a hipGraph (fiode_amd.graph_step).  ``fused``: Adam/AdamW as torch's
+        fused multi-tensor kernel (default on ROCm device parameters)."""
+        params = list(self.parameters())
+        if fused is None:
+            fused = bool(params) and params[0].is_cuda
+        fk = {"fused": True, "capturable": capturable} if fused else {"capturable": capturable}
         if self.current_epoch < self.warmup:
-            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas,
-                                     capturable=capturable)]
+            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas, **fk)]
         if self.opt_name == "Adam":
-            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas,
-                                   capturable=capturable)
+            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
         elif self.opt_name == "AdamW":
-            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas,
-                                    capturable=capturable)
+            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
         elif self.opt_name == "SGD":
             opt = torch.optim.SGD(params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
         else:
