@@ -165,11 +165,13 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_lyap_fwd(LyapArgs a) {
+// 2 workgroups per CU where the grid has them (LDS 72.9 KB, <= 256 registers): one wave's QP
+// (VALU) overlaps the other's MFMA on each SIMD.
+__global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false, C);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256) void k_lyap_fwd(LyapArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_lyap_bwd(LyapArgs a) {
+__global__ __launch_bounds__(256, 2) void k_lyap_bwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2Ts = smem;      // Q2Ts[i][k] = Q2[k][i]
   load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
@@ -608,7 +610,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   };
   const int ntiles = (a.N + 31) / 32;
   const int fwd_blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
-  const size_t lds_fwd = (size_t)(M + 32) * LDQ * sizeof(float);
+  const size_t lds_fwd = (size_t)(M + C) * LDQ * sizeof(float);
   const size_t lds_bwd = (size_t)M * LDQ * sizeof(float);
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);

@@ -107,7 +107,9 @@ __device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, c
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 q = *reinterpret_cast<const f32x4*>(Q3s + col * LDQ + 32 * kb + 8 * g + 4 * half);
+      // rows >= C of the layer-3 A operand are zero (the image may hold only C rows)
+      const f32x4 q = col < C ? *reinterpret_cast<const f32x4*>(Q3s + col * LDQ + 32 * kb + 8 * g + 4 * half)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 4; ++t) z3 = mfma32(q[t], z2[kb][4 * g + t], z3);
     }
@@ -117,14 +119,14 @@ __device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, c
 // Stage the 128x128 mlp_to_mlp weight (optionally transposed) and the 10x128 mlp_to_hidden weight
 // (zero-padded to 32 rows) into padded LDS images.
 __device__ __forceinline__ void load_weight_images(const float* Q2, const float* Q3, float* Q2s, float* Q3s,
-                                                   bool transpose_q2) {
+                                                   bool transpose_q2, int q3_rows = 32) {
   for (int e = threadIdx.x; e < M * M; e += blockDim.x) {
     const int i = e >> 7, k = e & 127;
     if (transpose_q2) Q2s[k * LDQ + i] = Q2[e];
     else Q2s[i * LDQ + k] = Q2[e];
   }
   if (Q3s)
-    for (int e = threadIdx.x; e < 32 * M; e += blockDim.x) {
+    for (int e = threadIdx.x; e < q3_rows * M; e += blockDim.x) {
       const int i = e >> 7, k = e & 127;
       Q3s[i * LDQ + k] = i < C ? Q3[i * M + k] : 0.f;
     }
