@@ -60,6 +60,7 @@ struct LyapArgs {
   float *a1, *a2, *gz2, *gz1;   // [N][M]
   float* gft;          // [N][C]
   uint4* kw;           // [4][N] dropout keep words (bit t of word mb = keep hidden 32mb+t)
+  float* Q2T;          // [M][M] mlp_to_mlp transposed (written by k_static_proj)
   float* tile_sc;      // [ntiles][4]
   float* slabs;        // [B*parts][SLAB]
   float* g_u;          // [B][M]
@@ -134,6 +135,7 @@ __device__ __forceinline__ void keep_words(const LyapArgs& a, int row, int set, 
 __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
   const int b = blockIdx.x, i = threadIdx.x;
   if (b == 0 && i < 2) a.conv[i] = 0xFFFFFFFFu;
+  if (b < M) a.Q2T[b * M + i] = a.Q2[i * M + b];   // Q2^T for the backward's LDS image (coalesced stores)
   if (b >= a.B) return;
   float s = 0.f;
   const float* xb = a.x_feat + (size_t)b * FIODE_X;
@@ -219,8 +221,8 @@ __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
 
 __global__ __launch_bounds__(256, 2) void k_lyap_bwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Q2Ts = smem;      // Q2Ts[i][k] = Q2[k][i]
-  load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
+  float* Q2Ts = smem;      // Q2Ts[i][k] = Q2[k][i], staged from the pre-transposed copy (no LDS bank conflicts)
+  load_weight_images(a.Q2T, nullptr, Q2Ts, nullptr, false);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q3t[4][5];         // A operand of g_a2^T = Q3^T g_ft^T: Q3[2s+half][32mb+col]
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
 
 // ---- workspace ----------------------------------------------------------------------------------
 struct WsLayout {
-  size_t conv, u, h, ft, a1, a2, gz2, gz1, gft, kw, tsc, slabs, gu, total;
+  size_t conv, u, h, ft, a1, a2, gz2, gz1, gft, kw, tsc, slabs, gu, q2t, total;
 };
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline void parts_for(int B, int S, int& parts, int& chunk) {
@@ -521,6 +523,7 @@ inline WsLayout ws_layout(int B, int S) {
   L.tsc = o; o = al(o + ((N + 31) / 32) * 16);
   L.slabs = o; o = al(o + (size_t)B * parts * SLAB * 4);
   L.gu = o; o = al(o + (size_t)B * M * 4);
+  L.q2t = o; o = al(o + (size_t)M * M * 4);
   L.total = o;
   return L;
 }
@@ -593,6 +596,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.tile_sc = reinterpret_cast<float*>(ws + L.tsc);
   a.slabs = reinterpret_cast<float*>(ws + L.slabs);
   a.g_u = reinterpret_cast<float*>(ws + L.gu);
+  a.Q2T = reinterpret_cast<float*>(ws + L.q2t);
   a.scalars = io->scalars;
   a.h_out = io->h_out; a.V = io->V; a.Vdot = io->Vdot; a.f = io->f; a.f_log = io->f_log;
   a.qp_lower = io->qp_lower; a.qp_nominal = io->qp_nominal; a.g_ftilde = io->g_ftilde;
@@ -613,7 +617,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   const size_t lds_fwd = (size_t)(M + C) * LDQ * sizeof(float);
   const size_t lds_bwd = (size_t)M * LDQ * sizeof(float);
   if ((rc = mark())) return rc;
-  hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);
+  hipLaunchKernelGGL(k_static_proj, dim3(B > M ? B : M), dim3(128), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_prep, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
