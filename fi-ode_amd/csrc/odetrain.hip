@@ -20,11 +20,13 @@
 // Weight gradients: the training step's wgrad chain over rows r = b*E + e (wgrad.h).
 #include "common.h"
 #include "tile.h"
+#include "tile16.h"
 #include "wgrad.h"
 #include "../../include/fiode.h"
 
 namespace {
 using namespace fiode_tile;
+using namespace fiode_t16;
 
 
 struct OTArgs {
@@ -83,41 +85,6 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// MFMA layout: v_mfma_f32_16x16x4_f32, "hidden on M, samples on N".  A tile is TR = 16 rows
-// (samples); lane l holds sample j = l & 15 of the tile and q = l >> 4 selects the K slot.
-// A operand A[i = j][k = q], B operand B[k = q][col = j]; accumulator register r holds
-// D[row = 4q + r][col = j].  A layer's accumulator block hb (hidden 16hb + 4q + r) is directly
-// the B operand of the next layer's k-steps (hb, r), whose k index 4q' + r ... is hidden
-// 16hb + 4q + r, so the A operand of that k-step is Q[out][16hb + 4q + r] (r = 0..3): one
-// ds_read_b128 of 4 consecutive weights.  32-cycle issue, 40-cycle dependent latency: every
-// accumulation runs >= 2 independent accumulators except the short layer-3 chain.
-constexpr int TR = 16;
-
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4v z4() { return f32x4v{0.f, 0.f, 0.f, 0.f}; }
-
-// relu(dropout(z)) on a 16x16 block: hidden 16hb + 4q + r, keep bit from w = kw[hidden >> 5]
-__device__ __forceinline__ void dropout_relu16(f32x4v& z, uint32_t w, int hb, int q, float scale) {
-  const int sh = 16 * (hb & 1) + 4 * q;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const bool keep = (w >> (sh + r)) & 1u;
-    z[r] = keep ? fmaxf(z[r] * scale, 0.f) : 0.f;
-  }
-}
-__device__ __forceinline__ float sel4(const float (&v)[C], int s, int q) {   // v[4s + q], 0 past C
-  const int k = 4 * s + q;
-  float x = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    if (4 * s + t < C) x = (q == t) ? v[4 * s + t] : x;
-  return k < C ? x : 0.f;
-}
-
-// ---------------------------------------------------------------------------------------------
 // forward: one workgroup per 16-row tile, persistent over all evals; 4 waves = 4 parts of the
 // hidden dimension.  Per eval every wave computes layer 1 in full (24 MFMA), its 32 of the 128
 // layer-2 outputs (64 MFMA) and their layer-3 partial (8 MFMA); the partials meet in LDS and
@@ -139,71 +106,6 @@ struct OtShared {
   int pad[2];
 };
 
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-
-__device__ __forceinline__ void publish_mask(unsigned long long* slot, unsigned epoch, uint32_t mask) {
-  __hip_atomic_store((gu64_t*)(slot), ((unsigned long long)epoch << 32) | mask, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...)
-__device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int ntiles, unsigned epoch,
-                                                 int32_t* status, int lane) {
-  uint32_t acc = 0xFFFFFFFFu;
-  for (int base = 0; base < ntiles; base += 64) {
-    const int t = base + lane;
-    unsigned spins = 0;
-    for (;;) {
-      bool ok = true;
-      unsigned long long x = 0;
-      if (t < ntiles) {
-        x = __hip_atomic_load((gu64_t*)(slots + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = (unsigned)(x >> 32) == epoch;
-      }
-      if (__all(ok)) {
-        if (t < ntiles) acc &= (uint32_t)x;
-        break;
-      }
-      if (++spins > (1u << 22)) {           // ~0.5 s: a non-resident tile; record and give up
-        if (lane == 0) atomicMax(status, 4);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  return wave_and(acc);
-}
-
-// The bisection of FastBarrierProjectionNoUpper (qp_bisect, common.h) split so it can stop and
-// resume: iterations [from, to] from the bracket state (lo, hi), recording mu per iteration.  The
-// returned mask is the WAVE's: bit it set iff every valid lane converged at iteration it (ballot).
-__device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float (&nom)[C], float& lo, float& hi) {
-  hi = nom[0] - lower[0];
-  lo = nom[0];
-#pragma unroll
-  for (int j = 1; j < C; ++j) {
-    hi = fmaxf(hi, nom[j] - lower[j]);
-    lo = fminf(lo, nom[j]);
-  }
-}
-__device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], const float (&nom)[C], int from, int to,
-                                                    float tol, float& lo, float& hi, float* mu_rec, bool rec,
-                                                    bool valid) {
-  uint32_t conv = 0;
-  for (int it = from; it <= to; ++it) {
-    const float mu = (hi - lo) / 2.0f + lo;
-    float eps = 0.f;
-#pragma unroll
-    for (int j = 0; j < C; ++j) eps = eps + fmaxf(nom[j] - mu, lower[j]);
-    if (rec) mu_rec[it] = mu;
-    const unsigned long long open = __ballot(valid && !(fabsf(eps) < tol));
-    conv |= (open == 0ull ? 1u : 0u) << it;
-    lo = eps > 0.f ? mu : lo;
-    hi = eps < 0.f ? mu : hi;
-  }
-  return conv;
-}
-
 #ifdef OT_PROFILE
 #define OT_MARK(i) do { const uint64_t t_ = wall_clock64(); if (blockIdx.x == 0 && threadIdx.x == 0) \
     atomicAdd((unsigned long long*)&a.prof[i], (unsigned long long)(t_ - t_prev)); t_prev = t_; } while (0)
@@ -221,105 +123,18 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   uint64_t t_prev = wall_clock64();
 #endif
   if (p == 0 && valid && q == 0) store_row10(a.hs + r * C, h);
-  // layer 1 (full): z1 = u[b] + Q1 h, 8 hidden blocks, K = 10 in 3 k-steps
-  f32x4v z1[8];
-#pragma unroll
-  for (int hb = 0; hb < 8; ++hb) z1[hb] = uacc[hb];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const float bs = sel4(h, s, q);
-    const bool kin = 4 * s + q < C;
-#pragma unroll
-    for (int hb = 0; hb < 8; ++hb) {
-      const float av = kin ? sh.Q1s[(16 * hb + j) * C + 4 * s + q] : 0.f;
-      z1[hb] = mfma16(av, bs, z1[hb]);
-    }
-  }
-#pragma unroll
-  for (int hb = 0; hb < 8; ++hb) dropout_relu16(z1[hb], kw1[hb >> 1], hb, q, a.drop_scale);
-  OT_MARK(0);
-  if (valid) {                 // part p saves a1 blocks 2p, 2p+1
-#pragma unroll
-    for (int hb = 0; hb < 8; ++hb)
-      if ((hb >> 1) == p)
-        *reinterpret_cast<f32x4*>(a.a1 + r * M + 16 * hb + 4 * q) = f32x4{z1[hb][0], z1[hb][1], z1[hb][2], z1[hb][3]};
-  }
-  // layer 2, output blocks 2p, 2p+1: z2 = b2 + Q2[16 ob.., :] a1 (two independent accumulators)
-  f32x4v z2[2];
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.b2 + 16 * (2 * p + o) + 4 * q);
-    z2[o] = f32x4v{bv[0], bv[1], bv[2], bv[3]};
-  }
-#pragma unroll
-  for (int hb = 0; hb < 8; ++hb) {
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      const f32x4 qv = *reinterpret_cast<const f32x4*>(Q2s + (16 * (2 * p + o) + j) * LDQ + 16 * hb + 4 * q);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) z2[o] = mfma16(qv[t], z1[hb][t], z2[o]);
-    }
-  }
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    dropout_relu16(z2[o], kw2p, 2 * p + o, q, a.drop_scale);
-    if (valid)
-      *reinterpret_cast<f32x4*>(a.a2 + r * M + 16 * (2 * p + o) + 4 * q) = f32x4{z2[o][0], z2[o][1], z2[o][2], z2[o][3]};
-  }
-  // layer-3 partial over hidden blocks 2p, 2p+1 (bias on part 0); rows >= 10 of Q3s are zero
-  f32x4v z3 = z4();
-  if (p == 0) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) z3[t] = 4 * q + t < C ? a.b3[4 * q + t] : 0.f;
-  }
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const f32x4 qv = *reinterpret_cast<const f32x4*>(Q3s + j * LDQ + 16 * (2 * p + o) + 4 * q);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) z3 = mfma16(qv[t], z2[o][t], z3);
-  }
-  *reinterpret_cast<f32x4*>(&sh.zpart[p][lane][0]) = f32x4{z3[0], z3[1], z3[2], z3[3]};
+  mlp16_part(sh.Q1s, Q2s, Q3s, a.b2, a.b3, uacc, h, kw1, kw2p, a.drop_scale, p, q, j, valid ? a.a1 + r * M : nullptr,
+             valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0]);
   OT_MARK(1);
   __syncthreads();
-  // this lane's sample j: output i sits in lane 16 (i >> 2) + j, register i & 3, of every part
   float ft[C];
-#pragma unroll
-  for (int i = 0; i < C; ++i) {
-    const int ln = 16 * (i >> 2) + j, rg = i & 3;
-    ft[i] = ((sh.zpart[0][ln][rg] + sh.zpart[1][ln][rg]) + sh.zpart[2][ln][rg]) + sh.zpart[3][ln][rg];
-  }
+  ft16_sum(sh.zpart, j, ft);
   float lower[C], nominal[C], sig[C], span[C];
   barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
   OT_MARK(5);
-  // Speculative exit: bisect up to the previous eval's exit + 3 and exchange; only if no iteration
-  // <= that converged on every row of the batch, continue to max_iter - 1 and exchange again.
-  // K is the same as the full sweep's (the lowest all-converged iteration wins either way).
-  const int last = a.d.max_iter - 1;
-  const int kspec = min(last, sh.Kprev + 3);
-  float lo, hi;
-  qp_bracket(lower, nominal, lo, hi);
   float* rec = &sh.mu_rec[p][j][0];
-  uint32_t conv = qp_bisect_range(lower, nominal, 0, kspec, a.d.tol, lo, hi, rec, q == 0, valid);
-  OT_MARK(2);
-  const int ntiles = gridDim.x;
-  unsigned long long* slots = a.xslots + (size_t)e * 2 * ntiles;
-  if (p == 0) {
-    if (lane == 0) publish_mask(slots + blockIdx.x, (unsigned)e + 1u, conv);
-    const uint32_t all = gather_masks(slots, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
-    const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
-    const uint32_t bits = all & lowm;
-    if (lane == 0) sh.K = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
-  }
-  __syncthreads();
-  if (sh.K < 0) {                       // block-uniform: every tile saw the same masks
-    conv |= qp_bisect_range(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, rec, q == 0, valid);
-    if (p == 0) {
-      if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, (unsigned)e + 1u, conv);
-      const uint32_t all = gather_masks(slots + ntiles, ntiles, (unsigned)e + 1u, a.stats + 3, lane);
-      if (lane == 0) sh.K = qp_exit_iter(all, a.d.max_iter);
-    }
-    __syncthreads();
-  }
+  qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
+            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K);
   OT_MARK(3);
   const int K = sh.K;
   const float mu = sh.mu_rec[p][j][K];
