@@ -230,6 +230,7 @@ def main():
     tot = [0.0] * nk
     for r in range(args.prof_reps + 2):
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(nk + 1)]
+        torch.cuda._sleep(4_000_000)
         ops.lyap_step(feat, y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"], sampler=plan["sampler"],
                       dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"], offset=r, events=evs)
         torch.cuda.synchronize()
@@ -247,6 +248,9 @@ def main():
         t_f = t_b = 0.0
         for r in range(args.prof_reps + 2):
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            # keep the stream busy while the host enqueues, so e0..e2 time GPU work only (not the
+            # host's allocation / argument packing between the event records)
+            torch.cuda._sleep(4_000_000)
             e0.record()
             yo, _, ws = ops.odetrain_forward(feat, h0, w, oplan["dyn"], oplan["cfg"], offset_dev=oplan["offset_dev"])
             e1.record()

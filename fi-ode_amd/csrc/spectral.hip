@@ -1,0 +1,568 @@
+// Fused spectral Cayley map of the backbone's orthogonal convolutions (gfx950).
+//
+// CayleyConv (fiode_amd/cayley.py; the absent libs/ortho_conv of models.py:12-14) parametrises a
+// circular k x k convolution on n x n inputs by one cout x cin channel matrix per rFFT frequency
+// f = (ka, kb), ka < n, kb <= n/2 (nf = n (n/2 + 1) of them):
+//     Wf[f] = shift(f) * conj(rfft2(w, (n, n)))[f]  =  sum_t w_t e^{i theta_t(f)},
+//     theta_t(f) = 2 pi (ka (a_t + s) + kb (b_t + s)) / n,  s = -(k - 1) / 2,  tap t = (a_t, b_t),
+// and maps every Wf[f] to an orthonormal (or orthonormal-column / -row) matrix
+//     Q[f] = cayley(alpha Wf[f] / ||Wf||)   (one alpha and one norm over all frequencies),
+//     X = sc Wf (transposed when cin > cout), U = X[:K], V = X[K:], K = min(cout, cin),
+//     M = I + U - U^H + V^H V,  Q = [2 M^-1 - I ; -2 V M^-1].
+// In PyTorch this is ~35 small kernels forward and ~40 backward per layer (rfft2, permute copies,
+// the norm, the Gram and inverse batches, slicing, cat, and their autograd); here it is:
+//   k_spec_dft    Wf of every frequency as a 9-tap sum over a table of n-th roots of unity (no
+//                 FFT), stored in X's orientation for both directions, and ||Wf||^2 as per-block
+//                 partial sums (fixed order, no atomics);
+//   k_spec_fwd    one workgroup per frequency: X = sc Wf into LDS, M's Gram in the register tile
+//                 of the Gauss-Jordan inverse (gj.h), the inverse, Q;
+//   k_spec_bwd    one workgroup per frequency: the analytic Cayley backward (as _CayleyScaledFn):
+//                 G_inv = 2 Gt - 2 V^H Gb, G_M = -M^-H G_inv M^-H, gU = G_M - G_M^H,
+//                 gV = V (G_M + G_M^H) - 2 Gb M^-H, and the partial D = Re<gX, Wf>;
+//   k_spec_taps   dL/dw_t = sum_f Re(e^{-i theta_t(f)} (sc gX[f] - alpha D / ||Wf||^3 Wf[f])),
+//                 dL/dalpha = D / ||Wf|| (torch's convention for complex gradients:
+//                 g = dL/dRe + i dL/dIm, so a real w with z = c w gets Re(conj(c) g)).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "fiode.h"
+#include "gj.h"
+
+namespace {
+
+using fiode_gj::ComplexOps;
+typedef float2 c32;
+
+constexpr int NORM_THREADS = 256;
+constexpr int KS = 3;            // kernel size of the fused path (KWLarge: 3 x 3)
+constexpr int TAPS = KS * KS;
+constexpr int SH = -(KS - 1) / 2;
+
+__device__ __forceinline__ c32 cmul(c32 a, c32 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__device__ __forceinline__ c32 cconj(c32 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ c32 cadd(c32 a, c32 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ c32 csub(c32 a, c32 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ c32 cscale(c32 a, float s) { return make_float2(a.x * s, a.y * s); }
+// acc += conj(a) b
+__device__ __forceinline__ c32 cfma_conj(c32 a, c32 b, c32 acc) {
+  return make_float2(fmaf(a.y, b.y, fmaf(a.x, b.x, acc.x)), fmaf(-a.y, b.x, fmaf(a.x, b.y, acc.y)));
+}
+// acc += a b
+__device__ __forceinline__ c32 cfma(c32 a, c32 b, c32 acc) {
+  return make_float2(fmaf(-a.y, b.y, fmaf(a.x, b.x, acc.x)), fmaf(a.y, b.x, fmaf(a.x, b.y, acc.y)));
+}
+
+struct SpecArgs {
+  int cout, cin, n, nf, half;       // half = n/2 + 1
+  int R, K, wide;                   // X is R x K; wide: X = Wf^T
+  int nparts;                       // norm partial blocks
+  const float* w;                   // [cout][cin][ks][ks]
+  const float* alpha;               // [1]
+  float* part;                      // [nparts] ||Wf||^2 partials
+  float* dpart;                     // [nf] D partials
+  c32* Q;                           // [nf][cout][cin]
+  c32* inv;                         // [nf][K][K]
+  const c32* gQ;                    // [nf][cout][cin]
+  c32* gX;                          // [nf][cout][cin] (backward scratch)
+  c32* Wx;                          // [nf][R][K] unscaled Wf in X's orientation (fwd -> bwd)
+  float* gw;                        // [cout][cin][ks][ks]
+  float* galpha;                    // [1]
+};
+
+__device__ __forceinline__ c32 root(int m, int n) {
+  float sn, cs;
+  sincospif(2.0f * (float)m / (float)n, &sn, &cs);
+  return make_float2(cs, sn);
+}
+
+// Sum of p[0..n) in a fixed order that does not depend on the block size (wave 0: lane-strided
+// partial sums, then a butterfly), broadcast to the block through `slot`.  Every kernel that needs
+// ||Wf|| or D therefore sees bit-identical values.  Call from all threads (contains a barrier).
+__device__ __forceinline__ float block_sum_fixed(const float* __restrict__ p, int n, float* slot) {
+  if (threadIdx.x < 64) {
+    float v = 0.f;
+    for (int i = threadIdx.x; i < n; i += 64) v += p[i];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (threadIdx.x == 0) *slot = v;
+  }
+  __syncthreads();
+  return *slot;
+}
+
+__device__ __forceinline__ float norm_scale(const SpecArgs& a, float* slot, float* nrm_out = nullptr) {
+  const float nrm = sqrtf(block_sum_fixed(a.part, a.nparts, slot));
+  if (nrm_out) *nrm_out = nrm;
+  return a.alpha[0] / nrm;
+}
+
+// ---- Wf for all frequencies (X orientation) + ||Wf||^2 partials ---------------------------------
+// Thread p of the x-grid owns X element p = (r, c) of every frequency in its y-group; its taps are
+// read once, the frequencies come from an n-entry table of roots of unity, and the stores
+// Wx[f][p] are coalesced.  ||Wf||^2 = sum |Wf|^2 over the half spectrum, one partial per block.
+constexpr int DFT_FG = 16;      // frequencies per y-block
+__global__ void __launch_bounds__(NORM_THREADS) k_spec_dft(SpecArgs a) {
+  __shared__ c32 roots[64];
+  __shared__ float red[NORM_THREADS / 64];
+  const int tid = threadIdx.x;
+  for (int m = tid; m < a.n; m += NORM_THREADS) roots[m] = root(m, a.n);
+  __syncthreads();
+  const int p = blockIdx.x * NORM_THREADS + tid;
+  const int RK = a.R * a.K;
+  float q = 0.f;
+  if (p < RK) {
+    const int r = p / a.K, c = p - r * a.K;
+    const int co = a.wide ? c : r, ci = a.wide ? r : c;
+    float w[TAPS];
+    const float* wp = a.w + ((int64_t)co * a.cin + ci) * TAPS;
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) w[t] = wp[t];
+    const int f1 = min(a.nf, (int)(blockIdx.y + 1) * DFT_FG);
+    for (int f = blockIdx.y * DFT_FG; f < f1; ++f) {
+      const int ka = f / a.half, kb = f - ka * a.half;
+      c32 z = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        int m = (ka * (t / KS + SH) + kb * (t % KS + SH)) % a.n;
+        m = m < 0 ? m + a.n : m;
+        const c32 e = roots[m];
+        z.x = fmaf(w[t], e.x, z.x);
+        z.y = fmaf(w[t], e.y, z.y);
+      }
+      a.Wx[(int64_t)f * RK + p] = z;
+      q = fmaf(z.x, z.x, fmaf(z.y, z.y, q));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  if ((tid & 63) == 0) red[tid >> 6] = q;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = 0; i < NORM_THREADS / 64; ++i) s += red[i];
+    a.part[blockIdx.y * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// ---- forward: one workgroup per frequency --------------------------------------------------------
+template <int NP, int TR, int TC, int NT>
+__global__ void __launch_bounds__(NT) k_spec_fwd(SpecArgs a) {
+  typedef fiode_gj::GJ<ComplexOps, NP, TR, TC> G;
+  static_assert(G::NT == NT, "thread count");
+  extern __shared__ c32 X[];                  // [R][K]: rows < K hold U, later M^-1
+  __shared__ typename G::Smem gsm;
+  __shared__ float slot;
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int R = a.R, K = a.K;
+  const float sc = norm_scale(a, &slot);
+  const c32* Wf = a.Wx + (int64_t)f * R * K;
+#pragma unroll 4
+  for (int idx = tid; idx < R * K; idx += NT) X[idx] = cscale(Wf[idx], sc);
+  __syncthreads();
+  // M = I + U - U^H + V^H V in the Gauss-Jordan register tile
+  const int r0 = (tid / G::CT) * TR, c0 = (tid % G::CT) * TC;
+  c32 m[TR][TC];
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      if (i < K && j < K) m[r][c] = csub(X[i * K + j], cconj(X[j * K + i]));
+      else m[r][c] = make_float2(0.f, 0.f);
+      if (i == j) m[r][c].x += 1.0f;
+    }
+#pragma unroll 4
+  for (int rr = K; rr < R; ++rr) {
+    c32 xi[TR], xj[TC];
+#pragma unroll
+    for (int r = 0; r < TR; ++r) xi[r] = (r0 + r < K) ? X[rr * K + r0 + r] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < TC; ++c) xj[c] = (c0 + c < K) ? X[rr * K + c0 + c] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) m[r][c] = cfma_conj(xi[r], xj[c], m[r][c]);
+  }
+  G::invert(m, K, gsm);                       // (barriers inside: every read of U above is done)
+  c32* invg = a.inv + (int64_t)f * K * K;
+  G::store(m, invg, K, K);
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c)
+      if (r0 + r < K && c0 + c < K) X[(r0 + r) * K + c0 + c] = m[r][c];
+  __syncthreads();
+  // Q = [2 M^-1 - I ; -2 V M^-1], written in the [cout][cin] orientation
+  c32* Qf = a.Q + (int64_t)f * a.cout * a.cin;
+  auto put = [&](int r, int j, c32 v) {
+    if (a.wide) Qf[(int64_t)j * a.cin + r] = v;
+    else Qf[(int64_t)r * a.cin + j] = v;
+  };
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      if (i < K && j < K) {
+        c32 v = cscale(m[r][c], 2.0f);
+        if (i == j) v.x -= 1.0f;
+        put(i, j, v);
+      }
+    }
+  for (int q0 = K; q0 < R; q0 += NP) {        // bottom rows in NP-row chunks, same register tile
+    c32 acc[TR][TC];
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) acc[r][c] = make_float2(0.f, 0.f);
+#pragma unroll 4
+    for (int k = 0; k < K; ++k) {
+      c32 v[TR], iv[TC];
+#pragma unroll
+      for (int r = 0; r < TR; ++r) v[r] = (q0 + r0 + r < R) ? X[(q0 + r0 + r) * K + k] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < TC; ++c) iv[c] = (c0 + c < K) ? X[k * K + c0 + c] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) acc[r][c] = cfma(v[r], iv[c], acc[r][c]);
+    }
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) {
+        const int rr = q0 + r0 + r, j = c0 + c;
+        if (rr < R && j < K) put(rr, j, cscale(acc[r][c], -2.0f));
+      }
+  }
+}
+
+// ---- backward: one workgroup per frequency -------------------------------------------------------
+template <int NP, int TR, int TC, int NT>
+__global__ void __launch_bounds__(NT) k_spec_bwd(SpecArgs a) {
+  typedef fiode_gj::GJ<ComplexOps, NP, TR, TC> G;
+  static_assert(G::NT == NT, "thread count");
+  extern __shared__ c32 sm[];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int R = a.R, K = a.K, RV = R - K;
+  c32* V = sm;                    // [RV][K]  sc * V
+  c32* Ub = sm + RV * K;          // [K][K]   G chunk staging, then M^-H
+  c32* Bm = Ub + K * K;           // [K][K]   G_inv, T1, G_M, H
+  // (the dynamic image may take all 160 KiB: the norm's broadcast slot borrows Ub, which is first
+  // written after the next barrier)
+  const float sc = norm_scale(a, reinterpret_cast<float*>(Ub));
+  const c32* Wf = a.Wx + (int64_t)f * R * K;      // unscaled, X orientation
+#pragma unroll 4
+  for (int idx = tid; idx < RV * K; idx += NT) V[idx] = cscale(Wf[K * K + idx], sc);
+  const c32* Gf = a.gQ + (int64_t)f * a.cout * a.cin;
+  auto gget = [&](int r, int j) -> c32 {        // G in X's orientation
+    return a.wide ? Gf[(int64_t)j * a.cin + r] : Gf[(int64_t)r * a.cin + j];
+  };
+  const int r0 = (tid / G::CT) * TR, c0 = (tid % G::CT) * TC;
+  // G_inv = 2 Gt - 2 V^H Gb   (Gb staged through Ub in K-row chunks)
+  c32 acc[TR][TC];
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) acc[r][c] = make_float2(0.f, 0.f);
+  for (int q0 = 0; q0 < RV; q0 += K) {
+    const int rows = min(K, RV - q0);
+    __syncthreads();
+    for (int idx = tid; idx < rows * K; idx += NT) {
+      const int r = idx / K, c = idx - r * K;
+      Ub[idx] = gget(K + q0 + r, c);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < rows; ++rr) {
+      c32 vi[TR], gj[TC];
+#pragma unroll
+      for (int r = 0; r < TR; ++r) vi[r] = (r0 + r < K) ? V[(q0 + rr) * K + r0 + r] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < TC; ++c) gj[c] = (c0 + c < K) ? Ub[rr * K + c0 + c] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) acc[r][c] = cfma_conj(vi[r], gj[c], acc[r][c]);
+    }
+  }
+  __syncthreads();
+  const c32* invg = a.inv + (int64_t)f * K * K;
+  for (int idx = tid; idx < K * K; idx += NT) {   // Ub = M^-H
+    const int i = idx / K, j = idx - i * K;
+    Ub[idx] = cconj(invg[(int64_t)j * K + i]);
+  }
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      if (i < K && j < K) Bm[i * K + j] = cscale(csub(gget(i, j), acc[r][c]), 2.0f);
+    }
+  __syncthreads();
+  // T1 = G_inv M^-H ;  G_M = -M^-H T1
+  auto kxk = [&](const c32* A, const c32* Bq, c32 (&o)[TR][TC]) {
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) o[r][c] = make_float2(0.f, 0.f);
+#pragma unroll 4
+    for (int k = 0; k < K; ++k) {
+      c32 x[TR], y[TC];
+#pragma unroll
+      for (int r = 0; r < TR; ++r) x[r] = (r0 + r < K) ? A[(r0 + r) * K + k] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < TC; ++c) y[c] = (c0 + c < K) ? Bq[k * K + c0 + c] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) o[r][c] = cfma(x[r], y[c], o[r][c]);
+    }
+  };
+  auto tile_to = [&](c32* dst, const c32 (&o)[TR][TC], float s) {
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c)
+        if (r0 + r < K && c0 + c < K) dst[(r0 + r) * K + c0 + c] = cscale(o[r][c], s);
+  };
+  kxk(Bm, Ub, acc);
+  __syncthreads();
+  tile_to(Bm, acc, 1.0f);
+  __syncthreads();
+  kxk(Ub, Bm, acc);
+  __syncthreads();
+  tile_to(Bm, acc, -1.0f);                         // Bm = G_M
+  __syncthreads();
+  // gU = G_M - G_M^H (output rows < K), H = G_M + G_M^H (kept in Bm)
+  c32* gXf = a.gX + (int64_t)f * a.cout * a.cin;
+  auto gput = [&](int r, int j, c32 v) {
+    if (a.wide) gXf[(int64_t)j * a.cin + r] = v;
+    else gXf[(int64_t)r * a.cin + j] = v;
+  };
+  c32 hreg[TR][TC];
+  float dsum = 0.f;
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      hreg[r][c] = make_float2(0.f, 0.f);
+      if (i < K && j < K) {
+        const c32 gm = Bm[i * K + j], gmt = cconj(Bm[j * K + i]);
+        const c32 gu = csub(gm, gmt);
+        hreg[r][c] = cadd(gm, gmt);
+        gput(i, j, gu);
+        const c32 u = Wf[i * K + j];
+        dsum = fmaf(gu.x, u.x, dsum);
+        dsum = fmaf(gu.y, u.y, dsum);
+      }
+    }
+  __syncthreads();
+  tile_to(Bm, hreg, 1.0f);                          // Bm = H
+  __syncthreads();
+  // gV = V H - 2 Gb M^-H, NP-row chunks
+  for (int q0 = 0; q0 < RV; q0 += NP) {
+    c32 o[TR][TC];
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) o[r][c] = make_float2(0.f, 0.f);
+#pragma unroll 4
+    for (int k = 0; k < K; ++k) {
+      c32 v[TR], gb[TR], h[TC], ih[TC];
+#pragma unroll
+      for (int r = 0; r < TR; ++r) {
+        const int rr = q0 + r0 + r;
+        v[r] = rr < RV ? V[rr * K + k] : make_float2(0.f, 0.f);
+        gb[r] = rr < RV ? gget(K + rr, k) : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int c = 0; c < TC; ++c) {
+        h[c] = (c0 + c < K) ? Bm[k * K + c0 + c] : make_float2(0.f, 0.f);
+        ih[c] = (c0 + c < K) ? Ub[k * K + c0 + c] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) o[r][c] = cfma(v[r], h[c], cfma(cscale(gb[r], -2.0f), ih[c], o[r][c]));
+    }
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) {
+        const int rr = q0 + r0 + r, j = c0 + c;
+        if (rr < RV && j < K) {
+          gput(K + rr, j, o[r][c]);
+          const c32 v = Wf[(K + rr) * K + j];
+          dsum = fmaf(o[r][c].x, v.x, dsum);
+          dsum = fmaf(o[r][c].y, v.y, dsum);
+        }
+      }
+  }
+  // D partial of this frequency (fixed-order reduction)
+  for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(Ub);
+  if ((tid & 63) == 0) red[tid >> 6] = dsum;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+    a.dpart[f] = s;
+  }
+}
+
+// ---- taps: TP (co, ci) pairs per block, FG frequency groups per pair ---------------------------
+constexpr int TAPS_TP = 32, TAPS_FG = 8;
+__global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
+  __shared__ c32 roots[64];
+  __shared__ float red[TAPS_FG][TAPS][TAPS_TP + 1];
+  const int tid = threadIdx.x, pl = tid % TAPS_TP, fg = tid / TAPS_TP;
+  for (int m = tid; m < a.n; m += TAPS_TP * TAPS_FG) roots[m] = root(m, a.n);
+  __syncthreads();
+  __shared__ float slot[2];
+  float nrm;
+  const float sc = norm_scale(a, &slot[0], &nrm);
+  const float D = block_sum_fixed(a.dpart, a.nf, &slot[1]);
+  const float cw = a.alpha[0] * D / (nrm * nrm * nrm);
+  if (blockIdx.x == 0 && tid == 0) a.galpha[0] = D / nrm;
+  const int pair = blockIdx.x * TAPS_TP + pl;
+  const int npair = a.cout * a.cin;
+  float w[TAPS], g[TAPS];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) {
+    w[t] = pair < npair ? a.w[(int64_t)pair * TAPS + t] : 0.f;
+    g[t] = 0.f;
+  }
+  if (pair < npair) {
+    for (int f = fg; f < a.nf; f += TAPS_FG) {
+      const int ka = f / a.half, kb = f - ka * a.half;
+      c32 e[TAPS];
+      c32 wf = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        int m = (ka * (t / KS + SH) + kb * (t % KS + SH)) % a.n;
+        m = m < 0 ? m + a.n : m;
+        e[t] = roots[m];
+        wf.x = fmaf(w[t], e[t].x, wf.x);
+        wf.y = fmaf(w[t], e[t].y, wf.y);
+      }
+      const c32 gx = a.gX[(int64_t)f * npair + pair];        // consecutive pairs: coalesced
+      const c32 gw = make_float2(sc * gx.x - cw * wf.x, sc * gx.y - cw * wf.y);
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) g[t] = fmaf(gw.x, e[t].x, fmaf(gw.y, e[t].y, g[t]));   // Re(gw conj(e))
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) red[fg][t][pl] = g[t];
+  __syncthreads();
+  // fixed-order sum over the frequency groups; thread (pl, t) writes tap t of its pair
+  for (int idx = tid; idx < TAPS_TP * TAPS; idx += TAPS_TP * TAPS_FG) {
+    const int p = idx / TAPS, t = idx % TAPS;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < TAPS_FG; ++q) s += red[q][t][p];
+    const int pr = blockIdx.x * TAPS_TP + p;
+    if (pr < npair) a.gw[(int64_t)pr * TAPS + t] = s;
+  }
+}
+
+// ---- host side ----------------------------------------------------------------------------------
+struct Plan {
+  SpecArgs a;
+  size_t ws_part, ws_dpart, ws_gx, ws_wx, ws_total;
+};
+
+int make_plan(const fiode_spectral_config* cfg, Plan& p) {
+  if (!cfg) return FIODE_EINVAL;
+  SpecArgs& a = p.a;
+  a = SpecArgs{};
+  a.cout = cfg->cout;
+  a.cin = cfg->cin;
+  a.n = cfg->n;
+  if (a.cout < 1 || a.cin < 1 || a.n < 2 || a.n % 2 || a.n > 64) return FIODE_EINVAL;
+  if (cfg->ks != KS || KS >= a.n) return FIODE_ESHAPE;
+  a.half = a.n / 2 + 1;
+  a.nf = a.n * a.half;
+  a.wide = a.cin > a.cout;
+  a.R = a.wide ? a.cin : a.cout;
+  a.K = a.wide ? a.cout : a.cin;
+  if (a.K > 64) return FIODE_ESHAPE;
+  const size_t lds_f = (size_t)a.R * a.K * sizeof(c32), lds_b = (size_t)(a.R + a.K) * a.K * sizeof(c32);
+  if (lds_f + 8192 > 163840 || lds_b > 163840) return FIODE_ESHAPE;
+  a.nparts = ((a.R * a.K + NORM_THREADS - 1) / NORM_THREADS) * ((a.nf + DFT_FG - 1) / DFT_FG);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  p.ws_part = 0;
+  p.ws_dpart = al((size_t)a.nparts * 4);
+  p.ws_gx = p.ws_dpart + al((size_t)a.nf * 4);
+  p.ws_wx = p.ws_gx + al((size_t)a.nf * a.cout * a.cin * sizeof(c32));
+  p.ws_total = p.ws_wx + al((size_t)a.nf * a.cout * a.cin * sizeof(c32));
+  return FIODE_OK;
+}
+
+void bind_ws(Plan& p, void* ws) {
+  char* b = (char*)ws;
+  p.a.part = (float*)(b + p.ws_part);
+  p.a.dpart = (float*)(b + p.ws_dpart);
+  p.a.gX = (c32*)(b + p.ws_gx);
+  p.a.Wx = (c32*)(b + p.ws_wx);
+}
+
+}  // namespace
+
+extern "C" size_t fiode_spectral_workspace_bytes(const fiode_spectral_config* cfg) {
+  Plan p;
+  return make_plan(cfg, p) == FIODE_OK ? p.ws_total : 0;
+}
+
+extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_config* cfg, const float* weight,
+                                             const float* alpha, void* Q, void* inv, void* workspace,
+                                             size_t workspace_bytes) {
+  Plan p;
+  int rc = make_plan(cfg, p);
+  if (rc) return rc;
+  if (!weight || !alpha || !Q || !inv || !workspace) return FIODE_EINVAL;
+  if (workspace_bytes < p.ws_total) return FIODE_EWORKSPACE;
+  bind_ws(p, workspace);
+  SpecArgs& a = p.a;
+  a.w = weight;
+  a.alpha = alpha;
+  a.Q = (c32*)Q;
+  a.inv = (c32*)inv;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_spec_dft, dim3((a.R * a.K + NORM_THREADS - 1) / NORM_THREADS, (a.nf + DFT_FG - 1) / DFT_FG),
+                     dim3(NORM_THREADS), 0, st, a);
+  const size_t lds = (size_t)a.R * a.K * sizeof(c32);
+  if (a.K <= 16) hipLaunchKernelGGL((k_spec_fwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
+  else if (a.K <= 32) hipLaunchKernelGGL((k_spec_fwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((k_spec_fwd<64, 2, 2, 1024>), dim3(a.nf), dim3(1024), lds, st, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_spectral_cayley_backward(void* stream, const fiode_spectral_config* cfg, const float* weight,
+                                              const float* alpha, const void* gQ, const void* inv,
+                                              float* grad_weight, float* grad_alpha, void* workspace,
+                                              size_t workspace_bytes) {
+  Plan p;
+  int rc = make_plan(cfg, p);
+  if (rc) return rc;
+  if (!weight || !alpha || !gQ || !inv || !grad_weight || !grad_alpha || !workspace) return FIODE_EINVAL;
+  if (workspace_bytes < p.ws_total) return FIODE_EWORKSPACE;
+  bind_ws(p, workspace);
+  SpecArgs& a = p.a;
+  a.w = weight;
+  a.alpha = alpha;
+  a.gQ = (const c32*)gQ;
+  a.inv = (c32*)inv;
+  a.gw = grad_weight;
+  a.galpha = grad_alpha;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)(a.R + a.K) * a.K * sizeof(c32);
+  if (a.K <= 16) hipLaunchKernelGGL((k_spec_bwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
+  else if (a.K <= 32) hipLaunchKernelGGL((k_spec_bwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((k_spec_bwd<64, 2, 2, 1024>), dim3(a.nf), dim3(1024), lds, st, a);
+  hipLaunchKernelGGL(k_spec_taps, dim3((a.cout * a.cin + TAPS_TP - 1) / TAPS_TP), dim3(TAPS_TP * TAPS_FG), 0, st, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}

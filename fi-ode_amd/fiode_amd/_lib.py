@@ -74,6 +74,10 @@ class OdeTrainConfig(ct.Structure):
                 ("t0", ct.c_double), ("t1", ct.c_double), ("step_size", ct.c_double)]
 
 
+class SpectralConfig(ct.Structure):
+    _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
+
+
 class CertifyConfig(ct.Structure):
     _fields_ = [("n_classes", ct.c_int32), ("T", ct.c_int32), ("batches", ct.c_int32), ("label", ct.c_int32),
                 ("eps", ct.c_float), ("min_std", ct.c_float)]
@@ -118,6 +122,11 @@ def _load():
         "fiode_groupsort_backward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp, _vp]),
         "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,
                                              ct.c_int64]),
+        "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),
+        "fiode_spectral_cayley_forward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp,
+                                                     ct.c_size_t]),
+        "fiode_spectral_cayley_backward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp, _vp,
+                                                      _vp, ct.c_size_t]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

@@ -253,6 +253,27 @@ class GroupSort(nn.Module):
         return torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=cd)
 
 
+class _SpectralCayleyFn(torch.autograd.Function):
+    """Q[f] = cayley(alpha Wf[f] / ||Wf||) for all rFFT frequencies of a 3x3 CayleyConv in two
+    fused launches each way (fiode_spectral_cayley_*; spectral.hip) instead of the ~75 kernels of
+    rfft2 + shift + conj + cayley_scaled and their autograd."""
+
+    @staticmethod
+    def forward(ctx, weight, alpha, n: int):
+        from . import ops
+        Q, inv, ws = ops.spectral_cayley_forward(weight.detach(), alpha.detach(), n)
+        ctx.save_for_backward(weight, alpha, inv, ws)
+        ctx.n = n
+        return Q
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from . import ops
+        weight, alpha, inv, ws = ctx.saved_tensors
+        gw, ga = ops.spectral_cayley_backward(gQ.contiguous(), weight.detach(), alpha.detach(), ctx.n, inv, ws)
+        return gw, ga.reshape(alpha.shape), None
+
+
 class CayleyConv(nn.Conv2d):
     """Orthogonal circular convolution parametrised per frequency: for each of the n*(n/2+1)
     rFFT frequencies the cout x cin channel matrix is Cayley-mapped, y = irfft2(Q(w) xfft).
@@ -265,6 +286,8 @@ class CayleyConv(nn.Conv2d):
                          padding=kernel_size // 2, bias=bias)
         self.alpha = nn.Parameter(torch.ones(1))
         self._alpha_init = False
+        self.fused = True               # fused spectral Cayley kernels on ROCm (spectral.hip)
+        self._fused_shapes = {}
         self._shift = {}
         self._n = None
         self._pre = None
@@ -284,7 +307,22 @@ class CayleyConv(nn.Conv2d):
         return self._shift[key]
 
     def spectral_weight(self, n: int, device) -> torch.Tensor:
-        """The per-frequency orthogonal channel matrices Q [n (n/2+1), cout, cin] for n x n inputs."""
+        """The per-frequency orthogonal channel matrices Q [n (n/2+1), cout, cin] for n x n inputs.
+        ROCm tensors of a supported shape (3x3 taps, min(cout, cin) <= 64) take the fused HIP map
+        (_SpectralCayleyFn); otherwise the op-by-op formula below (also the tests' reference)."""
+        if self.fused and self._alpha_init and self.weight.is_cuda and self._fused_ok(n):
+            return _SpectralCayleyFn.apply(self.weight, self.alpha, n)
+        return self.spectral_weight_reference(n, device)
+
+    def _fused_ok(self, n: int) -> bool:
+        ok = self._fused_shapes.get(n)
+        if ok is None:
+            from . import ops
+            ok = self._fused_shapes[n] = ops.spectral_supported(tuple(self.weight.shape), n)
+        return ok
+
+    def spectral_weight_reference(self, n: int, device) -> torch.Tensor:
+        """rfft2 of the taps, the shift of the 'same' padding, conj, cayley_scaled (PyTorch ops)."""
         cout, cin = self.weight.shape[:2]
         nf = n * (n // 2 + 1)
         wf = torch.fft.rfft2(self.weight, (n, n)).reshape(cout, cin, nf).permute(2, 0, 1).conj()

@@ -375,6 +375,61 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     return out
 
 
+def spectral_config(weight_shape, n: int) -> L.SpectralConfig:
+    cout, cin, kh, kw = weight_shape
+    if kh != kw:
+        raise ValueError(f"spectral Cayley: square kernels only, got {kh}x{kw}")
+    return L.SpectralConfig(int(cout), int(cin), int(kh), int(n))
+
+
+def spectral_supported(weight_shape, n: int) -> bool:
+    """Whether fiode_spectral_cayley_* takes this layer (3x3 taps, min(cout, cin) <= 64, the LDS
+    image of one frequency within 160 KiB)."""
+    cfg = spectral_config(weight_shape, n)
+    return L.lib().fiode_spectral_workspace_bytes(ct.byref(cfg)) > 0
+
+
+def spectral_cayley_forward(weight: torch.Tensor, alpha: torch.Tensor, n: int):
+    """fiode_spectral_cayley_forward: Q complex64 [n (n/2+1), cout, cin] = cayley(alpha Wf / ||Wf||)
+    per rFFT frequency.  Returns (Q, inv, workspace); inv and workspace feed the backward."""
+    dev = weight.device
+    cout, cin = int(weight.shape[0]), int(weight.shape[1])
+    weight = _need(weight, "weight", tuple(weight.shape), torch.float32, dev)
+    alpha = _need(alpha.reshape(1), "alpha", (1,), torch.float32, dev)
+    cfg = spectral_config(weight.shape, n)
+    lib = L.lib()
+    nb = lib.fiode_spectral_workspace_bytes(ct.byref(cfg))
+    if nb == 0:
+        raise ValueError(f"spectral Cayley: unsupported layer {tuple(weight.shape)} at n={n}")
+    nf, K = n * (n // 2 + 1), min(cout, cin)
+    Q = torch.empty((nf, cout, cin), dtype=torch.complex64, device=dev)
+    inv = torch.empty((nf, K, K), dtype=torch.complex64, device=dev)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    L.check(lib.fiode_spectral_cayley_forward(_stream(dev), ct.byref(cfg), weight.data_ptr(), alpha.data_ptr(),
+                                              Q.data_ptr(), inv.data_ptr(), ws.data_ptr(), ws.numel()),
+            "fiode_spectral_cayley_forward")
+    return Q, inv, ws
+
+
+def spectral_cayley_backward(gQ: torch.Tensor, weight: torch.Tensor, alpha: torch.Tensor, n: int,
+                             inv: torch.Tensor, ws: torch.Tensor):
+    """fiode_spectral_cayley_backward: (dL/dweight, dL/dalpha) from dL/dQ (torch's complex convention)."""
+    dev = weight.device
+    cout, cin = int(weight.shape[0]), int(weight.shape[1])
+    nf = n * (n // 2 + 1)
+    gQ = _need(gQ, "gQ", (nf, cout, cin), torch.complex64, dev)
+    weight = _need(weight, "weight", tuple(weight.shape), torch.float32, dev)
+    alpha = _need(alpha.reshape(1), "alpha", (1,), torch.float32, dev)
+    cfg = spectral_config(weight.shape, n)
+    gw = torch.empty_like(weight)
+    ga = torch.empty(1, dtype=torch.float32, device=dev)
+    L.check(L.lib().fiode_spectral_cayley_backward(_stream(dev), ct.byref(cfg), weight.data_ptr(), alpha.data_ptr(),
+                                                   gQ.data_ptr(), inv.data_ptr(), gw.data_ptr(), ga.data_ptr(),
+                                                   ws.data_ptr(), ws.numel()),
+            "fiode_spectral_cayley_backward")
+    return gw, ga
+
+
 def _gs_shape(x: torch.Tensor, cdim: int = 1):
     if x.device.type != "cuda" or x.dtype != torch.float32:
         raise ValueError(f"groupsort: float32 ROCm tensor expected, got {x.dtype} on {x.device}")

@@ -246,6 +246,29 @@ FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64
                                        float* gx);
 
 /* Error text for a return code. */
+/* ---- spectral Cayley map of an orthogonal convolution (CayleyConv; libs/ortho_conv, absent:
+ * restated in fiode_amd/cayley.py).  Replaces CayleyConv.spectral_weight + cayley_scaled
+ * (rfft2 of the taps, shift, conj, ||.||, the per-frequency Cayley map) and its autograd. */
+typedef struct fiode_spectral_config {
+  int32_t cout, cin;     /* weight [cout][cin][ks][ks] (cin after a stride-2 space-to-channel)   */
+  int32_t ks;            /* kernel size: 3 (KWLarge); other sizes return FIODE_ESHAPE           */
+  int32_t n;             /* even input size n <= 64: nf = n (n/2 + 1) rFFT frequencies          */
+} fiode_spectral_config;
+
+/* Workspace (norm partials, backward scratch): keep the forward's until the backward. */
+FIODE_API size_t fiode_spectral_workspace_bytes(const fiode_spectral_config* cfg);
+/* Q: complex64 [nf][cout][cin] = cayley(alpha Wf / ||Wf||) per frequency; inv: complex64 [nf][K][K]
+ * (K = min(cout, cin)) saved for the backward.  min(cout, cin) <= 64. */
+FIODE_API int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_config* cfg, const float* weight,
+                                            const float* alpha, void* Q, void* inv, void* workspace,
+                                            size_t workspace_bytes);
+/* gQ: dL/dQ (torch's complex-gradient convention); grad_weight [cout][cin][ks][ks], grad_alpha [1]
+ * are overwritten. */
+FIODE_API int fiode_spectral_cayley_backward(void* stream, const fiode_spectral_config* cfg, const float* weight,
+                                             const float* alpha, const void* gQ, const void* inv,
+                                             float* grad_weight, float* grad_alpha, void* workspace,
+                                             size_t workspace_bytes);
+
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);
 

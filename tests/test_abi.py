@@ -62,3 +62,22 @@ def test_batched_inverse_argument_checks():
     assert lib.fiode_batched_inverse(None, 7, 1, 4, None, 16, None, 16) == 1
     buf = ct.create_string_buffer(64)
     assert lib.fiode_batched_inverse(None, 0, 1, 4, buf, 15, buf, 16) == 2
+
+
+def test_spectral_cayley_host_checks():
+    """fiode_spectral_*: workspace sizing and argument checks run on the host (no launch)."""
+    import ctypes as ct
+    from fiode_amd import _lib
+    lib = _lib.lib()
+    ok = _lib.SpectralConfig(64, 256, 3, 8)          # KWLarge conv 4 (wide, K = 64)
+    nf = 8 * 5
+    nb = lib.fiode_spectral_workspace_bytes(ct.byref(ok))
+    assert nb >= nf * 64 * 256 * 8 + nf * 4           # gX scratch + D partials
+    assert lib.fiode_spectral_workspace_bytes(ct.byref(_lib.SpectralConfig(8, 8, 5, 16))) == 0   # 5x5 taps
+    assert lib.fiode_spectral_workspace_bytes(ct.byref(_lib.SpectralConfig(128, 128, 3, 16))) == 0  # K > 64
+    assert lib.fiode_spectral_workspace_bytes(ct.byref(_lib.SpectralConfig(8, 8, 3, 7))) == 0     # odd n
+    assert lib.fiode_spectral_cayley_forward(None, ct.byref(ok), None, None, None, None, None, 0) == 1
+    dummy = ct.c_void_p(1)
+    assert lib.fiode_spectral_cayley_forward(None, ct.byref(ok), dummy, dummy, dummy, dummy, dummy, nb - 1) == 3
+    assert lib.fiode_spectral_cayley_backward(None, ct.byref(_lib.SpectralConfig(8, 8, 5, 16)), dummy, dummy, dummy,
+                                              dummy, dummy, dummy, dummy, nb) == 2

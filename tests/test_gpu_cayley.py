@@ -195,3 +195,98 @@ def test_spatial_major_backbone_matches_nchw():
     assert float((y1 - y0).abs().max()) < 1e-4 * (float(y0.abs().max()) + 1)
     for a, b in zip(bb.parameters(), g0):
         assert float((a.grad - b).abs().max()) <= 1e-3 * (float(b.abs().max()) + 1e-6)
+
+
+# ---- fused spectral Cayley map of CayleyConv (spectral.hip) ---------------------------------------
+# (cout, cin, n): the four KWLarge convs (cin after the stride-2 space-to-channel) + square / tall /
+# small-K cases.  Reference: CayleyConv.spectral_weight_reference (rfft2 + shift + conj +
+# cayley_scaled, PyTorch ops) in float64 -- the formula the fused kernels restate.
+SPECTRAL_CASES = [(32, 3, 32), (32, 128, 16), (64, 32, 16), (64, 256, 8), (16, 16, 8), (40, 8, 6)]
+
+
+def _spectral_pair(cout, cin, n, dev, seed):
+    from fiode_amd.cayley import CayleyConv
+    torch.manual_seed(seed)
+    conv = CayleyConv(cin, cout, 3).to(dev)
+    with torch.no_grad():
+        conv.alpha.fill_(float(conv.spectral_weight_reference(n, dev).detach().abs().pow(2).sum().sqrt()) * 1.7)
+    conv._alpha_init = True
+    ref = CayleyConv(cin, cout, 3).to(dev).double()
+    ref.load_state_dict(conv.state_dict())
+    ref._shift = {}
+    return conv, ref
+
+
+def _ref_shift(conv, n, dev):
+    import math
+    s = -((conv.weight.shape[2] - 1) // 2)
+    k = torch.arange(n, device=dev, dtype=torch.float64)
+    sh = torch.exp(2j * math.pi * s * (k[None, :] + k[:, None]) / n)[:, : n // 2 + 1]
+    return sh.reshape(n * (n // 2 + 1), 1, 1)
+
+
+def _spectral_ref64(ref, n, dev):
+    """float64 spectral Q of the reference formula (shift kept in complex128)."""
+    from fiode_amd.cayley import cayley_scaled
+    cout, cin = ref.weight.shape[:2]
+    nf = n * (n // 2 + 1)
+    wf = torch.fft.rfft2(ref.weight, (n, n)).reshape(cout, cin, nf).permute(2, 0, 1).conj()
+    wf = _ref_shift(ref, n, dev) * wf
+    # cayley_scaled in float64 via the op-by-op formula (torch.linalg.inv)
+    X = wf * (ref.alpha / torch.linalg.vector_norm(wf))
+    wide = X.shape[-1] > X.shape[-2]
+    if wide:
+        X = X.mT
+    k = X.shape[-1]
+    U, V = X[..., :k, :], X[..., k:, :]
+    M = torch.eye(k, dtype=X.dtype, device=dev) + U - U.mH + V.mH @ V
+    inv = torch.linalg.inv(M)
+    Q = torch.cat([2 * inv - torch.eye(k, dtype=X.dtype, device=dev), -2 * V @ inv], dim=-2)
+    return Q.mT if wide else Q
+
+
+@pytest.mark.parametrize("case", SPECTRAL_CASES)
+def test_spectral_cayley_forward_matches_reference(case):
+    cout, cin, n = case
+    dev = _dev()
+    conv, ref = _spectral_pair(cout, cin, n, dev, seed=cout + cin + n)
+    Q = conv.spectral_weight(n, dev)
+    assert Q.dtype == torch.complex64 and tuple(Q.shape) == (n * (n // 2 + 1), cout, cin)
+    Q64 = _spectral_ref64(ref, n, dev)
+    err = float((Q.to(torch.complex128) - Q64).abs().max())
+    assert err <= 2e-5 * min(cout, cin) ** 0.5, err
+    # the fused path and the op-by-op float32 path agree too
+    Q32 = conv.spectral_weight_reference(n, dev)
+    assert float((Q - Q32).abs().max()) <= 4e-5 * min(cout, cin) ** 0.5
+
+
+@pytest.mark.parametrize("case", SPECTRAL_CASES)
+def test_spectral_cayley_backward_matches_autograd(case):
+    cout, cin, n = case
+    dev = _dev()
+    conv, ref = _spectral_pair(cout, cin, n, dev, seed=7 * cout + cin + n)
+    nf = n * (n // 2 + 1)
+    g = torch.Generator(device="cpu").manual_seed(n)
+    G = torch.randn(nf, cout, cin, 2, generator=g, dtype=torch.float64)
+    G = torch.view_as_complex(G).to(dev)
+    Q = conv.spectral_weight(n, dev)
+    (Q.to(torch.complex128) * G.conj()).real.sum().backward()
+    Q64 = _spectral_ref64(ref, n, dev)
+    (Q64 * G.conj()).real.sum().backward()
+    for name in ("weight", "alpha"):
+        a, b = getattr(conv, name).grad.double(), getattr(ref, name).grad
+        tol = 2e-4 * float(b.abs().max())
+        assert float((a - b).abs().max()) <= tol, (name, float((a - b).abs().max()), tol)
+
+
+def test_spectral_cayley_orthogonal_and_rejects():
+    from fiode_amd import ops
+    dev = _dev()
+    conv, _ = _spectral_pair(64, 256, 8, dev, seed=1)
+    Q = conv.spectral_weight(8, dev)                       # [40, 64, 256]: orthonormal rows
+    eye = torch.eye(64, dtype=torch.complex64, device=dev)
+    assert float((Q @ Q.mH - eye).abs().max()) < 1e-4
+    assert not ops.spectral_supported((8, 8, 5, 5), 16)     # 5x5 taps: not fused
+    assert not ops.spectral_supported((128, 128, 3, 3), 16)  # K > 64
+    with pytest.raises(ValueError):
+        ops.spectral_cayley_forward(torch.zeros(8, 8, 5, 5, device=dev), torch.ones(1, device=dev), 16)

@@ -6,6 +6,7 @@ python tools/step_probe.py  ->  one JSON line of per-part ms
 import json
 import pathlib
 import sys
+import time
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
@@ -17,30 +18,47 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 
 
-def graph_ms(fn, reps=20, warm=3):
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        for _ in range(warm):
-            fn()
-    torch.cuda.current_stream(dev).wait_stream(s)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        fn()
-    for _ in range(3):
-        g.replay()
-    torch.cuda.synchronize()
+def _cal():
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(1000)
     a.record()
-    for _ in range(reps):
-        g.replay()
+    torch.cuda._sleep(1_000_000)
     b.record()
     torch.cuda.synchronize()
-    return round(a.elapsed_time(b) / reps, 4)
+    return a.elapsed_time(b) / 1_000_000          # ms per _sleep cycle
+
+
+MS_PER_CYCLE = None
+
+
+def graph_ms(fn, reps=5, warm=3):
+    """GPU time of fn() dispatched eagerly behind a long _sleep (so the host runs ahead and the
+    events see back-to-back GPU work, no dispatch gaps); the median of reps."""
+    global MS_PER_CYCLE
+    if MS_PER_CYCLE is None:
+        MS_PER_CYCLE = _cal()
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(60.0 / MS_PER_CYCLE))   # 60 ms head start for the host
+        a.record()
+        t0 = time.perf_counter()
+        fn()
+        host = (time.perf_counter() - t0) * 1e3
+        b.record()
+        torch.cuda.synchronize()
+        assert host < 55.0, f"host enqueue {host:.1f} ms exceeds the head start"
+        out.append(a.elapsed_time(b))
+    ms = round(sorted(out)[len(out) // 2], 4)
+    print(getattr(fn, "__name__", "?"), ms, f"host {host:.2f} ms", file=sys.stderr, flush=True)
+    return ms
 
 
 res = {}
+print('start', file=sys.stderr, flush=True)
 mod = bench.build_module(dev, train_ode=True)
 x = torch.rand(128, 3, 32, 32, device=dev)
 y = torch.randint(0, 10, (128,), device=dev)
