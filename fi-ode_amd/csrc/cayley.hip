@@ -67,6 +67,116 @@ int launch_inv<ComplexOps>(hipStream_t s, int batch, int n, const void* in, int6
   return 0;
 }
 
+// ---- large real inverses: block Gauss-Jordan over 64-wide panels --------------------------------
+// For n > 64 (the 512 x 512 backbone CayleyLinears, the 128 x 128 dynamics map) the matrix lives in
+// HBM (padded with I to a multiple of 64) and each of the n/64 panel steps is two launches:
+//   k_panel_pivot   one workgroup: P = X_KK^-1 by the register Gauss-Jordan above (16 us at 64);
+//   k_panel_update  one workgroup per 64 x 64 output tile, ping-pong buffers (no read/write race):
+//                   R_Kj = P X_Kj,  X_ij -= X_iK R_Kj,  X_iK <- -X_iK P,  X_Kj <- R_Kj,  X_KK <- P.
+// Smaller pivot blocks are cheaper per eliminated column (a Gauss-Jordan round costs ~0.25 us at
+// 64, ~0.9 us at 128), and the update is a few us of LDS-tiled FMA on 64 workgroups.
+constexpr int PB = 64;
+
+__global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* __restrict__ in, float* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)np * np) return;
+  const int i = (int)(idx / np), j = (int)(idx % np);
+  out[idx] = (i < n && j < n) ? in[(int64_t)i * n + j] : (i == j ? 1.0f : 0.0f);
+}
+
+__global__ void __launch_bounds__(256) k_panel_pivot(int np, int k0, const float* __restrict__ X, float* __restrict__ P) {
+  typedef fiode_gj::GJ<RealOps, PB, 4, 4> G;
+  __shared__ typename G::Smem sm;
+  float a[4][4];
+  G::load(a, X + (int64_t)k0 * np + k0, PB, np);
+  G::invert(a, PB, sm);
+  G::store(a, P, PB, PB);
+}
+
+// out tile (ib, jb) of the next buffer; 256 threads, 4 x 4 outputs each
+__global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
+                                                      const float* __restrict__ P, float* __restrict__ Y,
+                                                      float* __restrict__ final_out, int n) {
+  __shared__ float sP[PB][PB + 4];
+  __shared__ float sA[PB][PB + 4];      // X_iK (rows of the tile, pivot columns)
+  __shared__ float sB[PB][PB + 4];      // X_Kj, then R_Kj
+  const int ib = blockIdx.x * PB, jb = blockIdx.y * PB, tid = threadIdx.x;
+  const bool piv_r = ib == k0, piv_c = jb == k0;
+  for (int idx = tid; idx < PB * PB; idx += 256) {
+    const int r = idx / PB, c = idx % PB;
+    sP[r][c] = P[idx];
+    sA[r][c] = X[(int64_t)(ib + r) * np + k0 + c];
+    sB[r][c] = X[(int64_t)(k0 + r) * np + jb + c];
+  }
+  __syncthreads();
+  const int tr = (tid / 16) * 4, tc = (tid % 16) * 4;
+  float acc[4][4];
+  auto gemm = [&](float (*A)[PB + 4], float (*B)[PB + 4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < PB; ++k) {
+      float x[4], y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = A[tr + r][k];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) y[c] = B[k][tc + c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(x[r], y[c], acc[r][c]);
+    }
+  };
+  float o[4][4];
+  if (piv_c) {
+    if (piv_r) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[r][c] = sP[tr + r][tc + c];
+    } else {
+      gemm(sA, sP);                       // -X_iK P
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[r][c] = -acc[r][c];
+    }
+  } else {
+    gemm(sP, sB);                         // R_Kj = P X_Kj
+    if (piv_r) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[r][c] = acc[r][c];
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sB[tr + r][tc + c] = acc[r][c];
+      __syncthreads();
+      gemm(sA, sB);                       // X_ij - X_iK R_Kj
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[r][c] = X[(int64_t)(ib + tr + r) * np + jb + tc + c] - acc[r][c];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int i = ib + tr + r, j = jb + tc + c;
+      if (final_out) {
+        if (i < n && j < n) final_out[(int64_t)i * n + j] = o[r][c];
+      } else {
+        Y[(int64_t)i * np + j] = o[r][c];
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch, int32_t n, const void* in,
@@ -79,6 +189,35 @@ extern "C" int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch,
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FIODE_DTYPE_F32) launch_inv<RealOps>(s, batch, n, in, in_stride, out, out_stride);
   else launch_inv<ComplexOps>(s, batch, n, in, in_stride, out, out_stride);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" size_t fiode_block_inverse_workspace_bytes(int32_t n) {
+  if (n < 1) return 0;
+  const size_t np = (size_t)((n + PB - 1) / PB) * PB;
+  return (2 * np * np + (size_t)PB * PB) * sizeof(float);
+}
+
+extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
+                                   size_t workspace_bytes) {
+  if (n < 1 || n > FIODE_BLOCK_INV_MAX_N || !in || !out || !workspace) return FIODE_EINVAL;
+  if (workspace_bytes < fiode_block_inverse_workspace_bytes(n)) return FIODE_EWORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int np = (n + PB - 1) / PB * PB, nb = np / PB;
+  float* A = (float*)workspace;
+  float* B = A + (size_t)np * np;
+  float* P = B + (size_t)np * np;
+  hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256)), dim3(256), 0, st, n, np, in, A);
+  for (int kb = 0; kb < nb; ++kb) {
+    const int k0 = kb * PB;
+    hipLaunchKernelGGL(k_panel_pivot, dim3(1), dim3(256), 0, st, np, k0, A, P);
+    const bool last = kb == nb - 1;
+    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb), dim3(256), 0, st, np, k0, A, P, B, last ? out : nullptr, n);
+    float* t = A;
+    A = B;
+    B = t;
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

@@ -122,6 +122,8 @@ def _load():
         "fiode_groupsort_backward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp, _vp]),
         "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,
                                              ct.c_int64]),
+        "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
+        "fiode_block_inverse": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),
         "fiode_spectral_cayley_forward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp,
                                                      ct.c_size_t]),

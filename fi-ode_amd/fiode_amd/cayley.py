@@ -24,12 +24,18 @@ _BLOCK = 128
 
 
 def _block_inverse(M: torch.Tensor) -> torch.Tensor:
-    """Inverse of (..., n, n) on the device: the HIP Gauss-Jordan kernel for n <= 128, else
-    block Gauss-Jordan in natural order over 128-wide panels (pivot blocks inverted by the
+    """Inverse of (..., n, n) on the device: real n > 64 by the 64-panel block Gauss-Jordan kernels
+    (fiode_block_inverse), n <= 128 otherwise by the register Gauss-Jordan kernel, complex n > 128
+    by block Gauss-Jordan in natural order over 128-wide panels here (pivot blocks inverted by the
     kernel, the rank-128 updates as batched GEMMs).  Valid for positive-real matrices (every
     Schur complement of one is positive-real), which all Cayley systems I + A are."""
     from . import ops
     n = M.shape[-1]
+    if n > 64 and M.dtype == torch.float32 and M.is_cuda:
+        if M.dim() == 2:
+            return ops.block_inverse(M)
+        flat = M.reshape(-1, n, n)
+        return torch.stack([ops.block_inverse(m) for m in flat]).reshape(M.shape)
     if n <= _BLOCK:
         return ops.batched_inverse(M)
     X = M.clone()

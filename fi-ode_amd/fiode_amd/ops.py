@@ -375,6 +375,24 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     return out
 
 
+def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(n, n) float32 -> inverse by 64-wide panel block Gauss-Jordan on the device
+    (fiode_block_inverse).  Valid for matrices with positive-definite symmetric part."""
+    if M.device.type != "cuda" or M.dtype != torch.float32 or M.dim() != 2 or M.shape[0] != M.shape[1]:
+        raise ValueError(f"block_inverse: square float32 ROCm matrix expected, got {tuple(M.shape)} {M.dtype} "
+                         f"on {M.device}")
+    n = int(M.shape[0])
+    M = M.contiguous()
+    if out is None:
+        out = torch.empty_like(M)
+    lib = L.lib()
+    nb = lib.fiode_block_inverse_workspace_bytes(n)
+    ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}")
+    L.check(lib.fiode_block_inverse(_stream(M.device), n, M.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel()),
+            "fiode_block_inverse")
+    return out
+
+
 def spectral_config(weight_shape, n: int) -> L.SpectralConfig:
     cout, cin, kh, kw = weight_shape
     if kh != kw:

@@ -246,6 +246,14 @@ FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64
                                        float* gx);
 
 /* Error text for a return code. */
+/* Inverse of one real n x n matrix with positive-definite symmetric part (the Cayley systems of the
+ * 512 x 512 backbone CayleyLinears and the 128 x 128 dynamics map): block Gauss-Jordan over
+ * 64-wide panels (2 launches per panel), no pivot search, no host sync.  in may equal out. */
+#define FIODE_BLOCK_INV_MAX_N 4096
+FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
+FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
+                                  size_t workspace_bytes);
+
 /* ---- spectral Cayley map of an orthogonal convolution (CayleyConv; libs/ortho_conv, absent:
  * restated in fiode_amd/cayley.py).  Replaces CayleyConv.spectral_weight + cayley_scaled
  * (rfft2 of the taps, shift, conj, ||.||, the per-frequency Cayley map) and its autograd. */

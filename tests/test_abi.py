@@ -81,3 +81,13 @@ def test_spectral_cayley_host_checks():
     assert lib.fiode_spectral_cayley_forward(None, ct.byref(ok), dummy, dummy, dummy, dummy, dummy, nb - 1) == 3
     assert lib.fiode_spectral_cayley_backward(None, ct.byref(_lib.SpectralConfig(8, 8, 5, 16)), dummy, dummy, dummy,
                                               dummy, dummy, dummy, dummy, nb) == 2
+
+
+def test_block_inverse_host_checks():
+    from fiode_amd import _lib
+    lib = _lib.lib()
+    assert lib.fiode_block_inverse_workspace_bytes(512) == (2 * 512 * 512 + 64 * 64) * 4
+    assert lib.fiode_block_inverse_workspace_bytes(65) == (2 * 128 * 128 + 64 * 64) * 4
+    assert lib.fiode_block_inverse(None, 0, None, None, None, 0) == 1
+    dummy = ct.c_void_p(1)
+    assert lib.fiode_block_inverse(None, 512, dummy, dummy, dummy, 100) == 3

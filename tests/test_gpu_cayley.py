@@ -47,6 +47,20 @@ def test_block_inverse_large(n):
     assert err <= 2e-5 * n ** 0.5, err
 
 
+@pytest.mark.parametrize("n", [65, 128, 130, 512])
+def test_panel_block_inverse_kernel(n):
+    """fiode_block_inverse (64-wide panels, padded with I) vs float64 torch.linalg.inv; in == out."""
+    from fiode_amd import ops
+    dev = _dev()
+    M64 = _system(1, n, torch.float32, dev, scale=3.0, seed=n)[0]
+    ref = torch.linalg.inv(M64)
+    inv = ops.block_inverse(M64.float())
+    assert float((inv.double() - ref).abs().max()) <= 2e-5 * n ** 0.5
+    buf = M64.float().clone()
+    ops.block_inverse(buf, out=buf)
+    assert torch.equal(buf, inv)
+
+
 def test_inverse_in_place_and_strided_batch():
     from fiode_amd import ops
     dev = _dev()
