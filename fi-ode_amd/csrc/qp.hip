@@ -210,7 +210,7 @@ extern "C" const char* fiode_error_string(int code) {
   switch (code) {
     case FIODE_OK: return "ok";
     case FIODE_EINVAL: return "invalid argument";
-    case FIODE_ESHAPE: return "unsupported shape (this build: n_hidden=10, mlp_size=128, x_dim=10)";
+    case FIODE_ESHAPE: return "unsupported shape (dynamics: n_hidden=10, mlp_size=128, x_dim=10; spectral: 3x3 taps, min(cout, cin) <= 64, n <= 64; transforms: n in {8, 16, 32})";
     case FIODE_EWORKSPACE: return "workspace too small";
     default: return code >= FIODE_EHIP ? hipGetErrorString((hipError_t)(code - FIODE_EHIP)) : "unknown error";
   }

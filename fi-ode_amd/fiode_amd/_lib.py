@@ -78,6 +78,10 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
+class SconvConfig(ct.Structure):
+    _fields_ = [("n", ct.c_int32), ("C", ct.c_int32), ("B", ct.c_int32), ("downsample", ct.c_int32)]
+
+
 class CertifyConfig(ct.Structure):
     _fields_ = [("n_classes", ct.c_int32), ("T", ct.c_int32), ("batches", ct.c_int32), ("label", ct.c_int32),
                 ("eps", ct.c_float), ("min_std", ct.c_float)]
@@ -124,6 +128,8 @@ def _load():
                                              ct.c_int64]),
         "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_block_inverse": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
+        "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
         "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),
         "fiode_spectral_cayley_forward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp,
                                                      ct.c_size_t]),

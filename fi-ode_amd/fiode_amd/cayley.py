@@ -280,6 +280,54 @@ class _SpectralCayleyFn(torch.autograd.Function):
         return gw, ga.reshape(alpha.shape), None
 
 
+class _SpectralConvFn(torch.autograd.Function):
+    """y = [GroupSort](irfft2(Q[f] @ rfft2(x)[f]) + bias) on spatial-major activations, the
+    transforms as HIP kernels that read / write the GEMM layout [f][C][B] (sconv.hip), the
+    per-frequency channel products as batched complex GEMMs.  Backward (torch's conventions for
+    the real transforms, w_kb = 1 at kb = 0, n/2 and 2 between):
+        G = rfft2(d/dpre),  dQ = (w_kb / n^2) G X^H,  dx = irfft2(Q^H G),  dbias = sum_b Re G[0]."""
+
+    @staticmethod
+    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool):
+        from . import ops
+        B = x.shape[-1]
+        nf, cout, cin = Q.shape
+        X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
+        Y = torch.matmul(Q.detach(), X)
+        y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort)
+        ctx.save_for_backward(X, Q, code)
+        ctx.cfg = (n, downsample, groupsort, bias is not None, cin, cout, B)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import ops
+        X, Q, code = ctx.saved_tensors
+        n, downsample, groupsort, has_bias, cin, cout, B = ctx.cfg
+        gy = gy.contiguous()
+        if groupsort:
+            G = ops.sconv_rfft2(None, n, cout, B, gy=gy, code=code)
+        else:
+            G = ops.sconv_rfft2(gy, n, cout, B)
+        gx = gQ = gb = None
+        if ctx.needs_input_grad[0]:
+            gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
+        if ctx.needs_input_grad[1]:
+            key = (n, str(G.device))
+            wq = _SPECTRAL_GRAD_WEIGHTS.get(key)
+            if wq is None:
+                kb = torch.arange(n // 2 + 1, device=G.device)
+                w = torch.where((kb == 0) | (kb == n // 2), 1.0, 2.0) / float(n * n)
+                wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
+            gQ = torch.matmul(G, X.mH) * wq
+        if has_bias and ctx.needs_input_grad[2]:
+            gb = G[0].real.sum(-1)
+        return gx, gQ, gb, None, None, None
+
+
+_SPECTRAL_GRAD_WEIGHTS = {}
+
+
 class CayleyConv(nn.Conv2d):
     """Orthogonal circular convolution parametrised per frequency: for each of the n*(n/2+1)
     rFFT frequencies the cout x cin channel matrix is Cayley-mapped, y = irfft2(Q(w) xfft).
@@ -369,6 +417,13 @@ class CayleyConv(nn.Conv2d):
         if self.bias is not None:
             y = y + self.bias[:, None, None]
         return y
+
+    def forward_hwcb_fused(self, x: torch.Tensor, groupsort: bool) -> torch.Tensor:
+        """forward_hwcb (+ the following GroupSort) with the transforms as HIP kernels
+        (_SpectralConvFn): [n][n][cin][B] (stride 2: [2n][2n][cin/4][B]) -> [n][n][cout][B]."""
+        n = x.shape[0] // 2 if self.downsample else x.shape[0]
+        Q = self._take_spectral(n, x.device)
+        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort)
 
     def forward_hwcb(self, x: torch.Tensor) -> torch.Tensor:
         """The same map on spatial-major activations [n, n, C, B] (the conv stack's HBM layout):

@@ -48,6 +48,7 @@ class KWLargeConcat(nn.Module):
         )
 
         self.spatial_major = True
+        self.fused_transforms = True      # sconv.hip rfft2 / irfft2 (+ GroupSort) around the GEMMs
 
     def forward(self, x):
         """On ROCm the conv stack runs spatial-major ([h, w, C, B]: FFT and GEMM operands without
@@ -61,6 +62,11 @@ class KWLargeConcat(nn.Module):
         while not isinstance(mods[i], nn.Flatten):
             m = mods[i]
             if isinstance(m, CayleyConv):
+                gs = i + 1 < len(mods) and isinstance(mods[i + 1], GroupSort)
+                if self.fused_transforms and h.shape[0] // (2 if m.downsample else 1) <= 32:
+                    h = m.forward_hwcb_fused(h, gs)     # transforms (+ GroupSort) in HIP kernels
+                    i += 2 if gs else 1
+                    continue
                 h = m.forward_hwcb(h)
             elif isinstance(m, GroupSort):
                 h = m(h, channel_dim=2)

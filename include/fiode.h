@@ -254,6 +254,23 @@ FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                   size_t workspace_bytes);
 
+/* ---- spectral convolution transforms on spatial-major activations [n][n][C][B] (CayleyConv
+ * forward_hwcb; fiode_amd/cayley.py).  Spectrum layout [f][C][B] complex64, f = ka (n/2+1) + kb. */
+typedef struct fiode_sconv_config {
+  int32_t n;             /* spatial size after any space-to-channel: 8, 16 or 32                */
+  int32_t C;             /* channels of the transformed tensor (after space-to-channel)         */
+  int32_t B;             /* batch                                                               */
+  int32_t downsample;    /* rfft2: gather x from [2n][2n][C/4][B]; irfft2: scatter y to it       */
+} fiode_sconv_config;
+/* X = rfft2(x) over (h, w).  With gy != NULL the input is the GroupSort backward of gy (d/dout
+ * [n][n][C][B]) with the comparison codes [n][n][C/2][B] of the forward (x unused). */
+FIODE_API int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, const float* x, const float* gy,
+                                const uint8_t* code, void* X);
+/* y = irfft2(Y) (c2c over h, c2r over w, 1/n^2), + bias[C] if given; groupsort != 0: y = GroupSort
+ * of it over the channel halves and code_out [n][n][C/2][B] records max/min/tie. */
+FIODE_API int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,
+                                 int32_t groupsort, float* y, uint8_t* code_out);
+
 /* ---- spectral Cayley map of an orthogonal convolution (CayleyConv; libs/ortho_conv, absent:
  * restated in fiode_amd/cayley.py).  Replaces CayleyConv.spectral_weight + cayley_scaled
  * (rfft2 of the taps, shift, conj, ||.||, the per-frequency Cayley map) and its autograd. */

@@ -304,3 +304,62 @@ def test_spectral_cayley_orthogonal_and_rejects():
     assert not ops.spectral_supported((128, 128, 3, 3), 16)  # K > 64
     with pytest.raises(ValueError):
         ops.spectral_cayley_forward(torch.zeros(8, 8, 5, 5, device=dev), torch.ones(1, device=dev), 16)
+
+
+# ---- spectral conv transforms (sconv.hip) ------------------------------------------------------------
+# (cin, cout, stride, input size): the four KWLarge convs + a non-GroupSort / odd-batch case.
+SCONV_CASES = [(3, 32, 1, 32, True, 128), (32, 32, 2, 32, True, 128), (32, 64, 1, 16, True, 16),
+               (64, 64, 2, 16, True, 24), (8, 6, 1, 8, False, 5)]
+
+
+@pytest.mark.parametrize("case", SCONV_CASES)
+def test_spectral_conv_fused_matches_torch_fft(case):
+    """CayleyConv.forward_hwcb_fused (HIP rfft2 / irfft2 + GroupSort around the complex GEMMs) vs
+    the torch.fft path (forward_hwcb + GroupSort) in float64, forward and every gradient."""
+    from fiode_amd.cayley import CayleyConv
+    cin, cout, stride, size, gs, B = case
+    dev = _dev()
+    torch.manual_seed(cin + cout + size)
+    conv = CayleyConv(cin, cout, 3, stride=stride).to(dev)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    n = size // stride
+    conv.spectral_weight(n, dev)                        # alpha init
+    ref = CayleyConv(cin, cout, 3, stride=stride).to(dev).double()
+    ref.load_state_dict(conv.state_dict())
+    x = torch.randn(size, size, cin, B, device=dev)
+    g = torch.randn(n, n, cout, B, device=dev, dtype=torch.float64)
+    xa = x.clone().requires_grad_(True)
+    y = conv.forward_hwcb_fused(xa, gs)
+    (y.double() * g).sum().backward()
+    xb = x.double().requires_grad_(True)
+    xr = xb
+    if stride == 2:
+        h, w, c, bb = xr.shape
+        xr = xr.reshape(h // 2, 2, w // 2, 2, c, bb).permute(0, 2, 4, 1, 3, 5).reshape(h // 2, w // 2, c * 4, bb)
+    nf = n * (n // 2 + 1)
+    xf = torch.fft.rfft2(xr, dim=(0, 1)).reshape(nf, xr.shape[2], B)
+    yf = _spectral_ref64(ref, n, dev) @ xf
+    yf = torch.cat([yf[:1] + (float(n * n) * ref.bias)[:, None], yf[1:]])
+    yr = torch.fft.irfft2(yf.reshape(n, n // 2 + 1, cout, B), s=(n, n), dim=(0, 1))
+    if gs:
+        a, b = yr.split(cout // 2, 2)
+        yr = torch.cat([torch.maximum(a, b), torch.minimum(a, b)], dim=2)
+    (yr * g).sum().backward()
+    assert float((y.double() - yr).abs().max()) <= 2e-5 * (float(yr.abs().max()) + 1)
+    for name, p, q in [("x", xa, xb), ("weight", conv.weight, ref.weight), ("alpha", conv.alpha, ref.alpha),
+                       ("bias", conv.bias, ref.bias)]:
+        d, r = p.grad.double(), q.grad
+        assert float((d - r).abs().max()) <= 2e-4 * (float(r.abs().max()) + 1e-6), name
+
+
+def test_sconv_rejects_bad_shapes():
+    from fiode_amd import ops
+    from fiode_amd._lib import FiodeError
+    dev = _dev()
+    with pytest.raises(FiodeError, match="unsupported shape"):
+        ops.sconv_rfft2(torch.zeros(64, 64, 3, 4, device=dev), 64, 3, 4)      # n > 32
+    with pytest.raises(FiodeError, match="unsupported shape"):   # space-to-channel needs C % 4 == 0
+        ops.sconv_irfft2(torch.zeros(8 * 5, 6, 4, dtype=torch.complex64, device=dev), 8, 6, 4, downsample=True)
+    with pytest.raises(ValueError):
+        ops.sconv_irfft2(torch.zeros(8 * 5, 6, 3, dtype=torch.complex64, device=dev), 8, 6, 4)   # wrong B
