@@ -14,9 +14,10 @@
 //   k_sconv_irfft2   y = irfft2(Y) (torch's c2c-then-c2r order and 1/n^2 scaling), optional + bias
 //                    and GroupSort (pairs c, c + C/2; codes saved for the backward), or the
 //                    inverse space-to-channel scatter (the input gradient of a stride-2 conv).
-// n in {8, 16, 32}, so each transform is a direct DFT per axis against an n-entry table of roots of unity
-// (n^2 (n/2+1) x 2 complex MACs per image, ~17 K at n = 32) on an LDS image of BT images of one
-// channel: no butterflies, no bit reversal, coalesced BT-wide loads and stores along B.
+// n in {8, 16, 32}, so each transform is a direct DFT per axis (n^2 (n/2+1) x 2 complex MACs per
+// image, ~17 K at n = 32), one length-n DFT per thread with inputs and twiddles in registers, on
+// an LDS image of BT images of one channel: no butterflies, no bit reversal, coalesced BT-wide
+// loads and stores along B.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,7 +27,7 @@
 namespace {
 
 typedef float2 c32;
-constexpr int NT = 256;
+constexpr int NT = 512;
 constexpr int BT_F = 16;     // images per forward-transform workgroup
 constexpr int BT_I = 8;      // images per inverse-transform workgroup
 
@@ -52,11 +53,15 @@ struct SArgs {
   uint8_t* code_out;             // [n][n][C/2][B]
 };
 
-__device__ __forceinline__ void roots_table(c32* tw, int n, float sign) {
-  for (int m = threadIdx.x; m < n; m += NT) {
-    float s, c;
-    sincospif(2.0f * (float)m / (float)n, &s, &c);
-    tw[m] = make_float2(c, sign * s);
+// e^{sign 2 pi i m / N}, m < N, in registers (every index below is a compile-time constant once the
+// transform loops are unrolled, so the table never touches LDS)
+template <int N>
+__device__ __forceinline__ void twiddles(c32 (&t)[N], float sign) {
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    float sn, cs;
+    sincospif(2.0f * (float)m / (float)N, &sn, &cs);
+    t[m] = make_float2(cs, sign * sn);
   }
 }
 
@@ -80,115 +85,154 @@ struct Geo {
 };
 
 // ---- X[f][c][b0..b0+BT) = rfft2 of channel c ------------------------------------------------------
-template <int N>
+template <int N, int BT>
 __global__ void __launch_bounds__(NT) k_sconv_rfft2(SArgs a) {
   typedef Geo<N> g;
-  __shared__ float img[BT_F * g::IS];
-  __shared__ c32 Z[BT_F * g::ZS];
-  __shared__ c32 tw[N];
+  __shared__ float img[BT * g::IS];
+  __shared__ c32 Z[BT * g::ZS];
   constexpr int H = g::H;
-  const int c = blockIdx.x, b0 = blockIdx.y * BT_F, tid = threadIdx.x;
-  roots_table(tw, N, -1.0f);
+  constexpr int NL = BT * N * N;
+  const int c = blockIdx.x, b0 = blockIdx.y * BT, tid = threadIdx.x;
   const int half = a.C >> 1;
-  for (int idx = tid; idx < BT_F * N * N; idx += NT) {
-    const int bt = idx % BT_F, hw = idx / BT_F, h = hw / N, w = hw % N;
-    const int b = b0 + bt;
-    float v = 0.f;
-    if (b < a.B) {
-      if (a.gy) {                                  // GroupSort backward: d/dpre of channel c
-        const bool first = c < half;
-        const int cp = first ? c + half : c - half;
-        const uint8_t code = a.code[(((int64_t)h * N + w) * half + (first ? c : cp)) * a.B + b];
-        v = gs_grad(a.gy[act_index(a, h, w, first ? c : cp, b)], a.gy[act_index(a, h, w, first ? cp : c, b)], code,
-                    first);
-      } else {
-        v = a.ds ? a.x[raw_index(a, h, w, c, b)] : a.x[act_index(a, h, w, c, b)];
-      }
+  // the loads of many loop trips must be in flight together (a trip-by-trip loop waits ~1 us per
+  // trip on the memory latency): fixed trip counts, unrolled, one loop per source mode
+  if (a.gy) {                                      // GroupSort backward: d/dpre of channel c
+    const bool first = c < half;
+    const int cp = first ? c + half : c - half, cmx = first ? c : cp, cmn = first ? cp : c;
+#pragma unroll 16
+    for (int idx = tid; idx < NL; idx += NT) {
+      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+      const int b = min(b0 + bt, a.B - 1);
+      const uint8_t code = a.code[(((int64_t)h * N + w) * half + cmx) * a.B + b];
+      const float gmx = a.gy[act_index(a, h, w, cmx, b)], gmn = a.gy[act_index(a, h, w, cmn, b)];
+      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? gs_grad(gmx, gmn, code, first) : 0.f;
     }
-    img[bt * g::IS + h * g::RS + w] = v;
+  } else if (a.ds) {
+#pragma unroll 16
+    for (int idx = tid; idx < NL; idx += NT) {
+      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+      const int b = min(b0 + bt, a.B - 1);
+      const float v = a.x[raw_index(a, h, w, c, b)];
+      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? v : 0.f;
+    }
+  } else {
+#pragma unroll 16
+    for (int idx = tid; idx < NL; idx += NT) {
+      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+      const int b = min(b0 + bt, a.B - 1);
+      const float v = a.x[act_index(a, h, w, c, b)];
+      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? v : 0.f;
+    }
   }
   __syncthreads();
-  // r2c along w
-  for (int idx = tid; idx < BT_F * N * H; idx += NT) {
-    const int bt = idx % BT_F, r = idx / BT_F, h = r / H, kb = r % H;
-    const float* row = img + bt * g::IS + h * g::RS;
-    c32 z = make_float2(0.f, 0.f);
-    int m = 0;
+  // The two 1-D transforms as one length-N DFT per thread in registers (rows, then columns): N^2
+  // complex MACs of pure VALU per transform with the inputs and twiddles in registers -- a
+  // tap-by-tap LDS loop here was LDS-latency bound at one wave per SIMD (~90 cycles per MAC).
+  c32 tw[N];
+  twiddles<N>(tw, -1.0f);
+  // r2c along w: one (image, h) row per thread; input-outer / output-inner loop order so the H
+  // accumulators form independent FMA chains (one wave per SIMD has no other latency hiding)
+  for (int row = tid; row < BT * N; row += NT) {
+    const int bt = row % BT, h = row / BT;
+    const float* src = img + bt * g::IS + h * g::RS;
+    c32 acc[H];
+#pragma unroll
+    for (int kb = 0; kb < H; ++kb) acc[kb] = make_float2(0.f, 0.f);
 #pragma unroll
     for (int w = 0; w < N; ++w) {
-      const float v = row[w];
-      const c32 e = tw[m];
-      z.x = fmaf(v, e.x, z.x);
-      z.y = fmaf(v, e.y, z.y);
-      m = (m + kb) & (N - 1);
+      const float v = src[w];
+#pragma unroll
+      for (int kb = 0; kb < H; ++kb) {
+        const c32 e = tw[(kb * w) % N];
+        acc[kb].x = fmaf(v, e.x, acc[kb].x);
+        acc[kb].y = fmaf(v, e.y, acc[kb].y);
+      }
     }
-    Z[bt * g::ZS + h * H + kb] = z;
+#pragma unroll
+    for (int kb = 0; kb < H; ++kb) Z[bt * g::ZS + h * H + kb] = acc[kb];
   }
   __syncthreads();
-  // c2c along h, written as X[f][c][b]
-  for (int idx = tid; idx < BT_F * N * H; idx += NT) {
-    const int bt = idx % BT_F, f = idx / BT_F, ka = f / H, kb = f % H;
-    const c32* col = Z + bt * g::ZS + kb;
-    c32 z = make_float2(0.f, 0.f);
-    int m = 0;
+  // c2c along h: one (image, kb) column per thread, written as X[f][c][b]
+  for (int col = tid; col < BT * H; col += NT) {
+    const int bt = col % BT, kb = col / BT;
+    c32 acc[N];
+#pragma unroll
+    for (int ka = 0; ka < N; ++ka) acc[ka] = make_float2(0.f, 0.f);
 #pragma unroll
     for (int h = 0; h < N; ++h) {
-      const c32 v = col[h * H], e = tw[m];
-      z.x = fmaf(v.x, e.x, fmaf(-v.y, e.y, z.x));
-      z.y = fmaf(v.x, e.y, fmaf(v.y, e.x, z.y));
-      m = (m + ka) & (N - 1);
+      const c32 v = Z[bt * g::ZS + h * H + kb];
+#pragma unroll
+      for (int ka = 0; ka < N; ++ka) {
+        const c32 e = tw[(ka * h) % N];
+        acc[ka].x = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[ka].x));
+        acc[ka].y = fmaf(v.x, e.y, fmaf(v.y, e.x, acc[ka].y));
+      }
     }
     const int b = b0 + bt;
-    if (b < a.B) a.X[((int64_t)f * a.C + c) * a.B + b] = z;
+    if (b < a.B) {
+#pragma unroll
+      for (int ka = 0; ka < N; ++ka) a.X[((int64_t)(ka * H + kb) * a.C + c) * a.B + b] = acc[ka];
+    }
   }
 }
 
 // irfft2 of one channel of BT_I images into out (LDS, real image stride Geo<N>::IS)
 template <int N>
-__device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c32* Ys, c32* Zs, float* out,
-                                               const c32* tw) {
+__device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c32* Ys, c32* Zs, float* out) {
   typedef Geo<N> g;
   constexpr int H = g::H;
   const int tid = threadIdx.x;
+#pragma unroll 16
   for (int idx = tid; idx < BT_I * N * H; idx += NT) {
     const int bt = idx % BT_I, f = idx / BT_I;
-    const int b = b0 + bt;
-    Ys[bt * g::ZS + f] = b < a.B ? a.Y[((int64_t)f * a.C + c) * a.B + b] : make_float2(0.f, 0.f);
+    const int b = min(b0 + bt, a.B - 1);
+    const c32 v = a.Y[((int64_t)f * a.C + c) * a.B + b];
+    Ys[bt * g::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
   }
   __syncthreads();
-  // inverse c2c along ka -> h
-  for (int idx = tid; idx < BT_I * N * H; idx += NT) {
-    const int bt = idx % BT_I, r = idx / BT_I, h = r / H, kb = r % H;
-    const c32* col = Ys + bt * g::ZS + kb;
-    c32 z = make_float2(0.f, 0.f);
-    int m = 0;
+  c32 tw[N];
+  twiddles<N>(tw, 1.0f);
+  // inverse c2c along ka: one (image, kb) column per thread (input-outer, independent accumulators)
+  for (int col = tid; col < BT_I * H; col += NT) {
+    const int bt = col % BT_I, kb = col / BT_I;
+    c32 acc[N];
+#pragma unroll
+    for (int h = 0; h < N; ++h) acc[h] = make_float2(0.f, 0.f);
 #pragma unroll
     for (int ka = 0; ka < N; ++ka) {
-      const c32 v = col[ka * H], e = tw[m];
-      z.x = fmaf(v.x, e.x, fmaf(-v.y, e.y, z.x));
-      z.y = fmaf(v.x, e.y, fmaf(v.y, e.x, z.y));
-      m = (m + h) & (N - 1);
+      const c32 v = Ys[bt * g::ZS + ka * H + kb];
+#pragma unroll
+      for (int h = 0; h < N; ++h) {
+        const c32 e = tw[(ka * h) % N];
+        acc[h].x = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[h].x));
+        acc[h].y = fmaf(v.x, e.y, fmaf(v.y, e.x, acc[h].y));
+      }
     }
-    Zs[bt * g::ZS + h * H + kb] = z;
+#pragma unroll
+    for (int h = 0; h < N; ++h) Zs[bt * g::ZS + h * H + kb] = acc[h];
   }
   __syncthreads();
-  // c2r along kb -> w: Re Z0 + Re(Z_{n/2} (-1)^w) + 2 sum_mid Re(Z_kb e^{+i..}), / n^2
+  // c2r along kb: one (image, h) row per thread: Re Z0 + Re(Z_{n/2} (-1)^w) + 2 sum_mid Re(Z_kb e^{+i..})
   constexpr float inv = 1.0f / (float)(N * N);
   constexpr int nh = N / 2;
-  for (int idx = tid; idx < BT_I * N * N; idx += NT) {
-    const int bt = idx % BT_I, hw = idx / BT_I, h = hw / N, w = hw % N;
-    const c32* row = Zs + bt * g::ZS + h * H;
-    float s = 0.f;
-    int m = w;
+  for (int row = tid; row < BT_I * N; row += NT) {
+    const int bt = row % BT_I, h = row / BT_I;
+    const c32* src = Zs + bt * g::ZS + h * H;
+    float acc[N];
+    const float z0 = src[0].x, zn = src[nh].x;
+#pragma unroll
+    for (int w = 0; w < N; ++w) acc[w] = 0.f;
 #pragma unroll
     for (int kb = 1; kb < nh; ++kb) {
-      const c32 v = row[kb], e = tw[m];
-      s = fmaf(v.x, e.x, fmaf(-v.y, e.y, s));
-      m = (m + w) & (N - 1);
+      const c32 v = src[kb];
+#pragma unroll
+      for (int w = 0; w < N; ++w) {
+        const c32 e = tw[(kb * w) % N];
+        acc[w] = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[w]));
+      }
     }
-    const float zn = row[nh].x;
-    const float v = row[0].x + ((w & 1) ? -zn : zn) + 2.0f * s;
-    out[bt * g::IS + h * g::RS + w] = v * inv;
+#pragma unroll
+    for (int w = 0; w < N; ++w) out[bt * g::IS + h * g::RS + w] = (z0 + ((w & 1) ? -zn : zn) + 2.0f * acc[w]) * inv;
   }
   __syncthreads();
 }
@@ -202,14 +246,11 @@ __global__ void __launch_bounds__(NT) k_sconv_irfft2(SArgs a) {
   __shared__ c32 Zs[BT_I * g::ZS];
   __shared__ float o0[BT_I * g::IS];
   __shared__ float o1[BT_I * g::IS];
-  __shared__ c32 tw[N];
   const int b0 = blockIdx.y * BT_I, tid = threadIdx.x;
-  roots_table(tw, N, 1.0f);
-  __syncthreads();
   if (a.gs) {
     const int half = a.C >> 1, c0 = blockIdx.x, c1 = c0 + half;
-    irfft2_channel<N>(a, c0, b0, Ys, Zs, o0, tw);
-    irfft2_channel<N>(a, c1, b0, Ys, Zs, o1, tw);
+    irfft2_channel<N>(a, c0, b0, Ys, Zs, o0);
+    irfft2_channel<N>(a, c1, b0, Ys, Zs, o1);
     const float bb0 = a.bias ? a.bias[c0] : 0.f, bb1 = a.bias ? a.bias[c1] : 0.f;
     for (int idx = tid; idx < BT_I * N * N; idx += NT) {
       const int bt = idx % BT_I, hw = idx / BT_I, h = hw / N, w = hw % N;
@@ -223,7 +264,7 @@ __global__ void __launch_bounds__(NT) k_sconv_irfft2(SArgs a) {
     }
   } else {
     const int c = blockIdx.x;
-    irfft2_channel<N>(a, c, b0, Ys, Zs, o0, tw);
+    irfft2_channel<N>(a, c, b0, Ys, Zs, o0);
     const float bb = a.bias ? a.bias[c] : 0.f;
     for (int idx = tid; idx < BT_I * N * N; idx += NT) {
       const int bt = idx % BT_I, hw = idx / BT_I, h = hw / N, w = hw % N;
@@ -261,11 +302,21 @@ extern "C" int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, co
   a.gy = gy;
   a.code = code;
   a.X = (c32*)X;
-  const dim3 grid(a.C, (a.B + BT_F - 1) / BT_F);
   hipStream_t st = (hipStream_t)stream;
-  if (a.n == 8) hipLaunchKernelGGL(k_sconv_rfft2<8>, grid, dim3(NT), 0, st, a);
-  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_rfft2<16>, grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL(k_sconv_rfft2<32>, grid, dim3(NT), 0, st, a);
+  // few channels (the 3-channel input of conv 1): 4 images per workgroup to spread over the CUs
+  const bool small = (int64_t)a.C * ((a.B + BT_F - 1) / BT_F) < 256;
+  const int bt = small ? 4 : BT_F;
+  const dim3 grid(a.C, (a.B + bt - 1) / bt);
+  if (a.n == 8) {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(NT), 0, st, a);
+  } else if (a.n == 16) {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(NT), 0, st, a);
+  } else {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<32, BT_F>), grid, dim3(NT), 0, st, a);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

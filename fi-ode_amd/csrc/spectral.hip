@@ -60,7 +60,10 @@ struct SpecArgs {
   const float* w;                   // [cout][cin][ks][ks]
   const float* alpha;               // [1]
   float* part;                      // [nparts] ||Wf||^2 partials
-  float* dpart;                     // [nf] D partials
+  float* dpart;                     // [ndpart] D partials
+  int ndpart;                       // nf (fused path) or nf * tiles (split path)
+  c32* B1;                          // [nf][K][K] split-path scratch (M, then G_inv, G_M)
+  c32* B2;                          // [nf][K][K] split-path scratch (T1)
   c32* Q;                           // [nf][cout][cin]
   c32* inv;                         // [nf][K][K]
   const c32* gQ;                    // [nf][cout][cin]
@@ -412,6 +415,208 @@ __global__ void __launch_bounds__(NT) k_spec_bwd(SpecArgs a) {
   }
 }
 
+// ---- split path (K > 32): the per-frequency products as 16 x 16 tiles over many workgroups -----
+// With K = 64 (KWLarge conv 4: 40 frequencies, X = 256 x 64) one workgroup per frequency leaves
+// 216 of 256 CUs idle and runs ~2.6 M complex MACs per CU on the VALU; here only the Gauss-Jordan
+// inverse stays one-workgroup-per-frequency, every product is a grid of 16 x 16 output tiles
+// (256 threads, one output each, operands staged through LDS in 64-deep panels).
+constexpr int TL = 16, KP = 64;
+
+// X element (r, c) of frequency f, scaled: sc * Wf
+__device__ __forceinline__ c32 xs(const SpecArgs& a, int f, int r, int c, float sc) {
+  return cscale(a.Wx[((int64_t)f * a.R + r) * a.K + c], sc);
+}
+__device__ __forceinline__ c32 gq(const SpecArgs& a, int f, int r, int j) {   // dL/dQ in X's orientation
+  const c32* Gf = a.gQ + (int64_t)f * a.cout * a.cin;
+  return a.wide ? Gf[(int64_t)j * a.cin + r] : Gf[(int64_t)r * a.cin + j];
+}
+
+// M = I + sc (U - U^H) + sc^2 V^H V   ->  B1
+__global__ void __launch_bounds__(TL * TL) k_spec_gram(SpecArgs a) {
+  __shared__ c32 Pi[KP][TL + 1], Pj[KP][TL + 1];
+  __shared__ float slot;
+  const int f = blockIdx.x, nt = a.K / TL, ti = blockIdx.y / nt, tj = blockIdx.y % nt, tid = threadIdx.x;
+  const int li = tid / TL, lj = tid % TL, i = ti * TL + li, j = tj * TL + lj;
+  const float sc = norm_scale(a, &slot);
+  c32 acc = make_float2(0.f, 0.f);
+  for (int r0 = a.K; r0 < a.R; r0 += KP) {
+    const int rows = min(KP, a.R - r0);
+    __syncthreads();
+    for (int idx = tid; idx < rows * TL; idx += TL * TL) {
+      const int r = idx / TL, c = idx % TL;
+      Pi[r][c] = xs(a, f, r0 + r, ti * TL + c, sc);
+      Pj[r][c] = xs(a, f, r0 + r, tj * TL + c, sc);
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int r = 0; r < rows; ++r) acc = cfma_conj(Pi[r][li], Pj[r][lj], acc);
+  }
+  c32 m = cadd(csub(xs(a, f, i, j, sc), cconj(xs(a, f, j, i, sc))), acc);
+  if (i == j) m.x += 1.0f;
+  a.B1[((int64_t)f * a.K + i) * a.K + j] = m;
+}
+
+// inv = M^-1 (one workgroup per frequency), Q top = 2 inv - I
+template <int NP, int TR, int TC, int NT>
+__global__ void __launch_bounds__(NT) k_spec_inv(SpecArgs a) {
+  typedef fiode_gj::GJ<ComplexOps, NP, TR, TC> G;
+  __shared__ typename G::Smem gsm;
+  const int f = blockIdx.x, K = a.K;
+  c32 m[TR][TC];
+  G::load(m, a.B1 + (int64_t)f * K * K, K, K);
+  G::invert(m, K, gsm);
+  G::store(m, a.inv + (int64_t)f * K * K, K, K);
+  c32* Qf = a.Q + (int64_t)f * a.cout * a.cin;
+  const int r0 = (threadIdx.x / G::CT) * TR, c0 = (threadIdx.x % G::CT) * TC;
+#pragma unroll
+  for (int r = 0; r < TR; ++r)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      if (i < K && j < K) {
+        c32 v = cscale(m[r][c], 2.0f);
+        if (i == j) v.x -= 1.0f;
+        if (a.wide) Qf[(int64_t)j * a.cin + i] = v;
+        else Qf[(int64_t)i * a.cin + j] = v;
+      }
+    }
+}
+
+// Q bottom = -2 sc V inv, tile (rows K + 16 tr.., cols 16 tc..)
+__global__ void __launch_bounds__(TL * TL) k_spec_qbot(SpecArgs a) {
+  __shared__ c32 Vt[TL][KP + 1], It[KP][TL + 1];
+  __shared__ float slot;
+  const int f = blockIdx.x, nt = a.K / TL, tr = blockIdx.y / nt, tc = blockIdx.y % nt, tid = threadIdx.x;
+  const float sc = norm_scale(a, &slot);
+  // wide outputs are stored [j][r]: let the row index run fastest across threads
+  const int lr = a.wide ? tid % TL : tid / TL, lc = a.wide ? tid / TL : tid % TL;
+  const int r = a.K + tr * TL + lr, j = tc * TL + lc;
+  c32 acc = make_float2(0.f, 0.f);
+  for (int k0 = 0; k0 < a.K; k0 += KP) {
+    __syncthreads();
+    for (int idx = tid; idx < TL * KP; idx += TL * TL) {
+      const int q = idx / KP, k = idx % KP;
+      const int rr = a.K + tr * TL + q;
+      Vt[q][k] = rr < a.R ? xs(a, f, rr, k0 + k, sc) : make_float2(0.f, 0.f);
+      const int kk = idx / TL, c = idx % TL;
+      It[kk][c] = a.inv[((int64_t)f * a.K + k0 + kk) * a.K + tc * TL + c];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < KP; ++k) acc = cfma(Vt[lr][k], It[k][lc], acc);
+  }
+  if (r < a.R) {
+    c32* Qf = a.Q + (int64_t)f * a.cout * a.cin;
+    const c32 v = cscale(acc, -2.0f);
+    if (a.wide) Qf[(int64_t)j * a.cin + r] = v;
+    else Qf[(int64_t)r * a.cin + j] = v;
+  }
+}
+
+// backward 1: G_inv = 2 Gt - 2 V^H Gb  ->  B1
+__global__ void __launch_bounds__(TL * TL) k_spec_ginv(SpecArgs a) {
+  __shared__ c32 Pi[KP][TL + 1], Pj[KP][TL + 1];
+  __shared__ float slot;
+  const int f = blockIdx.x, nt = a.K / TL, ti = blockIdx.y / nt, tj = blockIdx.y % nt, tid = threadIdx.x;
+  const int li = tid / TL, lj = tid % TL, i = ti * TL + li, j = tj * TL + lj;
+  const float sc = norm_scale(a, &slot);
+  c32 acc = make_float2(0.f, 0.f);
+  for (int r0 = a.K; r0 < a.R; r0 += KP) {
+    const int rows = min(KP, a.R - r0);
+    __syncthreads();
+    for (int idx = tid; idx < rows * TL; idx += TL * TL) {
+      const int r = idx / TL, c = idx % TL;
+      Pi[r][c] = xs(a, f, r0 + r, ti * TL + c, sc);
+      Pj[r][c] = gq(a, f, r0 + r, tj * TL + c);
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int r = 0; r < rows; ++r) acc = cfma_conj(Pi[r][li], Pj[r][lj], acc);
+  }
+  a.B1[((int64_t)f * a.K + i) * a.K + j] = cscale(csub(gq(a, f, i, j), acc), 2.0f);
+}
+
+// backward 2/3: dst = s * A @ M^-H  (AH = false)  or  dst = s * M^-H @ A  (AH = true), K x K
+template <bool LEFT>
+__global__ void __launch_bounds__(TL * TL) k_spec_kk(SpecArgs a, const c32* __restrict__ A, c32* __restrict__ dst,
+                                                    float s) {
+  __shared__ c32 Pa[TL][KP + 1], Pb[KP][TL + 1];
+  const int f = blockIdx.x, nt = a.K / TL, ti = blockIdx.y / nt, tj = blockIdx.y % nt, tid = threadIdx.x;
+  const int li = tid / TL, lj = tid % TL, K = a.K;
+  const c32* Af = A + (int64_t)f * K * K;
+  const c32* If = a.inv + (int64_t)f * K * K;
+  c32 acc = make_float2(0.f, 0.f);
+  for (int k0 = 0; k0 < K; k0 += KP) {
+    __syncthreads();
+    for (int idx = tid; idx < TL * KP; idx += TL * TL) {
+      const int q = idx / KP, k = idx % KP;          // left operand row q, col k0 + k
+      const int kk = idx / TL, c = idx % TL;         // right operand row k0 + kk, col c
+      const int gi = ti * TL + q, gj = tj * TL + c;
+      if (LEFT) {   // M^-H (gi, k) = conj(inv[k][gi]);  A (k, gj)
+        Pa[q][k] = cconj(If[(int64_t)(k0 + k) * K + gi]);
+        Pb[kk][c] = Af[(int64_t)(k0 + kk) * K + gj];
+      } else {      // A (gi, k);  M^-H (k, gj) = conj(inv[gj][k])
+        Pa[q][k] = Af[(int64_t)gi * K + k0 + k];
+        Pb[kk][c] = cconj(If[(int64_t)gj * K + k0 + kk]);
+      }
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < KP; ++k) acc = cfma(Pa[li][k], Pb[k][lj], acc);
+  }
+  dst[((int64_t)f * K + ti * TL + li) * K + tj * TL + lj] = cscale(acc, s);
+}
+
+// backward 4: gX rows r (all R): r < K: gU = G_M - G_M^H;  r >= K: gV = V H - 2 Gb M^-H,
+// H = G_M + G_M^H (G_M in B1).  D partial per workgroup.
+__global__ void __launch_bounds__(TL * TL) k_spec_gv(SpecArgs a) {
+  __shared__ c32 Vt[TL][KP + 1], Gt_[TL][KP + 1], Ht[KP][TL + 1], It[KP][TL + 1];
+  __shared__ float slot, red[TL * TL / 64];
+  const int f = blockIdx.x, nt = a.K / TL, tr = blockIdx.y / nt, tc = blockIdx.y % nt, tid = threadIdx.x;
+  const int K = a.K;
+  const float sc = norm_scale(a, &slot);
+  const int lr = a.wide ? tid % TL : tid / TL, lc = a.wide ? tid / TL : tid % TL;
+  const int r = tr * TL + lr, j = tc * TL + lc;
+  const c32* GM = a.B1 + (int64_t)f * K * K;
+  const c32* If = a.inv + (int64_t)f * K * K;
+  c32 out = make_float2(0.f, 0.f);
+  if (tr * TL < K) {                      // gU tile (uniform per workgroup: K % 16 == 0)
+    out = csub(GM[(int64_t)r * K + j], cconj(GM[(int64_t)j * K + r]));
+  } else {
+    for (int k0 = 0; k0 < K; k0 += KP) {
+      __syncthreads();
+      for (int idx = tid; idx < TL * KP; idx += TL * TL) {
+        const int q = idx / KP, k = idx % KP;
+        const int rr = tr * TL + q;
+        Vt[q][k] = rr < a.R ? xs(a, f, rr, k0 + k, sc) : make_float2(0.f, 0.f);
+        Gt_[q][k] = rr < a.R ? gq(a, f, rr, k0 + k) : make_float2(0.f, 0.f);
+        const int kk = idx / TL, c = idx % TL, gk = k0 + kk, gj = tc * TL + c;
+        Ht[kk][c] = cadd(GM[(int64_t)gk * K + gj], cconj(GM[(int64_t)gj * K + gk]));
+        It[kk][c] = cconj(If[(int64_t)gj * K + gk]);
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int k = 0; k < KP; ++k) out = cfma(Vt[lr][k], Ht[k][lc], cfma(cscale(Gt_[lr][k], -2.0f), It[k][lc], out));
+    }
+  }
+  float d = 0.f;
+  if (r < a.R) {
+    c32* gXf = a.gX + (int64_t)f * a.cout * a.cin;
+    if (a.wide) gXf[(int64_t)j * a.cin + r] = out;
+    else gXf[(int64_t)r * a.cin + j] = out;
+    const c32 w = a.Wx[((int64_t)f * a.R + r) * K + j];     // unscaled Wf
+    d = fmaf(out.x, w.x, out.y * w.y);
+  }
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+  if ((tid & 63) == 0) red[tid >> 6] = d;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int q = 0; q < TL * TL / 64; ++q) s += red[q];
+    a.dpart[(int64_t)f * gridDim.y + blockIdx.y] = s;
+  }
+}
+
 // ---- taps: TP (co, ci) pairs per block, FG frequency groups per pair ---------------------------
 constexpr int TAPS_TP = 32, TAPS_FG = 8;
 __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
@@ -423,7 +628,7 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
   __shared__ float slot[2];
   float nrm;
   const float sc = norm_scale(a, &slot[0], &nrm);
-  const float D = block_sum_fixed(a.dpart, a.nf, &slot[1]);
+  const float D = block_sum_fixed(a.dpart, a.ndpart, &slot[1]);
   const float cw = a.alpha[0] * D / (nrm * nrm * nrm);
   if (blockIdx.x == 0 && tid == 0) a.galpha[0] = D / nrm;
   const int pair = blockIdx.x * TAPS_TP + pl;
@@ -470,7 +675,8 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
 // ---- host side ----------------------------------------------------------------------------------
 struct Plan {
   SpecArgs a;
-  size_t ws_part, ws_dpart, ws_gx, ws_wx, ws_total;
+  size_t ws_part, ws_dpart, ws_gx, ws_wx, ws_b1, ws_b2, ws_total;
+  bool split;
 };
 
 int make_plan(const fiode_spectral_config* cfg, Plan& p) {
@@ -492,11 +698,18 @@ int make_plan(const fiode_spectral_config* cfg, Plan& p) {
   if (lds_f + 8192 > 163840 || lds_b > 163840) return FIODE_ESHAPE;
   a.nparts = ((a.R * a.K + NORM_THREADS - 1) / NORM_THREADS) * ((a.nf + DFT_FG - 1) / DFT_FG);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  p.split = a.K > 32;
+  if (p.split && a.K % TL) return FIODE_ESHAPE;
+  a.ndpart = p.split ? a.nf * (a.R / TL) * (a.K / TL) : a.nf;
+  if (p.split && a.R % TL) return FIODE_ESHAPE;
+  const size_t kk = p.split ? (size_t)a.nf * a.K * a.K * sizeof(c32) : 0;
   p.ws_part = 0;
   p.ws_dpart = al((size_t)a.nparts * 4);
-  p.ws_gx = p.ws_dpart + al((size_t)a.nf * 4);
+  p.ws_gx = p.ws_dpart + al((size_t)a.ndpart * 4);
   p.ws_wx = p.ws_gx + al((size_t)a.nf * a.cout * a.cin * sizeof(c32));
-  p.ws_total = p.ws_wx + al((size_t)a.nf * a.cout * a.cin * sizeof(c32));
+  p.ws_b1 = p.ws_wx + al((size_t)a.nf * a.cout * a.cin * sizeof(c32));
+  p.ws_b2 = p.ws_b1 + al(kk);
+  p.ws_total = p.ws_b2 + al(kk);
   return FIODE_OK;
 }
 
@@ -506,6 +719,8 @@ void bind_ws(Plan& p, void* ws) {
   p.a.dpart = (float*)(b + p.ws_dpart);
   p.a.gX = (c32*)(b + p.ws_gx);
   p.a.Wx = (c32*)(b + p.ws_wx);
+  p.a.B1 = (c32*)(b + p.ws_b1);
+  p.a.B2 = (c32*)(b + p.ws_b2);
 }
 
 }  // namespace
@@ -535,7 +750,12 @@ extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_
   const size_t lds = (size_t)a.R * a.K * sizeof(c32);
   if (a.K <= 16) hipLaunchKernelGGL((k_spec_fwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
   else if (a.K <= 32) hipLaunchKernelGGL((k_spec_fwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((k_spec_fwd<64, 2, 2, 1024>), dim3(a.nf), dim3(1024), lds, st, a);
+  else {
+    const int nt = a.K / TL;
+    hipLaunchKernelGGL(k_spec_gram, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
+    hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
+    if (a.R > a.K) hipLaunchKernelGGL(k_spec_qbot, dim3(a.nf, ((a.R - a.K) / TL) * nt), dim3(TL * TL), 0, st, a);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
@@ -561,7 +781,13 @@ extern "C" int fiode_spectral_cayley_backward(void* stream, const fiode_spectral
   const size_t lds = (size_t)(a.R + a.K) * a.K * sizeof(c32);
   if (a.K <= 16) hipLaunchKernelGGL((k_spec_bwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
   else if (a.K <= 32) hipLaunchKernelGGL((k_spec_bwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((k_spec_bwd<64, 2, 2, 1024>), dim3(a.nf), dim3(1024), lds, st, a);
+  else {
+    const int nt = a.K / TL;
+    hipLaunchKernelGGL(k_spec_ginv, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
+    hipLaunchKernelGGL(k_spec_kk<false>, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a, (const c32*)a.B1, a.B2, 1.0f);
+    hipLaunchKernelGGL(k_spec_kk<true>, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a, (const c32*)a.B2, a.B1, -1.0f);
+    hipLaunchKernelGGL(k_spec_gv, dim3(a.nf, (a.R / TL) * nt), dim3(TL * TL), 0, st, a);
+  }
   hipLaunchKernelGGL(k_spec_taps, dim3((a.cout * a.cin + TAPS_TP - 1) / TAPS_TP), dim3(TAPS_TP * TAPS_FG), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;

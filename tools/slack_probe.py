@@ -1,0 +1,93 @@
+"""Critical-path probe of the replayed configs[1] step (not a test): a ~200 us GPU spin is
+inserted in front of one part of the step (on whatever stream that part runs), and the growth of
+the hipGraph step time tells whether that part is on the critical path (growth ~ 200 us) or has
+slack (growth ~ 0).
+
+python tools/slack_probe.py  ->  one JSON line: ms per step per variant
+"""
+import json
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fiode_amd import cayley as CY, lyapunov as LY, ops  # noqa: E402
+from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+
+
+def calib():
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(1000)
+    a.record()
+    torch.cuda._sleep(1_000_000)
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / 1_000_000
+
+
+MS_PER_CYCLE = calib()
+SPIN = int(0.2 / MS_PER_CYCLE)     # cycles for ~200 us
+
+
+def step_ms(steps=40):
+    mod = bench.build_module(dev, train_ode=True)
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    gs = GraphTrainStep(mod, opt, x, y)
+    for _ in range(5):
+        gs.step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        gs.step()
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t) / steps * 1e3, 4)
+
+
+def spin_before(owner, name, once_per_step=True):
+    orig = getattr(owner, name)
+
+    def wrapped(*a, **k):
+        torch.cuda._sleep(SPIN)
+        return orig(*a, **k)
+    setattr(owner, name, wrapped)
+    return lambda: setattr(owner, name, orig)
+
+
+variants = [
+    ("baseline", None),
+    ("conv0_map_fwd (side stream 0)", (CY._SpectralCayleyFn, "forward")),
+    ("linear_map_fwd (side streams 1-2)", (CY.CayleyLinear, "effective_weight")),
+    ("dyn_map_fwd (side stream 3)", (__import__("fiode_amd.dynamics", fromlist=["x"]), "cayley_scaled")),
+    ("odetrain_fwd (ode stream)", (ops, "odetrain_forward")),
+    ("odetrain_bwd", (ops, "odetrain_backward")),
+    ("lyap_step (main)", (ops, "lyap_step")),
+    ("sconv_bwd_rfft2", (ops, "sconv_rfft2")),
+    ("spectral_map_bwd", (ops, "spectral_cayley_backward")),
+    ("adam (main, end)", (torch.optim.Adam, "step")),
+]
+if len(sys.argv) > 1 and sys.argv[1] == "lyap_curve":
+    variants = [("baseline", None)]
+    for us in (10, 30, 60, 120, 200, 300):
+        variants.append((f"lyap spin {us} us", (ops, "lyap_step", us)))
+res = {}
+for name, tgt in variants:
+    if tgt is not None and len(tgt) == 3:
+        SPIN = int(tgt[2] * 1e-3 / MS_PER_CYCLE)
+        tgt = tgt[:2]
+    undo = spin_before(*tgt) if tgt else (lambda: None)
+    try:
+        res[name] = step_ms()
+    finally:
+        undo()
+    print(name, res[name], file=sys.stderr, flush=True)
+print(json.dumps({"spin_us": 200, **res}), flush=True)
