@@ -27,7 +27,7 @@
 namespace {
 
 typedef float2 c32;
-constexpr int NT = 512;
+constexpr int NT = 1024;
 constexpr int BT_F = 16;     // images per forward-transform workgroup
 constexpr int BT_I = 8;      // images per inverse-transform workgroup
 
