@@ -1,0 +1,255 @@
+// Elementwise stages of the dense Cayley map Q = cayley(alpha W / ||W||) (gfx950): the
+// CayleyLinears of the backbone (4096 -> 512 -> 512 -> 10) and of the dynamics (classification.py:
+// 282-293 convert_cayley; fiode_amd/cayley.py _DenseCayleyFn).  The GEMMs of the map stay library
+// GEMMs (hipBLASLt through torch.matmul) and the inverse is fiode_block_inverse / the batched
+// Gauss-Jordan; everything between them -- ~30 PyTorch elementwise / copy / reduction kernels per
+// map forward + backward -- is one kernel per stage here:
+//
+// X = s Wx (Wx = W, or W^T when cin > cout), s = alpha / ||W||, U = X[:k], V = X[k:], k = min(cout, cin),
+// primes denote the unscaled blocks (U', V' of Wx):
+//   prep    M = I + s (U' - U'^T) + s^2 G,                  G = V'^T V'           (GEMM)
+//   finish  Q = [2 inv - I ; -2 s P] in W's orientation,     P = V' inv            (GEMM)
+//   ginv    G_inv = 2 Gt - 2 s A,                            A = V'^T Gb           (GEMM)
+//           (G_M' = inv^T G_inv inv^T by two GEMMs; G_M = -G_M')
+//   h       gU = G_M - G_M^T, H = G_M + G_M^T
+//   gv      gV = s P1 - 2 P2, D partials of <gX, Wx>,        P1 = V' H, P2 = Gb inv^T (GEMMs)
+//   gw      dL/dW = s gX - alpha D / ||W||^3 W, dL/dalpha = D / ||W||  (fixed-order D sum)
+// with the matrices batched over a leading index (the dynamics' three 128 x 10 maps share one
+// launch, per-matrix norms and alphas).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "fiode.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int DPARTS = 64;      // D partial sums per matrix (grid.x of k_dense_gv)
+
+struct DArgs {
+  int cout, cin, k, R, wide;
+  const float* W;       // [b][cout][cin]
+  const float* alpha;   // [b]
+  const float* nrm;     // [b]
+};
+
+__device__ __forceinline__ float wx(const DArgs& a, const float* Wb, int r, int c) {
+  return a.wide ? Wb[(int64_t)c * a.cin + r] : Wb[(int64_t)r * a.cin + c];
+}
+__device__ __forceinline__ int64_t wpos(const DArgs& a, int r, int c) {   // X (r, c) -> W offset
+  return a.wide ? (int64_t)c * a.cin + r : (int64_t)r * a.cin + c;
+}
+
+__global__ void __launch_bounds__(NT) k_dense_prep(DArgs a, const float* __restrict__ G, float* __restrict__ M) {
+  const int b = blockIdx.y, k = a.k;
+  const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
+  const float s = a.alpha[b] / a.nrm[b];
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < k * k; idx += gridDim.x * NT) {
+    const int i = idx / k, j = idx % k;
+    float m = s * (wx(a, Wb, i, j) - wx(a, Wb, j, i));
+    if (G) m = fmaf(s * s, G[(int64_t)b * k * k + idx], m);
+    if (i == j) m += 1.0f;
+    M[(int64_t)b * k * k + idx] = m;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_dense_finish(DArgs a, const float* __restrict__ inv,
+                                                     const float* __restrict__ P, float* __restrict__ Q) {
+  const int b = blockIdx.y, k = a.k;
+  const float s = a.alpha[b] / a.nrm[b];
+  float* Qb = Q + (int64_t)b * a.cout * a.cin;
+  // walk Q in its own (W) layout so the stores are coalesced
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < a.cout * a.cin; idx += gridDim.x * NT) {
+    const int o = idx / a.cin, c = idx % a.cin;
+    const int r = a.wide ? c : o, j = a.wide ? o : c;      // X element (r, j)
+    float q;
+    if (r < k) {
+      q = 2.0f * inv[((int64_t)b * k + r) * k + j];
+      if (r == j) q -= 1.0f;
+    } else {
+      q = -2.0f * s * P[((int64_t)b * (a.R - k) + (r - k)) * k + j];
+    }
+    Qb[idx] = q;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_dense_ginv(DArgs a, const float* __restrict__ Gq, const float* __restrict__ A,
+                                                   float* __restrict__ Ginv) {
+  const int b = blockIdx.y, k = a.k;
+  const float s = a.alpha[b] / a.nrm[b];
+  const float* Gb = Gq + (int64_t)b * a.cout * a.cin;
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < k * k; idx += gridDim.x * NT) {
+    const int i = idx / k, j = idx % k;
+    float g = 2.0f * Gb[wpos(a, i, j)];
+    if (A) g = fmaf(-2.0f * s, A[(int64_t)b * k * k + idx], g);
+    Ginv[(int64_t)b * k * k + idx] = g;
+  }
+}
+
+// GMn = -G_M: gU = G_M - G_M^T -> gX rows < k (X layout [b][R][k]); H = G_M + G_M^T
+__global__ void __launch_bounds__(NT) k_dense_h(DArgs a, const float* __restrict__ GMn, float* __restrict__ gX,
+                                                float* __restrict__ H) {
+  const int b = blockIdx.y, k = a.k;
+  const float* Gm = GMn + (int64_t)b * k * k;
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < k * k; idx += gridDim.x * NT) {
+    const int i = idx / k, j = idx % k;
+    const float g = -Gm[idx], gt = -Gm[(int64_t)j * k + i];
+    gX[((int64_t)b * a.R + i) * k + j] = g - gt;
+    H[(int64_t)b * k * k + idx] = g + gt;
+  }
+}
+
+// gV = s P1 - 2 P2 -> gX rows >= k; D partials of sum gX * Wx over the whole X
+__global__ void __launch_bounds__(NT) k_dense_gv(DArgs a, const float* __restrict__ P1, const float* __restrict__ P2,
+                                                 float* __restrict__ gX, float* __restrict__ dpart) {
+  __shared__ float red[NT / 64];
+  const int b = blockIdx.y, k = a.k, RK = a.R * k;
+  const float s = a.alpha[b] / a.nrm[b];
+  const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
+  float* gXb = gX + (int64_t)b * RK;
+  float d = 0.f;
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < RK; idx += DPARTS * NT) {
+    const int r = idx / k, j = idx % k;
+    float g;
+    if (r < k) {
+      g = gXb[idx];
+    } else {
+      const int64_t pi = ((int64_t)b * (a.R - k) + (r - k)) * k + j;
+      g = s * P1[pi] - 2.0f * P2[pi];
+      gXb[idx] = g;
+    }
+    d = fmaf(g, wx(a, Wb, r, j), d);
+  }
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int q = 0; q < NT / 64; ++q) t += red[q];
+    dpart[b * DPARTS + blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restrict__ gX, const float* __restrict__ dpart,
+                                                 float* __restrict__ gW, float* __restrict__ galpha) {
+  __shared__ float sD;
+  const int b = blockIdx.y, k = a.k;
+  if (threadIdx.x < 64) {                     // fixed-order sum of the D partials
+    float v = threadIdx.x < DPARTS ? dpart[b * DPARTS + threadIdx.x] : 0.f;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (threadIdx.x == 0) sD = v;
+  }
+  __syncthreads();
+  const float D = sD, n = a.nrm[b], al = a.alpha[b];
+  const float s = al / n, cw = al * D / (n * n * n);
+  if (blockIdx.x == 0 && threadIdx.x == 0) galpha[b] = D / n;
+  const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
+  const float* gXb = gX + (int64_t)b * a.R * k;
+  float* gWb = gW + (int64_t)b * a.cout * a.cin;
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < a.cout * a.cin; idx += gridDim.x * NT) {
+    const int o = idx / a.cin, c = idx % a.cin;
+    const int r = a.wide ? c : o, j = a.wide ? o : c;
+    gWb[idx] = s * gXb[(int64_t)r * k + j] - cw * Wb[idx];
+  }
+}
+
+int mk(const fiode_dense_config* cfg, DArgs& a, int& batch) {
+  if (!cfg || cfg->batch < 1 || cfg->cout < 1 || cfg->cin < 1) return FIODE_EINVAL;
+  a = DArgs{};
+  a.cout = cfg->cout;
+  a.cin = cfg->cin;
+  a.wide = a.cin > a.cout;
+  a.k = a.wide ? a.cout : a.cin;
+  a.R = a.wide ? a.cin : a.cout;
+  batch = cfg->batch;
+  return FIODE_OK;
+}
+
+dim3 grid_for(int64_t n, int batch) {
+  int64_t g = (n + NT - 1) / NT;
+  if (g > 1024) g = 1024;
+  return dim3((unsigned)g, (unsigned)batch);
+}
+
+#define DENSE_RET()                                            \
+  do {                                                         \
+    const hipError_t e = hipGetLastError();                    \
+    return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;   \
+  } while (0)
+
+}  // namespace
+
+extern "C" int fiode_dense_cayley_prep(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
+                                       const float* nrm, const float* G, float* M) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!W || !alpha || !nrm || !M || (a.R > a.k && !G)) return FIODE_EINVAL;
+  a.W = W;
+  a.alpha = alpha;
+  a.nrm = nrm;
+  hipLaunchKernelGGL(k_dense_prep, grid_for((int64_t)a.k * a.k, batch), dim3(NT), 0, (hipStream_t)stream, a,
+                     a.R > a.k ? G : nullptr, M);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_cayley_finish(void* stream, const fiode_dense_config* cfg, const float* alpha,
+                                         const float* nrm, const float* inv, const float* P, float* Q) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!alpha || !nrm || !inv || !Q || (a.R > a.k && !P)) return FIODE_EINVAL;
+  a.alpha = alpha;
+  a.nrm = nrm;
+  hipLaunchKernelGGL(k_dense_finish, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, (hipStream_t)stream, a,
+                     inv, P, Q);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_cayley_ginv(void* stream, const fiode_dense_config* cfg, const float* alpha,
+                                       const float* nrm, const float* gQ, const float* A, float* Ginv) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!alpha || !nrm || !gQ || !Ginv || (a.R > a.k && !A)) return FIODE_EINVAL;
+  a.alpha = alpha;
+  a.nrm = nrm;
+  hipLaunchKernelGGL(k_dense_ginv, grid_for((int64_t)a.k * a.k, batch), dim3(NT), 0, (hipStream_t)stream, a, gQ,
+                     a.R > a.k ? A : nullptr, Ginv);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_cayley_h(void* stream, const fiode_dense_config* cfg, const float* GMn, float* gX,
+                                    float* H) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!GMn || !gX || !H) return FIODE_EINVAL;
+  hipLaunchKernelGGL(k_dense_h, grid_for((int64_t)a.k * a.k, batch), dim3(NT), 0, (hipStream_t)stream, a, GMn, gX, H);
+  DENSE_RET();
+}
+
+extern "C" size_t fiode_dense_cayley_workspace_bytes(const fiode_dense_config* cfg) {
+  return cfg && cfg->batch > 0 ? (size_t)cfg->batch * DPARTS * sizeof(float) : 0;
+}
+
+extern "C" int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
+                                       const float* nrm, const float* P1, const float* P2, float* gX, float* gW,
+                                       float* galpha, void* workspace, size_t workspace_bytes) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!W || !alpha || !nrm || !gX || !gW || !galpha || !workspace || (a.R > a.k && (!P1 || !P2)))
+    return FIODE_EINVAL;
+  if (workspace_bytes < fiode_dense_cayley_workspace_bytes(cfg)) return FIODE_EWORKSPACE;
+  a.W = W;
+  a.alpha = alpha;
+  a.nrm = nrm;
+  hipStream_t st = (hipStream_t)stream;
+  float* dpart = (float*)workspace;
+  hipLaunchKernelGGL(k_dense_gv, dim3(DPARTS, batch), dim3(NT), 0, st, a, P1, P2, gX, dpart);
+  hipLaunchKernelGGL(k_dense_gw, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, st, a, (const float*)gX, dpart,
+                     gW, galpha);
+  DENSE_RET();
+}

@@ -82,6 +82,10 @@ class SconvConfig(ct.Structure):
     _fields_ = [("n", ct.c_int32), ("C", ct.c_int32), ("B", ct.c_int32), ("downsample", ct.c_int32)]
 
 
+class DenseConfig(ct.Structure):
+    _fields_ = [("batch", ct.c_int32), ("cout", ct.c_int32), ("cin", ct.c_int32)]
+
+
 class CertifyConfig(ct.Structure):
     _fields_ = [("n_classes", ct.c_int32), ("T", ct.c_int32), ("batches", ct.c_int32), ("label", ct.c_int32),
                 ("eps", ct.c_float), ("min_std", ct.c_float)]
@@ -128,6 +132,13 @@ def _load():
                                              ct.c_int64]),
         "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_block_inverse": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_dense_cayley_prep": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
+        "fiode_dense_cayley_finish": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
+        "fiode_dense_cayley_ginv": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
+        "fiode_dense_cayley_h": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp]),
+        "fiode_dense_cayley_workspace_bytes": (ct.c_size_t, [ct.POINTER(DenseConfig)]),
+        "fiode_dense_cayley_grad": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                               _vp, ct.c_size_t]),
         "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
         "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
         "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),

@@ -12,6 +12,7 @@ and stay in PyTorch: their gradients come from autograd, fed by the fused HIP st
 """
 from __future__ import annotations
 
+import ctypes as ct
 import math
 from typing import Optional
 
@@ -142,9 +143,84 @@ class _CayleyScaledFn(torch.autograd.Function):
         return gW, galpha, None
 
 
+class _DenseCayleyFn(torch.autograd.Function):
+    """cayley(alpha W / ||W||) for a batch of real [cout, cin] matrices (per-matrix norm and alpha):
+    the same forward / analytic backward as _CayleyScaledFn, with the GEMMs as library GEMMs and
+    every elementwise stage between them one HIP kernel (fiode_dense_cayley_*; dense.hip)."""
+
+    @staticmethod
+    def forward(ctx, W, alpha):
+        from . import ops, _lib as L
+        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
+        al = alpha.detach().reshape(-1).contiguous().float()
+        b, cout, cin = Wb.shape
+        wide = cin > cout
+        k = cout if wide else cin
+        nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
+        Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
+        G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
+        cfg = L.DenseConfig(b, cout, cin)
+        lib, st = L.lib(), ops._stream(W.device)
+        M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
+        L.check(lib.fiode_dense_cayley_prep(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
+                                            ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
+        inv = _block_inverse(M)
+        P = torch.matmul(Vp, inv).contiguous() if Vp is not None else None
+        Q = torch.empty_like(Wb)
+        L.check(lib.fiode_dense_cayley_finish(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), inv.data_ptr(),
+                                              ops._ptr(P), Q.data_ptr()), "fiode_dense_cayley_finish")
+        ctx.save_for_backward(Wb, al, nrm, inv)
+        ctx.shapes = (W.shape, alpha.shape)
+        return Q.reshape(W.shape)
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from . import ops, _lib as L
+        Wb, al, nrm, inv = ctx.saved_tensors
+        wshape, ashape = ctx.shapes
+        b, cout, cin = Wb.shape
+        wide = cin > cout
+        k = cout if wide else cin
+        R = max(cout, cin)
+        gQb = gQ.reshape(b, cout, cin).contiguous()
+        cfg = L.DenseConfig(b, cout, cin)
+        lib, st = L.lib(), ops._stream(Wb.device)
+        Vp = Gb = A = None
+        if R > k:
+            Vp = Wb[:, :, k:].mT if wide else Wb[:, k:, :]
+            Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
+            A = torch.matmul(Vp.mT, Gb).contiguous()
+        Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
+        L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
+                                            ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
+        ih = inv.mT
+        GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
+        gX = torch.empty((b, R, k), dtype=torch.float32, device=Wb.device)
+        H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
+        L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
+                "fiode_dense_cayley_h")
+        P1 = torch.matmul(Vp, H).contiguous() if R > k else None
+        P2 = torch.matmul(Gb, ih).contiguous() if R > k else None
+        gW = torch.empty_like(Wb)
+        ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
+        ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,
+                         device=Wb.device)
+        L.check(lib.fiode_dense_cayley_grad(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
+                                            ops._ptr(P1), ops._ptr(P2), gX.data_ptr(), gW.data_ptr(), ga.data_ptr(),
+                                            ws.data_ptr(), ws.numel()), "fiode_dense_cayley_grad")
+        return gW.reshape(wshape), ga.reshape(ashape)
+
+
 def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False) -> torch.Tensor:
-    """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293)."""
+    """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293).
+    Real matrices on ROCm (one matrix, or a batch with per-matrix norms) take the fused stages of
+    _DenseCayleyFn; complex ones and a batch under one norm take _CayleyScaledFn."""
+    if W.is_cuda and W.dtype == torch.float32 and (W.dim() == 2 or per_matrix) and DENSE_FUSED:
+        return _DenseCayleyFn.apply(W, alpha)
     return _CayleyScaledFn.apply(W, alpha, per_matrix)
+
+
+DENSE_FUSED = True
 
 
 def cayley(W: torch.Tensor) -> torch.Tensor:

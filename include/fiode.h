@@ -254,6 +254,24 @@ FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                   size_t workspace_bytes);
 
+/* ---- dense Cayley map stages (CayleyLinear; classification.py:282-293 convert_cayley): the
+ * elementwise steps between the library GEMMs and the inverse of Q = cayley(alpha W / ||W||) for a
+ * batch of [cout][cin] matrices with per-matrix alpha [b] and ||W|| [b] (see dense.hip). */
+typedef struct fiode_dense_config {
+  int32_t batch, cout, cin;
+} fiode_dense_config;
+FIODE_API int fiode_dense_cayley_prep(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
+                                      const float* nrm, const float* G, float* M);
+FIODE_API int fiode_dense_cayley_finish(void* stream, const fiode_dense_config* cfg, const float* alpha,
+                                        const float* nrm, const float* inv, const float* P, float* Q);
+FIODE_API int fiode_dense_cayley_ginv(void* stream, const fiode_dense_config* cfg, const float* alpha,
+                                      const float* nrm, const float* gQ, const float* A, float* Ginv);
+FIODE_API int fiode_dense_cayley_h(void* stream, const fiode_dense_config* cfg, const float* GMn, float* gX, float* H);
+FIODE_API size_t fiode_dense_cayley_workspace_bytes(const fiode_dense_config* cfg);
+FIODE_API int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
+                                      const float* nrm, const float* P1, const float* P2, float* gX, float* gW,
+                                      float* galpha, void* workspace, size_t workspace_bytes);
+
 /* ---- spectral convolution transforms on spatial-major activations [n][n][C][B] (CayleyConv
  * forward_hwcb; fiode_amd/cayley.py).  Spectrum layout [f][C][B] complex64, f = ka (n/2+1) + kb. */
 typedef struct fiode_sconv_config {

@@ -363,3 +363,24 @@ def test_sconv_rejects_bad_shapes():
         ops.sconv_irfft2(torch.zeros(8 * 5, 6, 4, dtype=torch.complex64, device=dev), 8, 6, 4, downsample=True)
     with pytest.raises(ValueError):
         ops.sconv_irfft2(torch.zeros(8 * 5, 6, 3, dtype=torch.complex64, device=dev), 8, 6, 4)   # wrong B
+
+
+@pytest.mark.parametrize("shape,per_matrix", [((512, 4096), False), ((4096, 512), False), ((512, 512), False),
+                                              ((3, 128, 10), True)])
+def test_dense_cayley_fused_matches_op_by_op(shape, per_matrix):
+    """_DenseCayleyFn (dense.hip stages + library GEMMs) = _CayleyScaledFn (torch ops) in float32."""
+    from fiode_amd.cayley import _CayleyScaledFn, _DenseCayleyFn
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    W = torch.randn(shape, generator=g).to(dev)
+    nb = shape[0] if per_matrix else 1
+    alpha = (torch.rand(nb, generator=g) * 3 + 0.5).to(dev)
+    G = torch.randn(shape, generator=g).to(dev)
+    out = []
+    for fn in (lambda w, a: _DenseCayleyFn.apply(w, a), lambda w, a: _CayleyScaledFn.apply(w, a, per_matrix)):
+        Wa, aa = W.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+        Q = fn(Wa, aa)
+        (Q * G).sum().backward()
+        out.append((Q.detach(), Wa.grad, aa.grad))
+    for a, b in zip(*out):
+        assert float((a - b).abs().max()) <= 1e-4 * (float(b.abs().max()) + 1e-6)

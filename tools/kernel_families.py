@@ -1,11 +1,12 @@
 """Group a rocprofv3 kernel_stats.csv by kernel family (not a test)."""
 import csv, re, sys
 from collections import defaultdict
-rows = list(csv.DictReader(open(sys.argv[1])))
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "spin_kernel" not in r["Name"]]
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 fam = defaultdict(lambda: [0.0, 0])
 def family(n):
-    for k in ("k_lyap", "k_static_proj", "k_ot_", "k_inv_gj", "k_cert", "k_ode", "k_dyn", "k_qp"):
+    for k in ("k_lyap", "k_static_proj", "k_ot_", "k_inv_gj", "k_cert", "k_ode", "k_dyn", "k_qp", "k_spec_",
+              "k_panel_", "k_sconv_", "k_groupsort"):
         if k in n:
             return k
     if n.startswith("Cijk") or "gemm" in n.lower():
