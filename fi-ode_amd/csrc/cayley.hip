@@ -102,7 +102,8 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
   __shared__ float sB[PB][PB + 4];      // X_Kj, then R_Kj
   const int ib = blockIdx.x * PB, jb = blockIdx.y * PB, tid = threadIdx.x;
   const bool piv_r = ib == k0, piv_c = jb == k0;
-  for (int idx = tid; idx < PB * PB; idx += 256) {
+#pragma unroll 16
+  for (int idx = tid; idx < PB * PB; idx += 256) {     // 16 trips: all loads in flight together
     const int r = idx / PB, c = idx % PB;
     sP[r][c] = P[idx];
     sA[r][c] = X[(int64_t)(ib + r) * np + k0 + c];

@@ -14,6 +14,9 @@
 //   h       gU = G_M - G_M^T, H = G_M + G_M^T
 //   gv      gV = s P1 - 2 P2, D partials of <gX, Wx>,        P1 = V' H, P2 = Gb inv^T (GEMMs)
 //   gw      dL/dW = s gX - alpha D / ||W||^3 W, dL/dalpha = D / ||W||  (fixed-order D sum)
+// Every [R-k] x k block (P, P1, P2) and gX are passed in W's layout -- for a wide W (cin > cout)
+// that is the transposed block, [k][R-k] (the host forms it with the GEMM operands swapped) --
+// so every stage streams W-layout rows: no strided gathers over the 4096 x 512 matrices.
 // with the matrices batched over a leading index (the dynamics' three 128 x 10 maps share one
 // launch, per-matrix norms and alphas).
 #include <hip/hip_runtime.h>
@@ -25,7 +28,7 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int DPARTS = 64;      // D partial sums per matrix (grid.x of k_dense_gv)
+constexpr int DPARTS = 256;     // D partial sums per matrix (grid.x of k_dense_gv)
 
 struct DArgs {
   int cout, cin, k, R, wide;
@@ -68,7 +71,7 @@ __global__ void __launch_bounds__(NT) k_dense_finish(DArgs a, const float* __res
       q = 2.0f * inv[((int64_t)b * k + r) * k + j];
       if (r == j) q -= 1.0f;
     } else {
-      q = -2.0f * s * P[((int64_t)b * (a.R - k) + (r - k)) * k + j];
+      q = -2.0f * s * P[(int64_t)b * (a.R - k) * k + (a.wide ? (int64_t)j * (a.R - k) + (r - k) : (int64_t)(r - k) * k + j)];
     }
     Qb[idx] = q;
   }
@@ -87,7 +90,7 @@ __global__ void __launch_bounds__(NT) k_dense_ginv(DArgs a, const float* __restr
   }
 }
 
-// GMn = -G_M: gU = G_M - G_M^T -> gX rows < k (X layout [b][R][k]); H = G_M + G_M^T
+// GMn = -G_M: gU = G_M - G_M^T -> gX (W layout); H = G_M + G_M^T
 __global__ void __launch_bounds__(NT) k_dense_h(DArgs a, const float* __restrict__ GMn, float* __restrict__ gX,
                                                 float* __restrict__ H) {
   const int b = blockIdx.y, k = a.k;
@@ -95,31 +98,35 @@ __global__ void __launch_bounds__(NT) k_dense_h(DArgs a, const float* __restrict
   for (int idx = blockIdx.x * NT + threadIdx.x; idx < k * k; idx += gridDim.x * NT) {
     const int i = idx / k, j = idx % k;
     const float g = -Gm[idx], gt = -Gm[(int64_t)j * k + i];
-    gX[((int64_t)b * a.R + i) * k + j] = g - gt;
+    gX[(int64_t)b * a.cout * a.cin + wpos(a, i, j)] = g - gt;
     H[(int64_t)b * k * k + idx] = g + gt;
   }
 }
 
-// gV = s P1 - 2 P2 -> gX rows >= k; D partials of sum gX * Wx over the whole X
+// gV = s P1 - 2 P2 -> gX (W layout); D partials of sum gX * W over the whole matrix
 __global__ void __launch_bounds__(NT) k_dense_gv(DArgs a, const float* __restrict__ P1, const float* __restrict__ P2,
                                                  float* __restrict__ gX, float* __restrict__ dpart) {
   __shared__ float red[NT / 64];
-  const int b = blockIdx.y, k = a.k, RK = a.R * k;
+  const int b = blockIdx.y, k = a.k, n = a.cout * a.cin, RV = a.R - k;
   const float s = a.alpha[b] / a.nrm[b];
-  const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
-  float* gXb = gX + (int64_t)b * RK;
+  const float* Wb = a.W + (int64_t)b * n;
+  const float* P1b = P1 ? P1 + (int64_t)b * RV * k : nullptr;
+  const float* P2b = P2 ? P2 + (int64_t)b * RV * k : nullptr;
+  float* gXb = gX + (int64_t)b * n;
   float d = 0.f;
-  for (int idx = blockIdx.x * NT + threadIdx.x; idx < RK; idx += DPARTS * NT) {
-    const int r = idx / k, j = idx % k;
+#pragma unroll 4
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < n; idx += DPARTS * NT) {
+    const int o = idx / a.cin, c = idx % a.cin;
+    const int r = a.wide ? c : o;
     float g;
     if (r < k) {
       g = gXb[idx];
-    } else {
-      const int64_t pi = ((int64_t)b * (a.R - k) + (r - k)) * k + j;
-      g = s * P1[pi] - 2.0f * P2[pi];
+    } else {                                  // P blocks in W layout: wide [k][RV] (o, c-k), tall [RV][k] (o-k, c)
+      const int64_t pi = a.wide ? (int64_t)o * RV + (c - k) : (int64_t)(o - k) * k + c;
+      g = s * P1b[pi] - 2.0f * P2b[pi];
       gXb[idx] = g;
     }
-    d = fmaf(g, wx(a, Wb, r, j), d);
+    d = fmaf(g, Wb[idx], d);
   }
   for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
@@ -134,9 +141,11 @@ __global__ void __launch_bounds__(NT) k_dense_gv(DArgs a, const float* __restric
 __global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restrict__ gX, const float* __restrict__ dpart,
                                                  float* __restrict__ gW, float* __restrict__ galpha) {
   __shared__ float sD;
-  const int b = blockIdx.y, k = a.k;
+  const int b = blockIdx.y;
   if (threadIdx.x < 64) {                     // fixed-order sum of the D partials
-    float v = threadIdx.x < DPARTS ? dpart[b * DPARTS + threadIdx.x] : 0.f;
+    float v = 0.f;
+#pragma unroll
+    for (int q = threadIdx.x; q < DPARTS; q += 64) v += dpart[b * DPARTS + q];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (threadIdx.x == 0) sD = v;
   }
@@ -145,13 +154,10 @@ __global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restric
   const float s = al / n, cw = al * D / (n * n * n);
   if (blockIdx.x == 0 && threadIdx.x == 0) galpha[b] = D / n;
   const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
-  const float* gXb = gX + (int64_t)b * a.R * k;
+  const float* gXb = gX + (int64_t)b * a.cout * a.cin;
   float* gWb = gW + (int64_t)b * a.cout * a.cin;
-  for (int idx = blockIdx.x * NT + threadIdx.x; idx < a.cout * a.cin; idx += gridDim.x * NT) {
-    const int o = idx / a.cin, c = idx % a.cin;
-    const int r = a.wide ? c : o, j = a.wide ? o : c;
-    gWb[idx] = s * gXb[(int64_t)r * k + j] - cw * Wb[idx];
-  }
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < a.cout * a.cin; idx += gridDim.x * NT)
+    gWb[idx] = s * gXb[idx] - cw * Wb[idx];
 }
 
 int mk(const fiode_dense_config* cfg, DArgs& a, int& batch) {

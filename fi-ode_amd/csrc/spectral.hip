@@ -85,7 +85,8 @@ __device__ __forceinline__ c32 root(int m, int n) {
 __device__ __forceinline__ float block_sum_fixed(const float* __restrict__ p, int n, float* slot) {
   if (threadIdx.x < 64) {
     float v = 0.f;
-    for (int i = threadIdx.x; i < n; i += 64) v += p[i];
+#pragma unroll 8
+    for (int i = threadIdx.x; i < n; i += 64) v += p[i];     // loads of 8 trips in flight
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (threadIdx.x == 0) *slot = v;
   }
@@ -640,6 +641,7 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
     g[t] = 0.f;
   }
   if (pair < npair) {
+#pragma unroll 4
     for (int f = fg; f < a.nf; f += TAPS_FG) {
       const int ka = f / a.half, kb = f - ka * a.half;
       c32 e[TAPS];

@@ -165,7 +165,10 @@ class _DenseCayleyFn(torch.autograd.Function):
         L.check(lib.fiode_dense_cayley_prep(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
                                             ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
         inv = _block_inverse(M)
-        P = torch.matmul(Vp, inv).contiguous() if Vp is not None else None
+        P = None                    # V' inv in W's layout (wide: its transpose inv^T V'^T = inv^T W[:, k:])
+        if Vp is not None:
+            P = torch.matmul(inv.mT, Wb[:, :, k:]) if wide else torch.matmul(Vp, inv)
+            P = P.contiguous()
         Q = torch.empty_like(Wb)
         L.check(lib.fiode_dense_cayley_finish(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), inv.data_ptr(),
                                               ops._ptr(P), Q.data_ptr()), "fiode_dense_cayley_finish")
@@ -195,12 +198,18 @@ class _DenseCayleyFn(torch.autograd.Function):
                                             ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
         ih = inv.mT
         GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
-        gX = torch.empty((b, R, k), dtype=torch.float32, device=Wb.device)
+        gX = torch.empty_like(Wb)                    # W layout
         H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
         L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
                 "fiode_dense_cayley_h")
-        P1 = torch.matmul(Vp, H).contiguous() if R > k else None
-        P2 = torch.matmul(Gb, ih).contiguous() if R > k else None
+        P1 = P2 = None                  # V' H and Gb inv^T in W's layout (wide: H^T W[:, k:], inv gQ[:, k:])
+        if R > k:
+            if wide:
+                P1 = torch.matmul(H.mT, Wb[:, :, k:]).contiguous()
+                P2 = torch.matmul(inv, gQb[:, :, k:]).contiguous()
+            else:
+                P1 = torch.matmul(Vp, H).contiguous()
+                P2 = torch.matmul(Gb, ih).contiguous()
         gW = torch.empty_like(Wb)
         ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
         ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,

@@ -256,7 +256,8 @@ FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, floa
 
 /* ---- dense Cayley map stages (CayleyLinear; classification.py:282-293 convert_cayley): the
  * elementwise steps between the library GEMMs and the inverse of Q = cayley(alpha W / ||W||) for a
- * batch of [cout][cin] matrices with per-matrix alpha [b] and ||W|| [b] (see dense.hip). */
+ * batch of [cout][cin] matrices with per-matrix alpha [b] and ||W|| [b] (see dense.hip).  The
+ * [R-k] x k blocks P, P1, P2 and gX are in W's layout (wide W: [k][R-k]). */
 typedef struct fiode_dense_config {
   int32_t batch, cout, cin;
 } fiode_dense_config;
