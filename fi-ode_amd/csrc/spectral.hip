@@ -495,16 +495,17 @@ __global__ void __launch_bounds__(TL * TL) k_spec_qbot(SpecArgs a) {
   c32 acc = make_float2(0.f, 0.f);
   for (int k0 = 0; k0 < a.K; k0 += KP) {
     __syncthreads();
+    const int kc = min(KP, a.K - k0);               // K = 32: one half-filled panel
     for (int idx = tid; idx < TL * KP; idx += TL * TL) {
       const int q = idx / KP, k = idx % KP;
       const int rr = a.K + tr * TL + q;
-      Vt[q][k] = rr < a.R ? xs(a, f, rr, k0 + k, sc) : make_float2(0.f, 0.f);
+      Vt[q][k] = (rr < a.R && k < kc) ? xs(a, f, rr, k0 + k, sc) : make_float2(0.f, 0.f);
       const int kk = idx / TL, c = idx % TL;
-      It[kk][c] = a.inv[((int64_t)f * a.K + k0 + kk) * a.K + tc * TL + c];
+      It[kk][c] = kk < kc ? a.inv[((int64_t)f * a.K + k0 + kk) * a.K + tc * TL + c] : make_float2(0.f, 0.f);
     }
     __syncthreads();
 #pragma unroll 8
-    for (int k = 0; k < KP; ++k) acc = cfma(Vt[lr][k], It[k][lc], acc);
+    for (int k = 0; k < kc; ++k) acc = cfma(Vt[lr][k], It[k][lc], acc);
   }
   if (r < a.R) {
     c32* Qf = a.Q + (int64_t)f * a.cout * a.cin;
@@ -549,21 +550,23 @@ __global__ void __launch_bounds__(TL * TL) k_spec_kk(SpecArgs a, const c32* __re
   c32 acc = make_float2(0.f, 0.f);
   for (int k0 = 0; k0 < K; k0 += KP) {
     __syncthreads();
+    const int kc = min(KP, K - k0);
     for (int idx = tid; idx < TL * KP; idx += TL * TL) {
       const int q = idx / KP, k = idx % KP;          // left operand row q, col k0 + k
       const int kk = idx / TL, c = idx % TL;         // right operand row k0 + kk, col c
       const int gi = ti * TL + q, gj = tj * TL + c;
+      const c32 zero = make_float2(0.f, 0.f);
       if (LEFT) {   // M^-H (gi, k) = conj(inv[k][gi]);  A (k, gj)
-        Pa[q][k] = cconj(If[(int64_t)(k0 + k) * K + gi]);
-        Pb[kk][c] = Af[(int64_t)(k0 + kk) * K + gj];
+        Pa[q][k] = k < kc ? cconj(If[(int64_t)(k0 + k) * K + gi]) : zero;
+        Pb[kk][c] = kk < kc ? Af[(int64_t)(k0 + kk) * K + gj] : zero;
       } else {      // A (gi, k);  M^-H (k, gj) = conj(inv[gj][k])
-        Pa[q][k] = Af[(int64_t)gi * K + k0 + k];
-        Pb[kk][c] = cconj(If[(int64_t)gj * K + k0 + kk]);
+        Pa[q][k] = k < kc ? Af[(int64_t)gi * K + k0 + k] : zero;
+        Pb[kk][c] = kk < kc ? cconj(If[(int64_t)gj * K + k0 + kk]) : zero;
       }
     }
     __syncthreads();
 #pragma unroll 8
-    for (int k = 0; k < KP; ++k) acc = cfma(Pa[li][k], Pb[k][lj], acc);
+    for (int k = 0; k < kc; ++k) acc = cfma(Pa[li][k], Pb[k][lj], acc);
   }
   dst[((int64_t)f * K + ti * TL + li) * K + tj * TL + lj] = cscale(acc, s);
 }
@@ -586,18 +589,20 @@ __global__ void __launch_bounds__(TL * TL) k_spec_gv(SpecArgs a) {
   } else {
     for (int k0 = 0; k0 < K; k0 += KP) {
       __syncthreads();
+      const int kc = min(KP, K - k0);
       for (int idx = tid; idx < TL * KP; idx += TL * TL) {
         const int q = idx / KP, k = idx % KP;
         const int rr = tr * TL + q;
-        Vt[q][k] = rr < a.R ? xs(a, f, rr, k0 + k, sc) : make_float2(0.f, 0.f);
-        Gt_[q][k] = rr < a.R ? gq(a, f, rr, k0 + k) : make_float2(0.f, 0.f);
+        const c32 zero = make_float2(0.f, 0.f);
+        Vt[q][k] = (rr < a.R && k < kc) ? xs(a, f, rr, k0 + k, sc) : zero;
+        Gt_[q][k] = (rr < a.R && k < kc) ? gq(a, f, rr, k0 + k) : zero;
         const int kk = idx / TL, c = idx % TL, gk = k0 + kk, gj = tc * TL + c;
-        Ht[kk][c] = cadd(GM[(int64_t)gk * K + gj], cconj(GM[(int64_t)gj * K + gk]));
-        It[kk][c] = cconj(If[(int64_t)gj * K + gk]);
+        Ht[kk][c] = kk < kc ? cadd(GM[(int64_t)gk * K + gj], cconj(GM[(int64_t)gj * K + gk])) : zero;
+        It[kk][c] = kk < kc ? cconj(If[(int64_t)gj * K + gk]) : zero;
       }
       __syncthreads();
 #pragma unroll 4
-      for (int k = 0; k < KP; ++k) out = cfma(Vt[lr][k], Ht[k][lc], cfma(cscale(Gt_[lr][k], -2.0f), It[k][lc], out));
+      for (int k = 0; k < kc; ++k) out = cfma(Vt[lr][k], Ht[k][lc], cfma(cscale(Gt_[lr][k], -2.0f), It[k][lc], out));
     }
   }
   float d = 0.f;
@@ -700,10 +705,9 @@ int make_plan(const fiode_spectral_config* cfg, Plan& p) {
   if (lds_f + 8192 > 163840 || lds_b > 163840) return FIODE_ESHAPE;
   a.nparts = ((a.R * a.K + NORM_THREADS - 1) / NORM_THREADS) * ((a.nf + DFT_FG - 1) / DFT_FG);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  p.split = a.K > 32;
-  if (p.split && a.K % TL) return FIODE_ESHAPE;
+  p.split = a.K >= 32 && a.K % TL == 0 && a.R % TL == 0;
+  if (a.K > 32 && !p.split) return FIODE_ESHAPE;
   a.ndpart = p.split ? a.nf * (a.R / TL) * (a.K / TL) : a.nf;
-  if (p.split && a.R % TL) return FIODE_ESHAPE;
   const size_t kk = p.split ? (size_t)a.nf * a.K * a.K * sizeof(c32) : 0;
   p.ws_part = 0;
   p.ws_dpart = al((size_t)a.nparts * 4);
@@ -750,12 +754,13 @@ extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_
   hipLaunchKernelGGL(k_spec_dft, dim3((a.R * a.K + NORM_THREADS - 1) / NORM_THREADS, (a.nf + DFT_FG - 1) / DFT_FG),
                      dim3(NORM_THREADS), 0, st, a);
   const size_t lds = (size_t)a.R * a.K * sizeof(c32);
-  if (a.K <= 16) hipLaunchKernelGGL((k_spec_fwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
-  else if (a.K <= 32) hipLaunchKernelGGL((k_spec_fwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
+  if (!p.split && a.K <= 16) hipLaunchKernelGGL((k_spec_fwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
+  else if (!p.split) hipLaunchKernelGGL((k_spec_fwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
   else {
     const int nt = a.K / TL;
     hipLaunchKernelGGL(k_spec_gram, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
-    hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
+    if (a.K <= 32) hipLaunchKernelGGL((k_spec_inv<32, 2, 2, 256>), dim3(a.nf), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
     if (a.R > a.K) hipLaunchKernelGGL(k_spec_qbot, dim3(a.nf, ((a.R - a.K) / TL) * nt), dim3(TL * TL), 0, st, a);
   }
   const hipError_t e = hipGetLastError();
@@ -781,8 +786,8 @@ extern "C" int fiode_spectral_cayley_backward(void* stream, const fiode_spectral
   a.galpha = grad_alpha;
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)(a.R + a.K) * a.K * sizeof(c32);
-  if (a.K <= 16) hipLaunchKernelGGL((k_spec_bwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
-  else if (a.K <= 32) hipLaunchKernelGGL((k_spec_bwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
+  if (!p.split && a.K <= 16) hipLaunchKernelGGL((k_spec_bwd<16, 2, 2, 64>), dim3(a.nf), dim3(64), lds, st, a);
+  else if (!p.split) hipLaunchKernelGGL((k_spec_bwd<32, 2, 2, 256>), dim3(a.nf), dim3(256), lds, st, a);
   else {
     const int nt = a.K / TL;
     hipLaunchKernelGGL(k_spec_ginv, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
