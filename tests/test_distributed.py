@@ -16,11 +16,21 @@ def _free_port():
     return p
 
 
+def _by_value(obj):
+    """Tensors cross the queue as numpy copies: a shared-memory tensor handle would need the
+    worker alive until the parent unpickles it (EOFError when the worker exits first)."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu().numpy().copy()
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_by_value(o) for o in obj)
+    return obj
+
+
 def _worker(rank, world, port, fn, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, fn(rank, world)))
+        q.put((rank, _by_value(fn(rank, world))))
     except Exception as e:  # pragma: no cover - surfaced by the parent
         q.put((rank, e))
     finally:
@@ -64,11 +74,12 @@ def test_grad_allreduce_mean_two_ranks():
     out = _run(_grad_case)
     (p0, l0, g0, alias0), (p1, l1, g1, alias1) = out[0], out[1]
     assert alias0 and alias1
+    T = torch.from_numpy
     for a, b in zip(p0, p1):
-        assert torch.equal(a, b)
+        assert torch.equal(T(a), T(b))
     for a, b, la, lb in zip(g0, g1, l0, l1):
-        assert torch.equal(a, b)
-        torch.testing.assert_close(a, (la + lb) / 2)
+        assert torch.equal(T(a), T(b))
+        torch.testing.assert_close(T(a), (T(la) + T(lb)) / 2)
 
 
 def _metric_case(rank, world):
