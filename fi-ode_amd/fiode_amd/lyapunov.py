@@ -188,6 +188,17 @@ class LyapunovLearning(nn.Module):
         return loss
 
     # Lightning-like surface -------------------------------------------------------------------
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location=None, strict: bool = True, **kwargs):
+        """LightningModule.load_from_checkpoint as the reference calls it (utils.py:14-28,
+        robustness/eval_utils.py:92-107): build from the config kwargs, load ``state_dict``
+        (torch.load(weights_only=True)), keep epoch / global_step of the file."""
+        from .checkpoint import load_from_checkpoint
+        mod = cls(**kwargs)
+        info = load_from_checkpoint(mod, checkpoint_path, strict=strict, map_location=map_location)
+        mod.loaded_checkpoint = info
+        return mod
+
     def log(self, name, value, **kw):
         self.logged[name] = value
 
