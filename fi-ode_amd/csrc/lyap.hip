@@ -84,10 +84,14 @@ __device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C])
     return;
   }
   const int b = row / a.S, s = row - b * a.S;
-  if (a.sampler == FIODE_SAMPLER_COMPOSITE) {
+  if (a.sampler == FIODE_SAMPLER_COMPOSITE || a.sampler == FIODE_SAMPLER_TRAJECTORY) {
     if (s < a.S1) {                      // UniformSimplexSampling, shared over the batch (sampler.py:209-210)
       draws10(a.rng, (uint32_t)s, RNG_STREAM_UNIFORM, h);
       l1_normalize(h);
+    } else if (a.sampler == FIODE_SAMPLER_TRAJECTORY) {
+      // TrajectorySampler (sampler.py:156-166): the solve's states at linspace(0, t_max, S - S1),
+      // given as [B][S - S1][C] (the per-image trajectory, transpose(0, 1) of odeint's output)
+      load_row10(a.h_in + ((size_t)b * (a.S - a.S1) + (s - a.S1)) * C, h);
     } else {                             // CorrectConeSampling (sampler.py:113-128)
       draws10(a.rng, (uint32_t)row, RNG_STREAM_CONE, h);
       l1_normalize(h);
@@ -557,9 +561,10 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   const int B = cfg->batch, S = cfg->sample_size;
   if (B <= 0 || S <= 0 || (long long)B * S > (1LL << 30)) return FIODE_EINVAL;
   if (cfg->n_uniform < 0 || cfg->n_uniform > S) return FIODE_EINVAL;
-  if (cfg->sampler < 0 || cfg->sampler > 2 || cfg->dropout_mode < 0 || cfg->dropout_mode > 2) return FIODE_EINVAL;
+  if (cfg->sampler < 0 || cfg->sampler > 3 || cfg->dropout_mode < 0 || cfg->dropout_mode > 2) return FIODE_EINVAL;
   if (!io->x_feat || !io->y || !io->scalars) return FIODE_EINVAL;
   if (cfg->sampler == FIODE_SAMPLER_GIVEN && !io->h) return FIODE_EINVAL;
+  if (cfg->sampler == FIODE_SAMPLER_TRAJECTORY && cfg->n_uniform < S && !io->h) return FIODE_EINVAL;
   if (cfg->dropout_mode == FIODE_DROPOUT_GIVEN && !io->masks) return FIODE_EINVAL;
   if (!w->Q1 || !w->b1 || !w->Qx || !w->bx || !w->Q2 || !w->b2 || !w->Q3 || !w->b3) return FIODE_EINVAL;
   if (!grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||

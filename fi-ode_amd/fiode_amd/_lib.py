@@ -12,7 +12,7 @@ import pathlib
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("FIODE_LIB", _HERE / "libfiode.so"))
 
-FIODE_SAMPLER_GIVEN, FIODE_SAMPLER_COMPOSITE, FIODE_SAMPLER_DECISION_BOUNDARY = 0, 1, 2
+FIODE_SAMPLER_GIVEN, FIODE_SAMPLER_COMPOSITE, FIODE_SAMPLER_DECISION_BOUNDARY, FIODE_SAMPLER_TRAJECTORY = 0, 1, 2, 3
 FIODE_DROPOUT_OFF, FIODE_DROPOUT_GIVEN, FIODE_DROPOUT_PHILOX = 0, 1, 2
 
 class FiodeLibraryError(RuntimeError):

@@ -25,7 +25,7 @@ from . import ops
 from .dynamics import OrthoClassDynProjectSimplexLips
 from .models import IVP, DefaultOutputFun
 from .odeint import make_solver_params
-from .sampling import CompositeSampler, CompositeSamplerScheduler
+from .sampling import CompositeSampler, CompositeSamplerScheduler, TrajectorySampler
 
 
 class LyapunovLossFn(torch.autograd.Function):
@@ -244,7 +244,7 @@ class LyapunovLearning(nn.Module):
         return dyn.kappa
 
     def step_plan(self, y: torch.Tensor, h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None,
-                  debug: bool = False) -> dict:
+                  debug: bool = False, static_state: Optional[torch.Tensor] = None) -> dict:
         mix = self.sampler_scheduler.get_mixer_coefficients(self.current_epoch)
         for i, m in enumerate(mix):
             self.log(f"mixing_weight_{i}", float(m))
@@ -254,6 +254,10 @@ class LyapunovLearning(nn.Module):
             drop = L.FIODE_DROPOUT_GIVEN
         if h is not None:
             kind = L.FIODE_SAMPLER_GIVEN
+        elif kind == L.FIODE_SAMPLER_TRAJECTORY and s1 < self.h_sample_size:
+            # TrajectorySampler rows (sampler.py:156-166): the solve's states, computed before the step
+            traj = next(t for t in self.sampler.samplers if isinstance(t, TrajectorySampler))
+            h = traj.trajectory(self, static_state, self.h_sample_size - s1)
         plan = dict(dyn=self.dyn_fun.dyn_cfg(), S=self.h_sample_size, S1=s1, sampler=kind, dropout_mode=drop,
                     kappa=self.current_kappa(), seed=self.seed,
                     offset=self._rng_offset if self.rng_counter is None else 0, h=h, masks=masks,
@@ -286,7 +290,7 @@ class LyapunovLearning(nn.Module):
         if self.parallel_cayley and self.training and x.is_cuda and self.dyn_fun.cayley:
             self._prefetch_weights(x.device)
         static_state, _ = self.init_coordinates(x, self.dyn_fun)
-        plan = self.step_plan(y, h=h, masks=masks, debug=debug)
+        plan = self.step_plan(y, h=h, masks=masks, debug=debug, static_state=static_state)
         w = self.dyn_fun.effective_weights()
         ode_on = self.train_ode and self.current_epoch > self.train_ode_epoch
         if ode_on:        # launched first: on ROCm it runs on a side stream beside the fan-out kernels

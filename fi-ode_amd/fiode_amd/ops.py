@@ -97,6 +97,10 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
         if h is None:
             raise ValueError("sampler GIVEN needs h")
         h = _need(h, "h", (N, C), torch.float32, dev)
+    if sampler == L.FIODE_SAMPLER_TRAJECTORY and n_uniform < S:
+        if h is None:
+            raise ValueError("sampler TRAJECTORY needs the trajectory rows h [B, S - n_uniform, C]")
+        h = _need(h, "h", (B, S - n_uniform, C), torch.float32, dev)
     if dropout_mode == L.FIODE_DROPOUT_GIVEN:
         if masks is None:
             raise ValueError("dropout GIVEN needs masks")

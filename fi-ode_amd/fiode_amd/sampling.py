@@ -3,8 +3,8 @@
 The schedulers are host-side float64 scalar logic, restated exactly (they decide the per-step
 S1/S2 split).  The samplers are descriptors: the fused Lyapunov step draws the samples itself
 (in-kernel Philox, ``k_lyap_prep``), so ``CompositeSampler.kernel_plan`` turns the mixer into the
-kernel's (sampler kind, n_uniform).  ``CompositeSampler.forward`` keeps the reference signature
-for callers that want the samples as a tensor (it runs the same kernel with debug output).
+kernel's (sampler kind, n_uniform).  ``TrajectorySampler`` rows come from the HIP ODE solve and
+reach the kernel as a [B, S - n_uniform, C] input (sampler kind TRAJECTORY).
 """
 from __future__ import annotations
 
@@ -95,6 +95,87 @@ class DecisionBoundarySampling(AbstractSampler):
     """Rows on the label's decision boundary (sampler.py:130-153)."""
 
 
+class TrajectorySampler(AbstractSampler):
+    """States along the ODE solve (sampler.py:156-166): ``model.model(x, ts=linspace(0, t_max, n),
+    int_params=train_solver_params, return_traj=True)`` under no_grad, transposed to [B, n, C].
+
+    The solve runs on libfiode: in eval mode (or dropout 0) the HIP stepper ``fiode_odeint``
+    (rk4 / dopri5 dense output at the n times); in train mode with the fixed-grid rk4 solver, the
+    train-mode solve ``fiode_odetrain_forward`` (fresh Philox dropout masks per f-eval, as the
+    reference's dropout draws fresh masks per call), whose saved stage-1 inputs are the grid states,
+    then torchdiffeq's FixedGridODESolver linear interpolation to the n output times.  A train-mode
+    adaptive solve with dropout is not fused and raises."""
+
+    TRAJ_SEED_SALT = 0x7A5C_3E11       # decorrelates its dropout masks from the train_ode solve's
+
+    def trajectory(self, module, static_state: torch.Tensor, n: int) -> torch.Tensor:
+        from . import ops
+        from .odeint import _rk4_grid
+        dyn = module.dyn_fun
+        dev = static_state.device
+        B = static_state.shape[0]
+        h0 = module.init_coordinates.h0_0[None].expand(B, -1).float().contiguous()
+        x = static_state.detach().float().contiguous()
+        params = module.train_solver_params
+        ts = torch.linspace(0.0, float(module.t_max), n)            # float32, as the reference builds it
+        with torch.no_grad():
+            w = {k: v.detach().float().contiguous() for k, v in dyn.effective_weights().items()}
+            if not (dyn.training and dyn.dropout.p > 0):
+                sol, _, _ = ops.odeint_dyn(x, h0, ts.to(dev, torch.float64), w, dyn.dyn_cfg(),
+                                           method=params["method"], rtol=float(params.get("rtol", 1e-7)),
+                                           atol=float(params.get("atol", 1e-9)),
+                                           step_size=params.get("options", {}).get("step_size"))
+                return sol.transpose(0, 1).contiguous()
+            if params["method"] != "rk4":
+                raise NotImplementedError("TrajectorySampler in train mode with dropout needs the fixed-grid rk4 "
+                                          "train solver (the HIP train-mode solve); adaptive + dropout is not fused")
+            step = float(params["options"]["step_size"])
+            cfg = ops.odetrain_config(B, 0.0, float(module.t_max), step, L.FIODE_DROPOUT_PHILOX,
+                                      seed=(module.seed ^ self.TRAJ_SEED_SALT),
+                                      offset=module._rng_offset if module.rng_counter is None else 0)
+            y1, _, ws = ops.odetrain_forward(x, h0, w, dyn.dyn_cfg(), cfg, offset_dev=module.rng_counter)
+            saved = ops.odetrain_saved(ws, cfg)
+            grid_states = torch.cat([saved["h"][:, 0::4], y1[:, None]], dim=1)       # [B, niters, C]
+            grid = _rk4_grid(ts[0], ts[-1], step, torch.float32)
+            assert grid.numel() == grid_states.shape[1]
+            k, slope, pick = fixed_grid_interp_plan(grid, ts)
+            k_t = torch.from_numpy(k).to(dev)
+            ya, yb = grid_states[:, k_t], grid_states[:, k_t + 1]
+            out = ya + torch.from_numpy(slope).to(dev)[None, :, None] * (yb - ya)
+            pick_t = torch.from_numpy(pick).to(dev)[None, :, None]
+            out = torch.where(pick_t == 1, ya, torch.where(pick_t == 2, yb, out))
+            return out.contiguous()
+
+
+def fixed_grid_interp_plan(grid: torch.Tensor, t: torch.Tensor):
+    """FixedGridODESolver's output rule (torchdiffeq 0.2.2, as restated in odeint._odeint_torch):
+    t[0] is y0; every later t[j] is served by the first grid interval (ta, tb] with tb >= t[j]:
+    t[j] == ta -> y(ta), t[j] == tb -> y(tb), else y(ta) + (t[j]-ta)/(tb-ta) (y(tb) - y(ta)) in float32.
+    Returns (interval index k[n], slope float32[n], pick int8[n]: 0 lerp, 1 y(ta), 2 y(tb))."""
+    g = grid.to(torch.float32).numpy()
+    tt = t.to(torch.float32).numpy()
+    n = tt.shape[0]
+    k = np.zeros(n, dtype=np.int64)
+    slope = np.zeros(n, dtype=np.float32)
+    pick = np.ones(n, dtype=np.int8)                 # t[0]: y0 = grid state 0
+    j = 1
+    for i in range(g.shape[0] - 1):
+        ta, tb = g[i], g[i + 1]
+        while j < n and tb >= tt[j]:
+            k[j] = i
+            if tt[j] == ta:
+                pick[j] = 1
+            elif tt[j] == tb:
+                pick[j] = 2
+            else:
+                pick[j] = 0
+                slope[j] = np.float32((tt[j] - ta) / (tb - ta))
+            j += 1
+    if j < n:
+        raise ValueError("output times beyond the solve's grid")
+    return k, slope, pick
+
+
 class CompositeSampler(nn.Module):
     """sampler.py:169-216."""
 
@@ -133,6 +214,10 @@ class CompositeSampler(nn.Module):
             raise NotImplementedError("the fused sampler orders Uniform rows before CorrectCone rows")
         if all(k is DecisionBoundarySampling for k in kinds):
             return L.FIODE_SAMPLER_DECISION_BOUNDARY, 0
+        if kinds == [UniformSimplexSampling, TrajectorySampler]:
+            return L.FIODE_SAMPLER_TRAJECTORY, split[0]
+        if kinds == [TrajectorySampler]:
+            return L.FIODE_SAMPLER_TRAJECTORY, 0
         if kinds == [UniformSimplexSampling]:
             return L.FIODE_SAMPLER_COMPOSITE, sample_size
         if kinds == [CorrectConeSampling]:

@@ -39,7 +39,10 @@ enum {
   FIODE_EHIP = 100        /* a HIP runtime error; FIODE_EHIP + hipError_t         */
 };
 
-enum { FIODE_SAMPLER_GIVEN = 0, FIODE_SAMPLER_COMPOSITE = 1, FIODE_SAMPLER_DECISION_BOUNDARY = 2 };
+/* TRAJECTORY: rows s < n_uniform are UniformSimplex draws (as COMPOSITE), rows s >= n_uniform are
+   read from io->h laid out [B][S - n_uniform][C] (TrajectorySampler, sampler.py:156-166).          */
+enum { FIODE_SAMPLER_GIVEN = 0, FIODE_SAMPLER_COMPOSITE = 1, FIODE_SAMPLER_DECISION_BOUNDARY = 2,
+       FIODE_SAMPLER_TRAJECTORY = 3 };
 enum { FIODE_DROPOUT_OFF = 0, FIODE_DROPOUT_GIVEN = 1, FIODE_DROPOUT_PHILOX = 2 };
 
 /* Effective (post-Cayley) dynamics weights of OrthoClassDynProjectSimplexLips
@@ -79,7 +82,7 @@ typedef struct fiode_lyap_config {
 typedef struct fiode_lyap_io {
   const float* x_feat;   /* [B][X] static features = param_map(x) (init_coordinates.py:35)     */
   const int64_t* y;      /* [B] labels                                                         */
-  const float* h;        /* [N][C] samples when sampler == GIVEN                               */
+  const float* h;        /* [N][C] samples (GIVEN) or [B][S-n_uniform][C] trajectory rows (TRAJECTORY) */
   const uint8_t* masks;  /* [4][N][M] keep masks (loss L1, loss L2, log L1, log L2), GIVEN mode */
   float* scalars;        /* [8] out: loss, eff_count, mean_active, qp_exit_loss, qp_exit_log,
                             viol_sum, active_count, rows                                       */
