@@ -263,16 +263,40 @@ struct OtBwdShared {
   float gpart[2][4][64][4];
 };
 
+// The saved forward values one VJP reads (independent of the adjoint): loaded one VJP ahead, so
+// their global-memory latency overlaps the previous VJP's dependent chain.
+struct VjpIn {
+  float h[C], ft[C], v[C], mu;
+  f32x4 a2[8];        // saved post-activations of layer 2, this lane's 4 hidden of each block
+  f32x4 a1[2];        // layer 1, hidden blocks 2p, 2p+1
+};
+
+__device__ __forceinline__ void load_vjp_in(const OTArgs& a, int p, int e, int b, bool valid, int q, VjpIn& in) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + (e < 0 ? 0 : e);
+  load_row10(a.hs + r * C, in.h);
+  load_row10(a.ftw + r * C, in.ft);
+  load_row10(a.vw + r * C, in.v);
+  in.mu = a.muw[r];
+#pragma unroll
+  for (int hb = 0; hb < 8; ++hb) in.a2[hb] = *reinterpret_cast<const f32x4*>(a.a2 + r * M + 16 * hb + 4 * q);
+#pragma unroll
+  for (int o = 0; o < 2; ++o) in.a1[o] = *reinterpret_cast<const f32x4*>(a.a1 + r * M + 16 * (2 * p + o) + 4 * q);
+}
+
 __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[8][3],
                        OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int q, int j,
-                       const float (&g)[C], float (&gy_out)[C]) {
+                       const VjpIn& in, const float (&g)[C], float (&gy_out)[C]) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
   float h[C], ft[C], v[C], lower[C], nominal[C], sig[C], span[C];
-  load_row10(a.hs + r * C, h);
-  load_row10(a.ftw + r * C, ft);
-  load_row10(a.vw + r * C, v);
-  const float mu = a.muw[r];
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    h[i] = in.h[i];
+    ft[i] = in.ft[i];
+    v[i] = in.v[i];
+  }
+  const float mu = in.mu;
   barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
   float g_nom[C], g_low[C], gft[C], ghb[C];
   float gin[C];
@@ -310,7 +334,7 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
   }
 #pragma unroll
   for (int hb = 0; hb < 8; ++hb) {
-    const f32x4 act = *reinterpret_cast<const f32x4*>(a.a2 + r * M + 16 * hb + 4 * q);
+    const f32x4 act = in.a2[hb];
 #pragma unroll
     for (int t = 0; t < 4; ++t) ga[hb][t] = act[t] > 0.f ? ga[hb][t] * a.drop_scale : 0.f;
     if (valid && (hb >> 1) == p)
@@ -329,7 +353,7 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
   }
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
-    const f32x4 act = *reinterpret_cast<const f32x4*>(a.a1 + r * M + 16 * (2 * p + o) + 4 * q);
+    const f32x4 act = in.a1[o];
 #pragma unroll
     for (int t = 0; t < 4; ++t) gb[o][t] = act[t] > 0.f ? gb[o][t] * a.drop_scale : 0.f;
     if (valid)
@@ -381,6 +405,14 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
     for (int i = 0; i < C; ++i) gy[i] = 0.f;
   const float third = 1.0f / 3.0f;
   int buf = 0;
+  VjpIn cur, nxt;
+  load_vjp_in(a, p, a.E - 1, b, valid, q, cur);
+  // evals are visited E-1, E-2, ..., 0: each VJP first issues the loads of the next one
+#define OT_VJP(E_, G_)                                                                  \
+  load_vjp_in(a, p, (E_) - 1, b, valid, q, nxt);                                        \
+  ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, (E_), b, valid, lane, q, j, cur, G_, gY);     \
+  cur = nxt;                                                                            \
+  buf ^= 1;
   for (int it = a.niters - 2; it >= 0; --it) {
     float ta, dt;
     step_times(a, it, ta, dt);
@@ -395,8 +427,7 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
       gk4[i] = gy[i] * c8;
     }
     const int e0 = 4 * it;
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 3, b, valid, lane, q, j, gk4, gY);  // Y4 = y + dt (k1 - k2 + k3)
-    buf ^= 1;
+    OT_VJP(e0 + 3, gk4)
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       acc[i] += gY[i];
@@ -405,8 +436,7 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
       gk2[i] -= d;
       gk3[i] += d;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 2, b, valid, lane, q, j, gk3, gY);  // Y3 = y + dt (k2 - k1/3)
-    buf ^= 1;
+    OT_VJP(e0 + 2, gk3)
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       acc[i] += gY[i];
@@ -414,18 +444,17 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
       gk2[i] += d;
       gk1[i] -= d * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0 + 1, b, valid, lane, q, j, gk2, gY);  // Y2 = y + (dt k1) / 3
-    buf ^= 1;
+    OT_VJP(e0 + 1, gk2)
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       acc[i] += gY[i];
       gk1[i] += (dt * gY[i]) * third;
     }
-    ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, e0, b, valid, lane, q, j, gk1, gY);      // Y1 = y
-    buf ^= 1;
+    OT_VJP(e0, gk1)
 #pragma unroll
     for (int i = 0; i < C; ++i) gy[i] = acc[i] + gY[i];
   }
+#undef OT_VJP
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -52,6 +52,7 @@ def freeze(mod, convs=False, linears=False, dyn=False):
     if dyn:
         w = {k: v.detach() for k, v in mod.dyn_fun._effective_weights().items()}
         mod.dyn_fun._effective_weights = (lambda w=w: w)
+        mod.dyn_fun.prefetch = (lambda s: None)     # nothing to overlap (a side-stream no-op is unjoined work)
 
 
 res = {}
