@@ -178,6 +178,10 @@ class _DenseCayleyFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gQ):
+        return _run_on_step_stream(DENSE_BWD_ON_MAIN, lambda: _DenseCayleyFn._backward(ctx, gQ))
+
+    @staticmethod
+    def _backward(ctx, gQ):
         from . import ops, _lib as L
         Wb, al, nrm, inv = ctx.saved_tensors
         wshape, ashape = ctx.shapes
@@ -252,6 +256,30 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
     if cout == cin:
         return top
     return torch.cat([top, -2.0 * (V @ inv)], dim=-2)
+
+
+# Backward placement of the prefetched maps.  autograd runs a node's backward on the stream its
+# forward ran on (a side stream); with these flags the backward of the spectral / dense maps runs
+# on the stream the step was launched from instead (set by LyapunovLearning.compute_loss), which
+# the hipGraph executor places on another hardware queue.
+SPECTRAL_BWD_ON_MAIN = False
+DENSE_BWD_ON_MAIN = False
+STEP_STREAM: Optional[torch.cuda.Stream] = None
+
+
+def _run_on_step_stream(flag: bool, fn):
+    tgt = STEP_STREAM if flag else None
+    cur = torch.cuda.current_stream()
+    if tgt is None or tgt == cur:
+        return fn()
+    tgt.wait_stream(cur)
+    with torch.cuda.stream(tgt):
+        out = fn()
+    cur.wait_stream(tgt)
+    for t in out:
+        if isinstance(t, torch.Tensor):
+            t.record_stream(cur)
+    return out
 
 
 def _prefetch(stream: torch.cuda.Stream, fn):
@@ -361,7 +389,8 @@ class _SpectralCayleyFn(torch.autograd.Function):
     def backward(ctx, gQ):
         from . import ops
         weight, alpha, inv, ws = ctx.saved_tensors
-        gw, ga = ops.spectral_cayley_backward(gQ.contiguous(), weight.detach(), alpha.detach(), ctx.n, inv, ws)
+        gw, ga = _run_on_step_stream(SPECTRAL_BWD_ON_MAIN, lambda: ops.spectral_cayley_backward(
+            gQ.contiguous(), weight.detach(), alpha.detach(), ctx.n, inv, ws))
         return gw, ga.reshape(alpha.shape), None
 
 

@@ -266,10 +266,17 @@ class LyapunovLearning(nn.Module):
         return plan
 
     def _prefetch_weights(self, device):
-        """Launch every Cayley map of the step (backbone convs / linears, dynamics) on side streams
-        before the backbone runs: they depend only on the weights, and their inverses are
-        latency-bound single-workgroup kernels, so they overlap each other and the convolutions.
-        Layers join them when they reach them (autograd runs their backward on the same streams)."""
+        """Launch every Cayley map of the step (backbone convs / linears, dynamics) on side streams:
+        they depend only on the weights, and their inverses are latency-bound small kernels, so they
+        overlap each other and the convolutions.  Layers join them when they reach them (autograd
+        runs their backward on the same streams).
+
+        ``prefetch_schedule`` = {"lin": [k0, k1, k2], "dyn": kd}: the map of linear layer i (of the
+        dynamics) is launched once conv layer k_i of the backbone has been launched (-1: at the
+        start of the step).  The hipGraph executor dispatches nodes in capture order over a few
+        hardware queues, so maps captured ahead of the main stream's first kernels can hold those
+        kernels back; deferring them past the first conv layers measured -0.16 ms per step
+        (tools/stream_probe.py)."""
         if self._side_streams is None:
             self._side_streams = [torch.cuda.Stream(device) for _ in range(4)]
         s = self._side_streams
@@ -279,17 +286,35 @@ class LyapunovLearning(nn.Module):
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
         for c in convs:
             c.prefetch(s[0])
-        for i, l in enumerate(lins):
-            l.prefetch(s[1 + min(i, 2)])
-        self.dyn_fun.prefetch(s[3])
+        sched = getattr(self, "prefetch_schedule", None) or {}
+        klin = list(sched.get("lin", [-1] * len(lins))) + [-1] * len(lins)
+        jobs = [(klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
+        jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[3])))
+        for k, fn in jobs:
+            if k < 0:
+                fn()
+        later = [(k, fn) for k, fn in jobs if k >= 0]
+        bb = self.init_coordinates.param_map
+        target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb
+        if later:
+            def hook(i):
+                for k, fn in later:
+                    if k == i:
+                        fn()
+            target.after_conv_hook = hook
 
     def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
         """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""
         if self.current_epoch == self.epoch_off_scale:
             self.dyn_fun.scale_nominal = False
         if self.parallel_cayley and self.training and x.is_cuda and self.dyn_fun.cayley:
+            from . import cayley as _cy
+            _cy.STEP_STREAM = torch.cuda.current_stream(x.device)
             self._prefetch_weights(x.device)
         static_state, _ = self.init_coordinates(x, self.dyn_fun)
+        bb = self.init_coordinates.param_map
+        if isinstance(bb, torch.nn.Sequential) and getattr(bb[-1], "after_conv_hook", None) is not None:
+            bb[-1].after_conv_hook = None       # never left armed for a later (e.g. validation) forward
         plan = self.step_plan(y, h=h, masks=masks, debug=debug, static_state=static_state)
         w = self.dyn_fun.effective_weights()
         ode_on = self.train_ode and self.current_epoch > self.train_ode_epoch

@@ -59,6 +59,8 @@ class KWLargeConcat(nn.Module):
         mods = list(self.model)
         h = x.permute(2, 3, 1, 0).contiguous()
         i = 0
+        nconv = 0
+        hook = getattr(self, "after_conv_hook", None)      # (conv index) -> None, e.g. a prefetch launch
         while not isinstance(mods[i], nn.Flatten):
             m = mods[i]
             if isinstance(m, CayleyConv):
@@ -66,8 +68,14 @@ class KWLargeConcat(nn.Module):
                 if self.fused_transforms and h.shape[0] // (2 if m.downsample else 1) <= 32:
                     h = m.forward_hwcb_fused(h, gs)     # transforms (+ GroupSort) in HIP kernels
                     i += 2 if gs else 1
+                    if hook is not None:
+                        hook(nconv)
+                    nconv += 1
                     continue
                 h = m.forward_hwcb(h)
+                if hook is not None:
+                    hook(nconv)
+                nconv += 1
             elif isinstance(m, GroupSort):
                 h = m(h, channel_dim=2)
             else:
