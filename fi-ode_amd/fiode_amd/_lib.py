@@ -62,6 +62,7 @@ FIODE_ODE_RK4, FIODE_ODE_DOPRI5 = 0, 1
 FIODE_DTYPE_F32, FIODE_DTYPE_C64 = 0, 1
 FIODE_INV_MAX_N = 128
 FIODE_ODE_MAX_BATCH = 4096
+FIODE_SMALL_CAYLEY_MAX_K, FIODE_SMALL_CAYLEY_MAX_RK = 16, 8192
 
 
 class OdeConfig(ct.Structure):
@@ -132,6 +133,9 @@ def _load():
                                              ct.c_int64]),
         "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_block_inverse": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_small_cayley_forward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp]),
+        "fiode_small_cayley_backward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                                   _vp, _vp]),
         "fiode_dense_cayley_prep": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_finish": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_ginv": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),

@@ -224,16 +224,64 @@ class _DenseCayleyFn(torch.autograd.Function):
         return gW.reshape(wshape), ga.reshape(ashape)
 
 
+class _SmallCayleyFn(torch.autograd.Function):
+    """cayley(alpha W / ||W||) for a batch of real [cout, cin] matrices with k = min(cout, cin)
+    <= 16: forward and backward are one kernel each (fiode_small_cayley_*; small_cayley.hip) --
+    the same formula as _CayleyScaledFn, one workgroup per matrix."""
+
+    @staticmethod
+    def forward(ctx, W, alpha):
+        from . import ops, _lib as L
+        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
+        al = alpha.detach().reshape(-1).contiguous().float()
+        b, cout, cin = Wb.shape
+        k = min(cout, cin)
+        Q = torch.empty_like(Wb)
+        inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
+        nrm = torch.empty(b, dtype=torch.float32, device=W.device)
+        L.check(L.lib().fiode_small_cayley_forward(ops._stream(W.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
+                                                   Q.data_ptr(), inv.data_ptr(), nrm.data_ptr()),
+                "fiode_small_cayley_forward")
+        ctx.save_for_backward(Wb, al, nrm, inv)
+        ctx.shapes = (W.shape, alpha.shape)
+        return Q.reshape(W.shape)
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from . import ops, _lib as L
+        Wb, al, nrm, inv = ctx.saved_tensors
+        wshape, ashape = ctx.shapes
+        b, cout, cin = Wb.shape
+        gQb = gQ.reshape(b, cout, cin).contiguous().float()
+        gW = torch.empty_like(Wb)
+        ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
+        L.check(L.lib().fiode_small_cayley_backward(ops._stream(Wb.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
+                                                    nrm.data_ptr(), inv.data_ptr(), gQb.data_ptr(), gW.data_ptr(),
+                                                    ga.data_ptr()), "fiode_small_cayley_backward")
+        return gW.reshape(wshape), ga.reshape(ashape)
+
+
+def _small_ok(W: torch.Tensor) -> bool:
+    from . import _lib as L
+    cout, cin = W.shape[-2], W.shape[-1]
+    k, R = min(cout, cin), max(cout, cin)
+    return k <= L.FIODE_SMALL_CAYLEY_MAX_K and R * k <= L.FIODE_SMALL_CAYLEY_MAX_RK
+
+
 def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False) -> torch.Tensor:
     """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293).
-    Real matrices on ROCm (one matrix, or a batch with per-matrix norms) take the fused stages of
+    Real matrices on ROCm (one matrix, or a batch with per-matrix norms) take one kernel per
+    direction when k = min(cout, cin) <= 16 (_SmallCayleyFn), else the fused stages of
     _DenseCayleyFn; complex ones and a batch under one norm take _CayleyScaledFn."""
     if W.is_cuda and W.dtype == torch.float32 and (W.dim() == 2 or per_matrix) and DENSE_FUSED:
+        if SMALL_FUSED and _small_ok(W):
+            return _SmallCayleyFn.apply(W, alpha)
         return _DenseCayleyFn.apply(W, alpha)
     return _CayleyScaledFn.apply(W, alpha, per_matrix)
 
 
 DENSE_FUSED = True
+SMALL_FUSED = True
 
 
 def cayley(W: torch.Tensor) -> torch.Tensor:

@@ -257,6 +257,19 @@ FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                   size_t workspace_bytes);
 
+/* ---- small Cayley maps in one launch (k = min(cout, cin) <= 16, max(cout, cin) * k <= 8192): the
+ * backbone's 512 -> 10 CayleyLinear and the dynamics' 128 x 10 maps (classification.py:282-293
+ * convert_cayley).  Q = cayley(alpha W / ||W||) for a batch of [cout][cin] matrices (per-matrix
+ * alpha [b]); the forward also writes ||W|| [b] and the inverse [b][k][k] the backward reads.
+ * One workgroup per matrix (small_cayley.hip). */
+#define FIODE_SMALL_CAYLEY_MAX_K 16
+#define FIODE_SMALL_CAYLEY_MAX_RK 8192
+FIODE_API int fiode_small_cayley_forward(void* stream, int32_t batch, int32_t cout, int32_t cin, const float* W,
+                                         const float* alpha, float* Q, float* inv, float* nrm);
+FIODE_API int fiode_small_cayley_backward(void* stream, int32_t batch, int32_t cout, int32_t cin, const float* W,
+                                          const float* alpha, const float* nrm, const float* inv, const float* gQ,
+                                          float* gW, float* galpha);
+
 /* ---- dense Cayley map stages (CayleyLinear; classification.py:282-293 convert_cayley): the
  * elementwise steps between the library GEMMs and the inverse of Q = cayley(alpha W / ||W||) for a
  * batch of [cout][cin] matrices with per-matrix alpha [b] and ||W|| [b] (see dense.hip).  The

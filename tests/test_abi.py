@@ -91,3 +91,15 @@ def test_block_inverse_host_checks():
     assert lib.fiode_block_inverse(None, 0, None, None, None, 0) == 1
     dummy = ct.c_void_p(1)
     assert lib.fiode_block_inverse(None, 512, dummy, dummy, dummy, 100) == 3
+
+
+def test_small_cayley_host_checks():
+    """fiode_small_cayley_*: k = min(cout, cin) <= 16 and max(cout, cin) * k <= 8192, else EINVAL
+    (checked before any launch); an empty batch is a no-op."""
+    from fiode_amd import _lib as L
+    lib = L.lib()
+    assert lib.fiode_small_cayley_forward(None, 1, 17, 40, None, None, None, None, None) == 1
+    assert lib.fiode_small_cayley_forward(None, 1, 10, 820, None, None, None, None, None) == 1
+    assert lib.fiode_small_cayley_forward(None, 1, 10, 20, None, None, None, None, None) == 1   # NULL pointers
+    assert lib.fiode_small_cayley_forward(None, 0, 10, 20, None, None, None, None, None) == 0
+    assert lib.fiode_small_cayley_backward(None, 1, 16, 513, None, None, None, None, None, None, None) == 1

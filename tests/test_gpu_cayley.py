@@ -384,3 +384,30 @@ def test_dense_cayley_fused_matches_op_by_op(shape, per_matrix):
         out.append((Q.detach(), Wa.grad, aa.grad))
     for a, b in zip(*out):
         assert float((a - b).abs().max()) <= 1e-4 * (float(b.abs().max()) + 1e-6)
+
+
+@pytest.mark.parametrize("shape", [(10, 512), (512, 10), (3, 128, 10), (2, 10, 128), (16, 16), (10, 819), (5, 7)])
+def test_small_cayley_kernel_matches_dense_path(shape):
+    """_SmallCayleyFn (small_cayley.hip, one workgroup per matrix) = _CayleyScaledFn (torch ops) in
+    float32, forward and backward; Q has orthonormal columns (rows for wide maps)."""
+    from fiode_amd.cayley import _CayleyScaledFn, _SmallCayleyFn
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    W = torch.randn(shape, generator=g).to(dev)
+    per_matrix = len(shape) == 3
+    nb = shape[0] if per_matrix else 1
+    alpha = (torch.rand(nb, generator=g) * 3 + 0.5).to(dev)
+    G = torch.randn(shape, generator=g).to(dev)
+    out = []
+    for fn in (lambda w, a: _SmallCayleyFn.apply(w, a), lambda w, a: _CayleyScaledFn.apply(w, a, per_matrix)):
+        Wa, aa = W.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+        Q = fn(Wa, aa)
+        (Q * G).sum().backward()
+        out.append((Q.detach(), Wa.grad, aa.grad))
+    for a, b in zip(*out):
+        assert float((a - b).abs().max()) <= 1e-4 * (float(b.abs().max()) + 1e-6)
+    Q = out[0][0].reshape(-1, shape[-2], shape[-1])
+    Qt = Q if shape[-2] >= shape[-1] else Q.mT
+    eye = torch.eye(Qt.shape[-1], device=dev)
+    assert float((Qt.mT @ Qt - eye).abs().max()) < 2e-5
+
