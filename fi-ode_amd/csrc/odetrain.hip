@@ -614,3 +614,42 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
   io.grads = *grads;
   return fiode_internal::launch_wgrad(st, io);
 }
+
+// ---- the train_ode loss term: F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497) --------
+// One workgroup: loss = -(1/B) sum_b log y_hat[b, y_b] (fixed-order block sum) and its gradient
+// per unit upstream gradient, g[b][c] = -1 / (B y_hat[b, y_b]) at c = y_b, else 0.  A label outside
+// [0, C) makes the loss NaN (torch raises a device assert there).
+namespace {
+__global__ __launch_bounds__(256) void k_ode_nll(int B, const float* __restrict__ y_hat, const int64_t* __restrict__ y,
+                                                 float* __restrict__ loss, float* __restrict__ gunit) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  float s = 0.f;
+  for (int b = tid; b < B; b += 256) {
+    const int64_t l = y[b];
+    const bool ok = l >= 0 && l < C;
+    const float v = ok ? y_hat[(size_t)b * C + l] : __builtin_nanf("");
+    s = s + (-logf(v));
+    const float g = -1.0f / ((float)B * v);
+#pragma unroll
+    for (int c = 0; c < C; ++c) gunit[(size_t)b * C + c] = (c == l) ? g : 0.f;
+  }
+  red[tid] = s;
+  __syncthreads();
+#pragma unroll
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = red[tid] + red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) loss[0] = red[0] / (float)B;
+}
+}  // namespace
+
+extern "C" int fiode_ode_nll(void* stream, int32_t batch, const float* y_hat, const int64_t* labels, float* loss,
+                             float* g_unit) {
+  if (batch <= 0 || !y_hat || !labels || !loss || !g_unit) return FIODE_EINVAL;
+  hipLaunchKernelGGL(k_ode_nll, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), batch, y_hat, labels, loss,
+                     g_unit);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}

@@ -72,6 +72,28 @@ class ODETrainFn(torch.autograd.Function):
         return tuple(grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")) + (None, None)
 
 
+class ODENllFn(torch.autograd.Function):
+    """F.nll_loss(torch.log(y_hat), y) as one kernel forward (fiode_ode_nll, which also writes
+    d loss / d y_hat) and one multiply backward -- the train_ode loss term between the solve's
+    forward and backward kernels, which sits on the step's critical path (pl_modules.py:494-497)."""
+
+    @staticmethod
+    def forward(ctx, y_hat, y):
+        yh = y_hat.detach().contiguous().float()
+        B = yh.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=yh.device)
+        gunit = torch.empty_like(yh)
+        L.check(L.lib().fiode_ode_nll(ops._stream(yh.device), B, yh.data_ptr(), y.contiguous().data_ptr(),
+                                      loss.data_ptr(), gunit.data_ptr()), "fiode_ode_nll")
+        ctx.save_for_backward(gunit)
+        return loss
+
+    @staticmethod
+    def backward(ctx, go):
+        gunit, = ctx.saved_tensors
+        return gunit * go, None
+
+
 class DecisionBoundary(nn.Module):
     """lya_cands.py:72-94 (kept for the validation/ODE path; the training step fuses it)."""
 
@@ -374,7 +396,10 @@ class LyapunovLearning(nn.Module):
             from .cayley import _take
             y_hat = _take(y_hat)
         if self.simplex:
-            loss_ode = F.nll_loss(torch.log(y_hat), y)
+            if y_hat.is_cuda and y.dtype == torch.int64 and y_hat.dim() == 2 and y_hat.shape[1] == 10:
+                loss_ode = ODENllFn.apply(y_hat, y)
+            else:
+                loss_ode = F.nll_loss(torch.log(y_hat), y)
         else:
             loss_ode = F.cross_entropy(y_hat, y)
         self.log("loss_ode", loss_ode)

@@ -202,6 +202,11 @@ FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* 
 FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets);
 /* Given g_y = dL/dy(t1) [B][C]: all weight gradients and dL/dx_feat (overwritten).  Must follow
  * fiode_odetrain_forward on the same workspace.  dbg_gft: optional [B][E][C] dL/d mlp output. */
+/* The train_ode loss term F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497) in one launch:
+ * loss[0] = -(1/B) sum_b log y_hat[b, y_b]; g_unit [B][C] = d loss / d y_hat (times the upstream
+ * gradient in the caller's backward).  labels int64 [B] in [0, C). */
+FIODE_API int fiode_ode_nll(void* stream, int32_t batch, const float* y_hat, const int64_t* labels, float* loss,
+                            float* g_unit);
 FIODE_API int fiode_odetrain_backward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
                                       const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
                                       fiode_lyap_grads* grads, float* dbg_gft, void* workspace,

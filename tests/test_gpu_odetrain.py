@@ -120,3 +120,23 @@ def test_module_train_ode_loss_mix():
     torch.cuda.synchronize()
     s = mod.last_ode_plan["stats"].cpu()
     assert int(s[0]) == 40 and int(s[1]) == 10
+
+
+@pytest.mark.parametrize("B", [1, 128, 300])
+def test_ode_nll_matches_torch(B):
+    """ODENllFn (fiode_ode_nll) = F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497), forward
+    and backward, on simplex rows."""
+    import torch.nn.functional as F
+    from fiode_amd.lyapunov import ODENllFn
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(B)
+    yh = torch.softmax(torch.randn(B, 10, generator=g), -1).to(dev)
+    y = torch.randint(0, 10, (B,), generator=g).to(dev)
+    a, b = yh.clone().requires_grad_(True), yh.clone().requires_grad_(True)
+    la = ODENllFn.apply(a, y)
+    lb = F.nll_loss(torch.log(b), y)
+    (la * 0.37).backward()
+    (lb * 0.37).backward()
+    torch.cuda.synchronize()
+    assert abs(float(la) - float(lb)) <= 1e-6 * max(1.0, abs(float(lb)))
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-7)
