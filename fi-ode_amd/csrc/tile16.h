@@ -91,6 +91,56 @@ __device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float 
     lo = fminf(lo, nom[j]);
   }
 }
+__device__ __forceinline__ float qp_eps(const float (&lower)[C], const float (&nom)[C], float mu) {
+  float eps = 0.f;
+#pragma unroll
+  for (int j = 0; j < C; ++j) eps = eps + fmaxf(nom[j] - mu, lower[j]);
+  return eps;
+}
+
+// The bisection two iterations per round: the 4 lanes of a row (q = 0..3, lanes j + 16 q) evaluate
+// the midpoint m0 (q = 0, 3) and both possible next midpoints -- the left child (q = 1, taken when
+// eps(m0) < 0) and the right child (q = 2, eps(m0) > 0) -- at once, and exchange the three eps
+// values by shuffles.  Every midpoint and eps is the same float32 expression the sequential loop
+// evaluates (m1 = (hi' - lo') / 2 + lo' with the updated bracket), so mu, the convergence bits and
+// the exit are bit-identical to qp_bisect_range; the dependent chain per iteration is halved.
+__device__ __forceinline__ uint32_t qp_bisect_range2(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                     float tol, float& lo, float& hi, float* mu_rec, bool rec,
+                                                     bool valid, int q, int j) {
+  uint32_t conv = 0;
+  int it = from;
+  for (; it + 1 <= to; it += 2) {
+    const float m0 = (hi - lo) / 2.0f + lo;
+    const float mL = (m0 - lo) / 2.0f + lo;
+    const float mR = (hi - m0) / 2.0f + m0;
+    const float e = qp_eps(lower, nom, q == 1 ? mL : (q == 2 ? mR : m0));
+    const float e0 = __shfl(e, j, 64);
+    const float eL = __shfl(e, j + 16, 64);
+    const float eR = __shfl(e, j + 32, 64);
+    if (rec) mu_rec[it] = m0;
+    unsigned long long open = __ballot(valid && !(fabsf(e0) < tol));
+    conv |= (open == 0ull ? 1u : 0u) << it;
+    const float lo1 = e0 > 0.f ? m0 : lo, hi1 = e0 < 0.f ? m0 : hi;
+    const float m1 = e0 < 0.f ? mL : (e0 > 0.f ? mR : m0);
+    const float e1 = e0 < 0.f ? eL : (e0 > 0.f ? eR : e0);
+    if (rec) mu_rec[it + 1] = m1;
+    open = __ballot(valid && !(fabsf(e1) < tol));
+    conv |= (open == 0ull ? 1u : 0u) << (it + 1);
+    lo = e1 > 0.f ? m1 : lo1;
+    hi = e1 < 0.f ? m1 : hi1;
+  }
+  if (it <= to) {
+    const float mu = (hi - lo) / 2.0f + lo;
+    const float eps = qp_eps(lower, nom, mu);
+    if (rec) mu_rec[it] = mu;
+    const unsigned long long open = __ballot(valid && !(fabsf(eps) < tol));
+    conv |= (open == 0ull ? 1u : 0u) << it;
+    lo = eps > 0.f ? mu : lo;
+    hi = eps < 0.f ? mu : hi;
+  }
+  return conv;
+}
+
 __device__ __forceinline__ uint32_t qp_bisect_range(const float (&lower)[C], const float (&nom)[C], int from, int to,
                                                     float tol, float& lo, float& hi, float* mu_rec, bool rec,
                                                     bool valid) {
@@ -196,7 +246,8 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   const int kspec = min(last, kprev + 3);
   float lo, hi;
   qp_bracket(lower, nominal, lo, hi);
-  uint32_t conv = qp_bisect_range(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, q == 0, valid);
+  const int j = lane & 15;
+  uint32_t conv = qp_bisect_range2(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, q == 0, valid, q, j);
   const int ntiles = gridDim.x;
   if (p == 0) {
     if (lane == 0) publish_mask(slots + blockIdx.x, epoch, conv);
@@ -207,7 +258,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   }
   __syncthreads();
   if (shK < 0) {                        // block-uniform: every tile saw the same masks
-    conv |= qp_bisect_range(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, q == 0, valid);
+    conv |= qp_bisect_range2(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, q == 0, valid, q, j);
     if (p == 0) {
       if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, epoch, conv);
       const uint32_t all = gather_masks(slots + ntiles, ntiles, epoch, status, lane);

@@ -1,0 +1,34 @@
+"""A/B bit-identity check of the train_ode solve between two builds of libfiode (not a test):
+FIODE_LIB=<lib> python tools/ab_odetrain.py out.pt  writes y(t1) and the saved (mu, v, h) of a
+seeded solve; compare two outputs with  python tools/ab_odetrain.py --cmp a.pt b.pt."""
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import torch  # noqa: E402
+
+if sys.argv[1] == "--cmp":
+    a, b = torch.load(sys.argv[2]), torch.load(sys.argv[3])
+    for k in a:
+        print(k, "identical" if torch.equal(a[k], b[k]) else f"DIFFER max {float((a[k] - b[k]).abs().max())}")
+    sys.exit(0 if all(torch.equal(a[k], b[k]) for k in a) else 1)
+
+import numpy as np  # noqa: E402
+from fiode_amd import _lib as L, ops  # noqa: E402
+from tests._util import make_params  # noqa: E402
+
+dev = torch.device("cuda:0")
+out = {}
+for B, sn in ((128, False), (300, True), (37, False)):
+    P = make_params(seed=B)
+    rng = np.random.default_rng(B)
+    x = torch.from_numpy(rng.normal(size=(B, 10)).astype(np.float32)).to(dev)
+    h0 = torch.full((B, 10), 0.1, device=dev)
+    w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
+    cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=3, offset=5)
+    y, st, ws = ops.odetrain_forward(x, h0, w, ops.DynCfg(scale_nominal=sn), cfg)
+    sv = ops.odetrain_saved(ws, cfg)
+    out.update({f"y{B}": y.cpu(), f"mu{B}": sv["mu"].cpu(), f"v{B}": sv["v"].cpu(), f"stats{B}": st.cpu()})
+torch.save(out, sys.argv[1])
+print("saved", sys.argv[1])
