@@ -77,30 +77,43 @@ int launch_inv<ComplexOps>(hipStream_t s, int batch, int n, const void* in, int6
 // 64, ~0.9 us at 128), and the update is a few us of LDS-tiled FMA on 64 workgroups.
 constexpr int PB = 64;
 
-__global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* __restrict__ in, float* __restrict__ out) {
+// Batched over matrices m = blockIdx.y (pad, pivot) / blockIdx.z (update): matrix m's buffers sit
+// at + m * wstride floats of the workspace, its input / output at + m * n * n.
+__global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* __restrict__ in, float* __restrict__ out,
+                                                   int64_t wstride) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)np * np) return;
+  const int64_t m = blockIdx.y;
+  in += m * n * n;
+  out += m * wstride;
   const int i = (int)(idx / np), j = (int)(idx % np);
   out[idx] = (i < n && j < n) ? in[(int64_t)i * n + j] : (i == j ? 1.0f : 0.0f);
 }
 
-__global__ void __launch_bounds__(256) k_panel_pivot(int np, int k0, const float* __restrict__ X, float* __restrict__ P) {
+__global__ void __launch_bounds__(256) k_panel_pivot(int np, int k0, const float* __restrict__ X, float* __restrict__ P,
+                                                     int64_t wstride) {
   typedef fiode_gj::GJ<RealOps, PB, 4, 4> G;
   __shared__ typename G::Smem sm;
   float a[4][4];
-  G::load(a, X + (int64_t)k0 * np + k0, PB, np);
+  const int64_t m = blockIdx.x;
+  G::load(a, X + m * wstride + (int64_t)k0 * np + k0, PB, np);
   G::invert(a, PB, sm);
-  G::store(a, P, PB, PB);
+  G::store(a, P + m * wstride, PB, PB);
 }
 
 // out tile (ib, jb) of the next buffer; 256 threads, 4 x 4 outputs each
 __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
                                                       const float* __restrict__ P, float* __restrict__ Y,
-                                                      float* __restrict__ final_out, int n) {
+                                                      float* __restrict__ final_out, int n, int64_t wstride) {
   __shared__ float sP[PB][PB + 4];
   __shared__ float sA[PB][PB + 4];      // X_iK (rows of the tile, pivot columns)
   __shared__ float sB[PB][PB + 4];      // X_Kj, then R_Kj
   const int ib = blockIdx.x * PB, jb = blockIdx.y * PB, tid = threadIdx.x;
+  const int64_t m = blockIdx.z;
+  X += m * wstride;
+  P += m * wstride;
+  Y += m * wstride;
+  if (final_out) final_out += m * (int64_t)n * n;
   const bool piv_r = ib == k0, piv_c = jb == k0;
 #pragma unroll 16
   for (int idx = tid; idx < PB * PB; idx += 256) {     // 16 trips: all loads in flight together
@@ -200,25 +213,34 @@ extern "C" size_t fiode_block_inverse_workspace_bytes(int32_t n) {
   return (2 * np * np + (size_t)PB * PB) * sizeof(float);
 }
 
-extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
-                                   size_t workspace_bytes) {
-  if (n < 1 || n > FIODE_BLOCK_INV_MAX_N || !in || !out || !workspace) return FIODE_EINVAL;
-  if (workspace_bytes < fiode_block_inverse_workspace_bytes(n)) return FIODE_EWORKSPACE;
+extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
+                                           void* workspace, size_t workspace_bytes) {
+  if (batch < 1 || batch > 65535 || n < 1 || n > FIODE_BLOCK_INV_MAX_N || !in || !out || !workspace)
+    return FIODE_EINVAL;
+  if (workspace_bytes < (size_t)batch * fiode_block_inverse_workspace_bytes(n)) return FIODE_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const int np = (n + PB - 1) / PB * PB, nb = np / PB;
+  const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
   float* A = (float*)workspace;
   float* B = A + (size_t)np * np;
   float* P = B + (size_t)np * np;
-  hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256)), dim3(256), 0, st, n, np, in, A);
+  hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256), (unsigned)batch), dim3(256), 0, st,
+                     n, np, in, A, wstride);
   for (int kb = 0; kb < nb; ++kb) {
     const int k0 = kb * PB;
-    hipLaunchKernelGGL(k_panel_pivot, dim3(1), dim3(256), 0, st, np, k0, A, P);
+    hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(256), 0, st, np, k0, A, P, wstride);
     const bool last = kb == nb - 1;
-    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb), dim3(256), 0, st, np, k0, A, P, B, last ? out : nullptr, n);
+    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, P, B,
+                       last ? out : nullptr, n, wstride);
     float* t = A;
     A = B;
     B = t;
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
+                                   size_t workspace_bytes) {
+  return fiode_block_inverse_batched(stream, 1, n, in, out, workspace, workspace_bytes);
 }

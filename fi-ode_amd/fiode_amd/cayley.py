@@ -35,8 +35,7 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
     if n > 64 and M.dtype == torch.float32 and M.is_cuda:
         if M.dim() == 2:
             return ops.block_inverse(M)
-        flat = M.reshape(-1, n, n)
-        return torch.stack([ops.block_inverse(m) for m in flat]).reshape(M.shape)
+        return ops.block_inverse(M.reshape(-1, n, n)).reshape(M.shape)
     if n <= _BLOCK:
         return ops.batched_inverse(M)
     X = M.clone()
@@ -143,6 +142,83 @@ class _CayleyScaledFn(torch.autograd.Function):
         return gW, galpha, None
 
 
+def _dense_prep(W: torch.Tensor, alpha: torch.Tensor, M: Optional[torch.Tensor] = None):
+    """Forward up to the Cayley system: norms, G = V'^T V' (GEMM), M = I + s (U' - U'^T) + s^2 G
+    (k_dense_prep).  ``M``: optional [b, k, k] output buffer (a slice of a batched system)."""
+    from . import ops, _lib as L
+    Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
+    al = alpha.detach().reshape(-1).contiguous().float()
+    b, cout, cin = Wb.shape
+    wide = cin > cout
+    k = cout if wide else cin
+    nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
+    Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
+    G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
+    cfg = L.DenseConfig(b, cout, cin)
+    if M is None:
+        M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
+    L.check(L.lib().fiode_dense_cayley_prep(ops._stream(W.device), ct.byref(cfg), Wb.data_ptr(), al.data_ptr(),
+                                            nrm.data_ptr(), ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
+    return dict(Wb=Wb, al=al, nrm=nrm, wide=wide, k=k, Vp=Vp, cfg=cfg), M
+
+
+def _dense_finish(st: dict, inv: torch.Tensor) -> torch.Tensor:
+    """Q = [2 inv - I ; -2 s V' inv] in W's layout (P GEMM + k_dense_finish)."""
+    from . import ops, _lib as L
+    Wb, k = st["Wb"], st["k"]
+    P = None                    # V' inv in W's layout (wide: its transpose inv^T V'^T = inv^T W[:, k:])
+    if st["Vp"] is not None:
+        P = torch.matmul(inv.mT, Wb[:, :, k:]) if st["wide"] else torch.matmul(st["Vp"], inv)
+        P = P.contiguous()
+    Q = torch.empty_like(Wb)
+    L.check(L.lib().fiode_dense_cayley_finish(ops._stream(Wb.device), ct.byref(st["cfg"]), st["al"].data_ptr(),
+                                              st["nrm"].data_ptr(), inv.data_ptr(), ops._ptr(P), Q.data_ptr()),
+            "fiode_dense_cayley_finish")
+    return Q
+
+
+def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
+    """dL/dW, dL/dalpha of the dense Cayley map from dL/dQ (GEMMs + dense.hip stages)."""
+    from . import ops, _lib as L
+    b, cout, cin = Wb.shape
+    wide = cin > cout
+    k = cout if wide else cin
+    R = max(cout, cin)
+    gQb = gQ.reshape(b, cout, cin).contiguous()
+    cfg = L.DenseConfig(b, cout, cin)
+    lib, st = L.lib(), ops._stream(Wb.device)
+    Vp = Gb = A = None
+    if R > k:
+        Vp = Wb[:, :, k:].mT if wide else Wb[:, k:, :]
+        Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
+        A = torch.matmul(Vp.mT, Gb).contiguous()
+    Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
+    L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
+                                        ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
+    ih = inv.mT
+    GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
+    gX = torch.empty_like(Wb)                    # W layout
+    H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
+    L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
+            "fiode_dense_cayley_h")
+    P1 = P2 = None                  # V' H and Gb inv^T in W's layout (wide: H^T W[:, k:], inv gQ[:, k:])
+    if R > k:
+        if wide:
+            P1 = torch.matmul(H.mT, Wb[:, :, k:]).contiguous()
+            P2 = torch.matmul(inv, gQb[:, :, k:]).contiguous()
+        else:
+            P1 = torch.matmul(Vp, H).contiguous()
+            P2 = torch.matmul(Gb, ih).contiguous()
+    gW = torch.empty_like(Wb)
+    ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
+    ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,
+                     device=Wb.device)
+    L.check(lib.fiode_dense_cayley_grad(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
+                                        ops._ptr(P1), ops._ptr(P2), gX.data_ptr(), gW.data_ptr(), ga.data_ptr(),
+                                        ws.data_ptr(), ws.numel()), "fiode_dense_cayley_grad")
+    return gW.reshape(wshape), ga.reshape(ashape)
+
+
 class _DenseCayleyFn(torch.autograd.Function):
     """cayley(alpha W / ||W||) for a batch of real [cout, cin] matrices (per-matrix norm and alpha):
     the same forward / analytic backward as _CayleyScaledFn, with the GEMMs as library GEMMs and
@@ -150,78 +226,61 @@ class _DenseCayleyFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, W, alpha):
-        from . import ops, _lib as L
-        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
-        al = alpha.detach().reshape(-1).contiguous().float()
-        b, cout, cin = Wb.shape
-        wide = cin > cout
-        k = cout if wide else cin
-        nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
-        Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
-        G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
-        cfg = L.DenseConfig(b, cout, cin)
-        lib, st = L.lib(), ops._stream(W.device)
-        M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
-        L.check(lib.fiode_dense_cayley_prep(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
-                                            ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
+        st, M = _dense_prep(W, alpha)
         inv = _block_inverse(M)
-        P = None                    # V' inv in W's layout (wide: its transpose inv^T V'^T = inv^T W[:, k:])
-        if Vp is not None:
-            P = torch.matmul(inv.mT, Wb[:, :, k:]) if wide else torch.matmul(Vp, inv)
-            P = P.contiguous()
-        Q = torch.empty_like(Wb)
-        L.check(lib.fiode_dense_cayley_finish(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), inv.data_ptr(),
-                                              ops._ptr(P), Q.data_ptr()), "fiode_dense_cayley_finish")
-        ctx.save_for_backward(Wb, al, nrm, inv)
+        Q = _dense_finish(st, inv)
+        ctx.save_for_backward(st["Wb"], st["al"], st["nrm"], inv)
         ctx.shapes = (W.shape, alpha.shape)
         return Q.reshape(W.shape)
 
     @staticmethod
     def backward(ctx, gQ):
-        return _run_on_step_stream(DENSE_BWD_ON_MAIN, lambda: _DenseCayleyFn._backward(ctx, gQ))
+        Wb, al, nrm, inv = ctx.saved_tensors
+        return _run_on_step_stream(DENSE_BWD_ON_MAIN, lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
+
+
+class _DenseCayleyGroupFn(torch.autograd.Function):
+    """Several dense Cayley maps with the same k = min(cout, cin) (the backbone's 4096 -> 512 and
+    512 -> 512 CayleyLinears) in one node: their systems are stacked and inverted by ONE batched
+    block inverse (fiode_block_inverse_batched), so the two latency chains of 2 k / 64 dependent
+    launches become one.  apply(W1, alpha1, W2, alpha2, ...) -> (Q1, Q2, ...); the backward is
+    each map's own (_dense_backward; the inverse is not in it)."""
 
     @staticmethod
-    def _backward(ctx, gQ):
-        from . import ops, _lib as L
-        Wb, al, nrm, inv = ctx.saved_tensors
-        wshape, ashape = ctx.shapes
-        b, cout, cin = Wb.shape
-        wide = cin > cout
-        k = cout if wide else cin
-        R = max(cout, cin)
-        gQb = gQ.reshape(b, cout, cin).contiguous()
-        cfg = L.DenseConfig(b, cout, cin)
-        lib, st = L.lib(), ops._stream(Wb.device)
-        Vp = Gb = A = None
-        if R > k:
-            Vp = Wb[:, :, k:].mT if wide else Wb[:, k:, :]
-            Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
-            A = torch.matmul(Vp.mT, Gb).contiguous()
-        Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
-        L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
-                                            ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
-        ih = inv.mT
-        GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
-        gX = torch.empty_like(Wb)                    # W layout
-        H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
-        L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
-                "fiode_dense_cayley_h")
-        P1 = P2 = None                  # V' H and Gb inv^T in W's layout (wide: H^T W[:, k:], inv gQ[:, k:])
-        if R > k:
-            if wide:
-                P1 = torch.matmul(H.mT, Wb[:, :, k:]).contiguous()
-                P2 = torch.matmul(inv, gQb[:, :, k:]).contiguous()
-            else:
-                P1 = torch.matmul(Vp, H).contiguous()
-                P2 = torch.matmul(Gb, ih).contiguous()
-        gW = torch.empty_like(Wb)
-        ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
-        ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,
-                         device=Wb.device)
-        L.check(lib.fiode_dense_cayley_grad(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
-                                            ops._ptr(P1), ops._ptr(P2), gX.data_ptr(), gW.data_ptr(), ga.data_ptr(),
-                                            ws.data_ptr(), ws.numel()), "fiode_dense_cayley_grad")
-        return gW.reshape(wshape), ga.reshape(ashape)
+    def forward(ctx, *args):
+        Ws, alphas = args[0::2], args[1::2]
+        k = min(Ws[0].shape[-2:])
+        Mall = torch.empty((len(Ws), k, k), dtype=torch.float32, device=Ws[0].device)
+        sts = [_dense_prep(W, a, M=Mall[i:i + 1])[0] for i, (W, a) in enumerate(zip(Ws, alphas))]
+        invs = _block_inverse(Mall)
+        Qs = [_dense_finish(st, invs[i:i + 1]).reshape(W.shape) for i, (st, W) in enumerate(zip(sts, Ws))]
+        saved = []
+        for i, st in enumerate(sts):
+            saved += [st["Wb"], st["al"], st["nrm"], invs[i:i + 1]]
+        ctx.save_for_backward(*saved)
+        ctx.shapes = [(W.shape, a.shape) for W, a in zip(Ws, alphas)]
+        return tuple(Qs)
+
+    @staticmethod
+    def backward(ctx, *gQs):
+        saved = ctx.saved_tensors
+        out = []
+        for i, (gQ, shp) in enumerate(zip(gQs, ctx.shapes)):
+            if gQ is None:
+                out += [None, None]
+                continue
+            Wb, al, nrm, inv = saved[4 * i:4 * i + 4]
+            out += list(_dense_backward(Wb, al, nrm, inv, gQ, *shp))
+        return tuple(out)
+
+
+def dense_cayley_group(Ws, alphas):
+    """Q_i = cayley(alpha_i W_i / ||W_i||) for 2-D real ROCm matrices with a common k, with one
+    batched inverse (see _DenseCayleyGroupFn)."""
+    args = []
+    for W, a in zip(Ws, alphas):
+        args += [W, a]
+    return _DenseCayleyGroupFn.apply(*args)
 
 
 class _SmallCayleyFn(torch.autograd.Function):
@@ -384,6 +443,29 @@ class CayleyLinear(nn.Linear):
         elif self.training or self._Q is None:
             self._Q = self.effective_weight()
         return F.linear(x, self._Q if self.training else self._Q.detach(), self.bias)
+
+
+def group_prefetch(lins, stream: torch.cuda.Stream) -> None:
+    """Prefetch the Cayley maps of several CayleyLinears with the same k as one group node on
+    ``stream`` (dense_cayley_group); each layer joins its own Q at its next training forward."""
+    main = torch.cuda.current_stream(stream.device)
+    stream.wait_stream(main)
+    with torch.cuda.stream(stream):
+        Qs = dense_cayley_group([l.weight for l in lins], [l.alpha for l in lins])
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    for l, Q in zip(lins, Qs):
+        l._pre = (Q, ev)
+
+
+def _group_eligible(l) -> bool:
+    """Dense (k > 64: block-inverse) CayleyLinear maps on ROCm; grouped by k by the caller."""
+    W = l.weight
+    return (isinstance(l, CayleyLinear) and W.is_cuda and W.dtype == torch.float32 and W.dim() == 2
+            and DENSE_FUSED and min(W.shape) > 64)
+
+
+group_prefetch.eligible = _group_eligible
 
 
 class _GroupSortFn(torch.autograd.Function):

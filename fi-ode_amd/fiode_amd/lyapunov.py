@@ -310,7 +310,22 @@ class LyapunovLearning(nn.Module):
             c.prefetch(s[0])
         sched = getattr(self, "prefetch_schedule", None) or {}
         klin = list(sched.get("lin", [-1] * len(lins))) + [-1] * len(lins)
-        jobs = [(klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
+        jobs = []
+        if getattr(self, "group_lin_maps", False) and not sched:
+            # the linear maps with a common k > 64 (4096 -> 512, 512 -> 512): one node, one batched inverse
+            # (off by default: tools/ab_step.py measured no gain -- 2.47 vs 2.44 ms interleaved)
+            from .cayley import group_prefetch
+            by_k: Dict[int, list] = {}
+            for l in lins:
+                if group_prefetch.eligible(l):
+                    by_k.setdefault(min(l.weight.shape), []).append(l)
+            big = max(by_k.values(), key=len) if by_k else []
+            if len(big) > 1:
+                jobs.append((-1, (lambda big=big: group_prefetch(big, s[1]))))
+                lins = [l for l in lins if l not in big]
+                klin = [-1] * len(lins)
+        jobs += [(klin[i], (lambda l=l, st=s[2 + min(i, 1)]: l.prefetch(st))) if jobs else
+                 (klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
         jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[3])))
         for k, fn in jobs:
             if k < 0:

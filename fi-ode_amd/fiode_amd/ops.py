@@ -380,20 +380,23 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
 
 
 def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """(n, n) float32 -> inverse by 64-wide panel block Gauss-Jordan on the device
-    (fiode_block_inverse).  Valid for matrices with positive-definite symmetric part."""
-    if M.device.type != "cuda" or M.dtype != torch.float32 or M.dim() != 2 or M.shape[0] != M.shape[1]:
+    """(n, n) or (b, n, n) float32 -> inverse by 64-wide panel block Gauss-Jordan on the device
+    (fiode_block_inverse[_batched]: one launch sequence for the whole batch).  Valid for matrices
+    with positive-definite symmetric part."""
+    if (M.device.type != "cuda" or M.dtype != torch.float32 or M.dim() not in (2, 3)
+            or M.shape[-1] != M.shape[-2]):
         raise ValueError(f"block_inverse: square float32 ROCm matrix expected, got {tuple(M.shape)} {M.dtype} "
                          f"on {M.device}")
-    n = int(M.shape[0])
+    n = int(M.shape[-1])
+    b = 1 if M.dim() == 2 else int(M.shape[0])
     M = M.contiguous()
     if out is None:
         out = torch.empty_like(M)
     lib = L.lib()
-    nb = lib.fiode_block_inverse_workspace_bytes(n)
+    nb = lib.fiode_block_inverse_workspace_bytes(n) * b
     ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}")
-    L.check(lib.fiode_block_inverse(_stream(M.device), n, M.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel()),
-            "fiode_block_inverse")
+    L.check(lib.fiode_block_inverse_batched(_stream(M.device), b, n, M.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                            ws.numel()), "fiode_block_inverse_batched")
     return out
 
 

@@ -261,6 +261,11 @@ FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64
 FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                   size_t workspace_bytes);
+/* The same for a batch of n x n matrices (in / out [batch][n][n] contiguous, workspace
+ * batch * fiode_block_inverse_workspace_bytes(n)): one launch sequence for all of them, so the
+ * Cayley systems of several layers share the 2 * n/64 dependent launches. */
+FIODE_API int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
+                                          void* workspace, size_t workspace_bytes);
 
 /* ---- small Cayley maps in one launch (k = min(cout, cin) <= 16, max(cout, cin) * k <= 8192): the
  * backbone's 512 -> 10 CayleyLinear and the dynamics' 128 x 10 maps (classification.py:282-293

@@ -411,3 +411,35 @@ def test_small_cayley_kernel_matches_dense_path(shape):
     eye = torch.eye(Qt.shape[-1], device=dev)
     assert float((Qt.mT @ Qt - eye).abs().max()) < 2e-5
 
+
+
+def test_batched_block_inverse_equals_single():
+    """fiode_block_inverse_batched: each matrix's result is bit-identical to its own inverse."""
+    from fiode_amd import ops
+    dev = _dev()
+    Ms = torch.stack([_system(1, n, torch.float32, dev, scale=3.0, seed=s)[0] for s, n in ((1, 192), (2, 192),
+                                                                                          (3, 192))]).float()
+    inv = ops.block_inverse(Ms)
+    for i in range(3):
+        assert torch.equal(inv[i], ops.block_inverse(Ms[i].contiguous()))
+
+
+def test_dense_cayley_group_equals_separate_maps():
+    """dense_cayley_group (one node, one batched inverse) = each map's _DenseCayleyFn, bit for bit,
+    forward and backward (the 4096 -> 512 and 512 -> 512 backbone shapes)."""
+    from fiode_amd.cayley import _DenseCayleyFn, dense_cayley_group
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    Ws = [torch.randn(512, 4096, generator=g).to(dev) * 0.02, torch.randn(512, 512, generator=g).to(dev) * 0.05]
+    als = [torch.tensor([1.5]).to(dev), torch.tensor([0.8]).to(dev)]
+    Gs = [torch.randn(W.shape, generator=g).to(dev) for W in Ws]
+    A = [W.clone().requires_grad_(True) for W in Ws]
+    Aa = [a.clone().requires_grad_(True) for a in als]
+    Qs = dense_cayley_group(A, Aa)
+    sum((Q * G).sum() for Q, G in zip(Qs, Gs)).backward()
+    for i in range(2):
+        W, a = Ws[i].clone().requires_grad_(True), als[i].clone().requires_grad_(True)
+        Q = _DenseCayleyFn.apply(W, a)
+        (Q * Gs[i]).sum().backward()
+        assert torch.equal(Q, Qs[i])
+        assert torch.equal(W.grad, A[i].grad) and torch.equal(a.grad, Aa[i].grad)

@@ -1,0 +1,60 @@
+"""Interleaved A/B of step variants (not a test): every variant's hipGraph step is captured first,
+then replayed round-robin (R rounds x K steps each), so box-level drift hits all variants alike.
+
+python tools/ab_step.py [rounds]  ->  one JSON line: median ms per step per variant
+"""
+import json
+import pathlib
+import statistics
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+
+
+def make(setup):
+    mod = bench.build_module(dev, train_ode=True)
+    setup(mod)
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    return GraphTrainStep(mod, opt, x, y)
+
+
+def nogroup(m):
+    m.group_lin_maps = False
+
+
+def after_ode(m):
+    m.lyap_after_ode = True
+
+
+def grouped(m):
+    m.group_lin_maps = True
+
+
+VARIANTS = {"default": lambda m: None, "lyap_after_ode": after_ode, "grouped_lin_maps": grouped}
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+steps = {k: make(f) for k, f in VARIANTS.items()}
+times = {k: [] for k in VARIANTS}
+for r in range(rounds):
+    for k, gs in steps.items():
+        for _ in range(3):
+            gs.step()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(20):
+            gs.step()
+        torch.cuda.synchronize()
+        times[k].append((time.perf_counter() - t) / 20 * 1e3)
+print(json.dumps({k: round(statistics.median(v), 4) for k, v in times.items()} |
+                 {k + "_all": [round(t, 3) for t in v] for k, v in times.items()}), flush=True)
