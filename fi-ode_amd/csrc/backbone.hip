@@ -56,7 +56,48 @@ int check_gs(int64_t B, int64_t C, int64_t S, const void* p0, const void* p1) {
   return FIODE_OK;
 }
 
+// Input normalisation fused with the layout change of the conv stack (models.py:17-26 Normalize,
+// then KWLargeConcat's NCHW -> spatial-major permute): y[h][w][c][b] = (x[b][c][h][w] - mu[c]) /
+// std[c] (std nullable: subtraction only) -- the same two float32 roundings as torch's sub + div.
+// 64 x 64 (image, pixel) tiles transposed through LDS: both the reads (along pixels) and the writes
+// (along images) are coalesced.
+__global__ void __launch_bounds__(256) k_normalize_hwcb(int B, int C, int HW, const float* __restrict__ x,
+                                                        const float* __restrict__ mu, const float* __restrict__ sd,
+                                                        float* __restrict__ y) {
+  __shared__ float t[64][65];
+  const int p0 = blockIdx.x * 64, b0 = blockIdx.y * 64, c = blockIdx.z, tid = threadIdx.x;
+  const float m = mu[c], s = sd ? sd[c] : 1.0f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int r = u * 4 + (tid >> 6), q = tid & 63;          // r: image in tile, q: pixel in tile
+    const int b = b0 + r, pix = p0 + q;
+    float v = 0.f;
+    if (b < B && pix < HW) {
+      v = x[((int64_t)b * C + c) * HW + pix] - m;
+      if (sd) v = v / s;
+    }
+    t[r][q] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int q = u * 4 + (tid >> 6), r = tid & 63;          // q: pixel, r: image
+    const int b = b0 + r, pix = p0 + q;
+    if (b < B && pix < HW) y[((int64_t)pix * C + c) * B + b] = t[r][q];
+  }
+}
+
 }  // namespace
+
+extern "C" int fiode_normalize_hwcb(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, const float* x,
+                                    const float* mu, const float* std, float* y) {
+  if (B < 1 || C < 1 || C > 65535 || H < 1 || W < 1 || !x || !mu || !y) return FIODE_EINVAL;
+  const int HW = H * W;
+  hipLaunchKernelGGL(k_normalize_hwcb, dim3((unsigned)((HW + 63) / 64), (unsigned)((B + 63) / 64), (unsigned)C),
+                     dim3(256), 0, (hipStream_t)stream, B, C, HW, x, mu, std, y);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
 
 extern "C" int fiode_groupsort_forward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, float* y) {
   int rc = check_gs(B, C, S, x, y);

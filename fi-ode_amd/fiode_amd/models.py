@@ -24,7 +24,24 @@ class Normalize(nn.Module):
         self.register_buffer("mu", torch.tensor(list(mu), dtype=torch.float32).view(-1, 1, 1))
         self.register_buffer("std", None if std is None else torch.tensor(list(std), dtype=torch.float32).view(-1, 1, 1))
 
+    fused_hwcb = True      # ROCm: one kernel that also lays the result out spatial-major (see forward)
+
     def forward(self, x):
+        """On ROCm inputs that need no gradient, one kernel (fiode_normalize_hwcb) computes the same
+        float32 (x - mu) / std and stores it spatial-major ([h, w, C, B], the conv stack's layout);
+        the NCHW-shaped result is a view of that storage, so KWLargeConcat's permute to
+        spatial-major is free.  Otherwise the two torch ops."""
+        if self.fused_hwcb and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and not x.requires_grad:
+            from . import _lib as L, ops
+            B, C, H, W = x.shape
+            xc = x.contiguous()
+            y = torch.empty((H, W, C, B), dtype=torch.float32, device=x.device)
+            mu = self.mu.reshape(-1).contiguous()
+            sd = None if self.std is None else self.std.reshape(-1).contiguous()
+            L.check(L.lib().fiode_normalize_hwcb(ops._stream(x.device), B, C, H, W, xc.data_ptr(), mu.data_ptr(),
+                                                 None if sd is None else sd.data_ptr(), y.data_ptr()),
+                    "fiode_normalize_hwcb")
+            return y.permute(3, 2, 0, 1)
         if self.std is not None:
             return (x - self.mu) / self.std
         return x - self.mu

@@ -249,6 +249,10 @@ FIODE_API int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch, 
 /* ---- Backbone GroupSort (KWLarge_Concat activation; absent libs/ortho_conv, restated) --------
  * x, y: [B][C][S] float32 (S = spatial size, 1 for linear layers); C even, (C/2)*S % 4 == 0.
  * y = cat(max(x[:, :C/2], x[:, C/2:]), min(...)); backward splits ties in half (torch.maximum). */
+/* Normalize (models.py:17-26) fused with the backbone's NCHW -> spatial-major layout change:
+ * y [H][W][C][B] = (x [B][C][H][W] - mu[c]) / std[c] (std may be NULL: no division). */
+FIODE_API int fiode_normalize_hwcb(void* stream, int32_t B, int32_t C, int32_t H, int32_t W, const float* x,
+                                   const float* mu, const float* std, float* y);
 FIODE_API int fiode_groupsort_forward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, float* y);
 FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, const float* g,
                                        float* gx);

@@ -443,3 +443,19 @@ def test_dense_cayley_group_equals_separate_maps():
         (Q * Gs[i]).sum().backward()
         assert torch.equal(Q, Qs[i])
         assert torch.equal(W.grad, A[i].grad) and torch.equal(a.grad, Aa[i].grad)
+
+
+@pytest.mark.parametrize("B,C,H,W,with_std", [(128, 3, 32, 32, True), (5, 3, 7, 9, True), (70, 2, 8, 8, False)])
+def test_normalize_hwcb_matches_torch(B, C, H, W, with_std):
+    """Normalize on ROCm (fiode_normalize_hwcb): bit-identical to (x - mu) / std, returned as an
+    NCHW view of spatial-major storage (so the conv stack's permute is a no-op)."""
+    from fiode_amd.models import Normalize
+    dev = _dev()
+    g = torch.Generator().manual_seed(B)
+    x = torch.rand(B, C, H, W, generator=g).to(dev)
+    mu, sd = [0.485, 0.456, 0.406][:C], ([0.225, 0.2, 0.25][:C] if with_std else None)
+    n = Normalize(mu, sd).to(dev)
+    y = n(x)
+    ref = (x - n.mu) / n.std if with_std else x - n.mu
+    assert torch.equal(y, ref)
+    assert y.permute(2, 3, 1, 0).is_contiguous()

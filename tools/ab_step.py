@@ -42,7 +42,21 @@ def grouped(m):
     m.group_lin_maps = True
 
 
-VARIANTS = {"default": lambda m: None, "lyap_after_ode": after_ode, "grouped_lin_maps": grouped}
+def unfused_normalize(m):
+    m.init_coordinates.param_map[0].fused_hwcb = False
+
+
+def no_small_cayley(m):
+    from fiode_amd import cayley
+    cayley.SMALL_FUSED = False      # (module-global: restored by the next variant's build)
+
+
+def small_cayley_on(m):
+    from fiode_amd import cayley
+    cayley.SMALL_FUSED = True
+
+
+VARIANTS = {"default": small_cayley_on, "unfused_normalize": unfused_normalize}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 steps = {k: make(f) for k, f in VARIANTS.items()}
 times = {k: [] for k in VARIANTS}
