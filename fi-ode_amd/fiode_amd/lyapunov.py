@@ -125,6 +125,13 @@ class UniformInitFun(nn.Module):
         return self.param_map(x), h0
 
 
+# Capture order of the Cayley-map prefetch in the training step: after the step's input kernels
+# (the hipGraph executor dispatches in capture order; maps captured ahead of the input
+# normalisation held the conv stack back): 2.41 -> 2.32 ms per step in the interleaved A/B of
+# tools/ab_step.py, better than every deferral of the linear / dynamics maps tried.
+DEFAULT_PREFETCH_SCHEDULE = {"after_input": True}
+
+
 class LyapunovLearning(nn.Module):
     """pl_modules.py:338-502 (order=1, act='relu', DecisionBoundary candidate)."""
 
@@ -299,6 +306,24 @@ class LyapunovLearning(nn.Module):
         hardware queues, so maps captured ahead of the main stream's first kernels can hold those
         kernels back; deferring them past the first conv layers measured -0.16 ms per step
         (tools/stream_probe.py)."""
+        sched = getattr(self, "prefetch_schedule", None)
+        if sched is None:
+            sched = dict(DEFAULT_PREFETCH_SCHEDULE)
+        if sched.get("after_input") and not getattr(self, "_in_input_hook", False):
+            # capture the map launches after the step's input kernels (see docstring)
+            bb = self.init_coordinates.param_map
+            target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb
+
+            def hook(i, _t=target):
+                if i == -1:
+                    _t.after_conv_hook = None
+                    self._in_input_hook = True
+                    try:
+                        self._prefetch_weights(device)
+                    finally:
+                        self._in_input_hook = False
+            target.after_conv_hook = hook
+            return
         if self._side_streams is None:
             self._side_streams = [torch.cuda.Stream(device) for _ in range(4)]
         s = self._side_streams
@@ -306,12 +331,12 @@ class LyapunovLearning(nn.Module):
         for m in self.init_coordinates.modules():
             if hasattr(m, "prefetch") and m is not self.dyn_fun:
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
-        for c in convs:
-            c.prefetch(s[0])
-        sched = getattr(self, "prefetch_schedule", None) or {}
+        if sched.get("order", "conv_first") == "conv_first":
+            for c in convs:
+                c.prefetch(s[0])
         klin = list(sched.get("lin", [-1] * len(lins))) + [-1] * len(lins)
         jobs = []
-        if getattr(self, "group_lin_maps", False) and not sched:
+        if getattr(self, "group_lin_maps", False) and not sched.get("lin"):
             # the linear maps with a common k > 64 (4096 -> 512, 512 -> 512): one node, one batched inverse
             # (off by default: tools/ab_step.py measured no gain -- 2.47 vs 2.44 ms interleaved)
             from .cayley import group_prefetch
@@ -330,6 +355,9 @@ class LyapunovLearning(nn.Module):
         for k, fn in jobs:
             if k < 0:
                 fn()
+        if sched.get("order", "conv_first") != "conv_first":
+            for c in convs:
+                c.prefetch(s[0])
         later = [(k, fn) for k, fn in jobs if k >= 0]
         bb = self.init_coordinates.param_map
         target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb

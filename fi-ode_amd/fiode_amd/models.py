@@ -77,7 +77,10 @@ class KWLargeConcat(nn.Module):
         h = x.permute(2, 3, 1, 0).contiguous()
         i = 0
         nconv = 0
-        hook = getattr(self, "after_conv_hook", None)      # (conv index) -> None, e.g. a prefetch launch
+        # after_conv_hook(conv index) -> None (e.g. a prefetch launch), re-read at every call site so a
+        # hook may install the next one; index -1: input laid out, before the first conv
+        if getattr(self, "after_conv_hook", None) is not None:
+            self.after_conv_hook(-1)
         while not isinstance(mods[i], nn.Flatten):
             m = mods[i]
             if isinstance(m, CayleyConv):
@@ -85,13 +88,13 @@ class KWLargeConcat(nn.Module):
                 if self.fused_transforms and h.shape[0] // (2 if m.downsample else 1) <= 32:
                     h = m.forward_hwcb_fused(h, gs)     # transforms (+ GroupSort) in HIP kernels
                     i += 2 if gs else 1
-                    if hook is not None:
-                        hook(nconv)
+                    if getattr(self, "after_conv_hook", None) is not None:
+                        self.after_conv_hook(nconv)
                     nconv += 1
                     continue
                 h = m.forward_hwcb(h)
-                if hook is not None:
-                    hook(nconv)
+                if getattr(self, "after_conv_hook", None) is not None:
+                    self.after_conv_hook(nconv)
                 nconv += 1
             elif isinstance(m, GroupSort):
                 h = m(h, channel_dim=2)

@@ -56,7 +56,23 @@ def small_cayley_on(m):
     cayley.SMALL_FUSED = True
 
 
-VARIANTS = {"default": small_cayley_on, "unfused_normalize": unfused_normalize}
+def maps_after_input(m):
+    m.prefetch_schedule = {"after_input": True}
+
+
+def sched(**kw):
+    def f(m):
+        m.prefetch_schedule = {"after_input": True, **kw}
+    return f
+
+
+def at_start(m):
+    m.prefetch_schedule = {}
+
+
+VARIANTS = {"default(after_input)": lambda m: None, "at_step_start": at_start,
+            "after_input_lins_first": sched(order="lin_first"),
+            "after_input_unfused_norm": lambda m: (maps_after_input(m), unfused_normalize(m))}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 steps = {k: make(f) for k, f in VARIANTS.items()}
 times = {k: [] for k in VARIANTS}
