@@ -70,9 +70,16 @@ def at_start(m):
     m.prefetch_schedule = {}
 
 
-VARIANTS = {"default(after_input)": lambda m: None, "at_step_start": at_start,
-            "after_input_lins_first": sched(order="lin_first"),
-            "after_input_unfused_norm": lambda m: (maps_after_input(m), unfused_normalize(m))}
+def grouped_ai(m):
+    m.group_lin_maps = True
+
+
+def grouped_ai_linfirst(m):
+    m.group_lin_maps = True
+    m.prefetch_schedule = {"after_input": True, "order": "lin_first"}
+
+
+VARIANTS = {"default(after_input)": lambda m: None, "grouped": grouped_ai, "grouped_lin_first": grouped_ai_linfirst}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 steps = {k: make(f) for k, f in VARIANTS.items()}
 times = {k: [] for k in VARIANTS}
