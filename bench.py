@@ -32,6 +32,12 @@ for _p in (ROOT, ROOT / "fi-ode_amd"):
     if str(_p) not in sys.path:
         sys.path.insert(0, str(_p))
 
+# The hipGraph executor of this ROCm runs a captured graph's parallel branches on a set of
+# internal streams; 2 of them measured 2 % faster than the default for this step (alternated runs,
+# tools/env_probe.sh: 2.29-2.30 vs 2.32-2.37 ms).  Read when HIP initialises, so set before any
+# torch.cuda call; an explicit setting in the environment wins.
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
