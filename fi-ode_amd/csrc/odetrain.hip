@@ -31,6 +31,7 @@ using namespace fiode_t16;
 
 struct OTArgs {
   int B, E, niters;
+  int nslots;               // u64 words of xslots zeroed by k_ot_masks before the forward
   float t0, t1, hstep;
   int dropout_mode, bit_mode;
   uint32_t thr8;
@@ -153,9 +154,13 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
 }
 
 // dropout keep words of every (eval, set, row): kw[e][set][b] (uint4 = the 4 words of the 128 units)
+// Also clears the exit-exchange granules (tags) and the status words the forward uses (one launch
+// instead of two memsets ahead of it on the critical path).
 __global__ __launch_bounds__(256) void k_ot_masks(OTArgs a) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= a.E * a.B) return;
+  if (q < a.nslots) a.xslots[q] = 0ull;
+  if (q < 8) a.stats[q] = 0;
+  if (a.dropout_mode == FIODE_DROPOUT_OFF || q >= a.E * a.B) return;
   const int e = q / a.B, b = q - e * a.B;
   const Rng rng = rng_of(a);
 #pragma unroll
@@ -579,13 +584,12 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int ntiles = (a.B + TR - 1) / TR;
   const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);
-  // zero the exchange granules (tags) and the status word before every launch
-  FIODE_HIP_CHECK(hipMemsetAsync(a.xslots, 0, (size_t)a.E * 2 * ntiles * 8 + 256, st));
-  FIODE_HIP_CHECK(hipMemsetAsync(stats, 0, 8 * sizeof(int32_t), st));
-  if (a.dropout_mode != FIODE_DROPOUT_OFF) {
-    hipLaunchKernelGGL(k_ot_masks, dim3((a.E * a.B + 255) / 256), dim3(256), 0, st, a);
-    FIODE_HIP_CHECK(hipGetLastError());
-  }
+  // k_ot_masks zeroes the exchange granules (tags) and the status words before every forward, and
+  // draws the dropout keep words when dropout is on
+  a.nslots = (int)(((size_t)a.E * 2 * ntiles * 8 + 256) / 8);
+  const int nthreads = a.nslots > a.E * a.B ? a.nslots : a.E * a.B;
+  hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_ot_fwd, dim3(ntiles), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
@@ -620,8 +624,11 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
 // per unit upstream gradient, g[b][c] = -1 / (B y_hat[b, y_b]) at c = y_b, else 0.  A label outside
 // [0, C) makes the loss NaN (torch raises a device assert there).
 namespace {
+// mix (nullable): the combined loss of pl_modules.py:500, mix[0] = lyap * (1 - p) + loss_ode * p
+// (the two float32 products rounded, then the sum, as torch evaluates it), and gunit scaled by p.
 __global__ __launch_bounds__(256) void k_ode_nll(int B, const float* __restrict__ y_hat, const int64_t* __restrict__ y,
-                                                 float* __restrict__ loss, float* __restrict__ gunit) {
+                                                 float* __restrict__ loss, float* __restrict__ gunit,
+                                                 const float* __restrict__ lyap, float p, float* __restrict__ mix) {
   __shared__ float red[256];
   const int tid = threadIdx.x;
   float s = 0.f;
@@ -630,7 +637,8 @@ __global__ __launch_bounds__(256) void k_ode_nll(int B, const float* __restrict_
     const bool ok = l >= 0 && l < C;
     const float v = ok ? y_hat[(size_t)b * C + l] : __builtin_nanf("");
     s = s + (-logf(v));
-    const float g = -1.0f / ((float)B * v);
+    const float g0 = -1.0f / ((float)B * v);
+    const float g = mix ? g0 * p : g0;
 #pragma unroll
     for (int c = 0; c < C; ++c) gunit[(size_t)b * C + c] = (c == l) ? g : 0.f;
   }
@@ -641,7 +649,11 @@ __global__ __launch_bounds__(256) void k_ode_nll(int B, const float* __restrict_
     if (tid < o) red[tid] = red[tid] + red[tid + o];
     __syncthreads();
   }
-  if (tid == 0) loss[0] = red[0] / (float)B;
+  if (tid == 0) {
+    const float lo = red[0] / (float)B;
+    loss[0] = lo;
+    if (mix) mix[0] = lyap[0] * (1.0f - p) + lo * p;
+  }
 }
 }  // namespace
 
@@ -649,7 +661,16 @@ extern "C" int fiode_ode_nll(void* stream, int32_t batch, const float* y_hat, co
                              float* g_unit) {
   if (batch <= 0 || !y_hat || !labels || !loss || !g_unit) return FIODE_EINVAL;
   hipLaunchKernelGGL(k_ode_nll, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), batch, y_hat, labels, loss,
-                     g_unit);
+                     g_unit, nullptr, 0.0f, nullptr);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
+
+extern "C" int fiode_ode_loss_mix(void* stream, int32_t batch, const float* y_hat, const int64_t* labels,
+                                  const float* lyap_loss, float portion, float* loss_ode, float* total, float* g_unit) {
+  if (batch <= 0 || !y_hat || !labels || !lyap_loss || !loss_ode || !total || !g_unit) return FIODE_EINVAL;
+  hipLaunchKernelGGL(k_ode_nll, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), batch, y_hat, labels,
+                     loss_ode, g_unit, lyap_loss, portion, total);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }

@@ -136,6 +136,7 @@ def _load():
         "fiode_block_inverse_batched": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_normalize_hwcb": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp]),
         "fiode_ode_nll": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, _vp]),
+        "fiode_ode_loss_mix": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_float, _vp, _vp, _vp]),
         "fiode_small_cayley_forward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp]),
         "fiode_small_cayley_backward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp,
                                                    _vp, _vp]),

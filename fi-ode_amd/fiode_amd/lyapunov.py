@@ -94,6 +94,34 @@ class ODENllFn(torch.autograd.Function):
         return gunit * go, None
 
 
+class ODELossMixFn(torch.autograd.Function):
+    """loss * (1 - p) + F.nll_loss(torch.log(y_hat), y) * p (pl_modules.py:494-500) as ONE kernel
+    forward (fiode_ode_loss_mix, which also writes p * d nll / d y_hat) and two multiplies backward,
+    so the solve's backward starts one kernel after its forward.  Returns (total, loss_ode); the
+    second output is for logging (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, loss, y_hat, y, p: float):
+        yh = y_hat.detach().contiguous().float()
+        B = yh.shape[0]
+        lo = loss.detach().reshape(1).contiguous().float()
+        total = torch.empty((), dtype=torch.float32, device=yh.device)
+        loss_ode = torch.empty((), dtype=torch.float32, device=yh.device)
+        gunit = torch.empty_like(yh)
+        L.check(L.lib().fiode_ode_loss_mix(ops._stream(yh.device), B, yh.data_ptr(), y.contiguous().data_ptr(),
+                                           lo.data_ptr(), float(p), loss_ode.data_ptr(), total.data_ptr(),
+                                           gunit.data_ptr()), "fiode_ode_loss_mix")
+        ctx.save_for_backward(gunit)
+        ctx.p = float(p)
+        ctx.mark_non_differentiable(loss_ode)
+        return total, loss_ode
+
+    @staticmethod
+    def backward(ctx, go, _g_ode):
+        gunit, = ctx.saved_tensors
+        return go * (1.0 - ctx.p), gunit * go, None, None
+
+
 class DecisionBoundary(nn.Module):
     """lya_cands.py:72-94 (kept for the validation/ODE path; the training step fuses it)."""
 
@@ -438,13 +466,15 @@ class LyapunovLearning(nn.Module):
         if isinstance(y_hat, tuple):
             from .cayley import _take
             y_hat = _take(y_hat)
+        p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
+        if (self.simplex and y_hat.is_cuda and y.dtype == torch.int64 and y_hat.dim() == 2 and y_hat.shape[1] == 10
+                and loss.is_cuda):
+            total, loss_ode = ODELossMixFn.apply(loss, y_hat, y, p)
+            self.log("loss_ode", loss_ode)
+            return total
         if self.simplex:
-            if y_hat.is_cuda and y.dtype == torch.int64 and y_hat.dim() == 2 and y_hat.shape[1] == 10:
-                loss_ode = ODENllFn.apply(y_hat, y)
-            else:
-                loss_ode = F.nll_loss(torch.log(y_hat), y)
+            loss_ode = F.nll_loss(torch.log(y_hat), y)
         else:
             loss_ode = F.cross_entropy(y_hat, y)
         self.log("loss_ode", loss_ode)
-        p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
         return loss * (1.0 - p) + loss_ode * p

@@ -207,6 +207,10 @@ FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int
  * gradient in the caller's backward).  labels int64 [B] in [0, C). */
 FIODE_API int fiode_ode_nll(void* stream, int32_t batch, const float* y_hat, const int64_t* labels, float* loss,
                             float* g_unit);
+/* The same fused with the loss mix of pl_modules.py:500: total[0] = lyap_loss[0] * (1 - portion) +
+ * loss_ode * portion; g_unit = portion * d loss_ode / d y_hat (= d total / d y_hat per unit). */
+FIODE_API int fiode_ode_loss_mix(void* stream, int32_t batch, const float* y_hat, const int64_t* labels,
+                                 const float* lyap_loss, float portion, float* loss_ode, float* total, float* g_unit);
 FIODE_API int fiode_odetrain_backward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
                                       const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
                                       fiode_lyap_grads* grads, float* dbg_gft, void* workspace,

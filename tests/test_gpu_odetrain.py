@@ -140,3 +140,28 @@ def test_ode_nll_matches_torch(B):
     torch.cuda.synchronize()
     assert abs(float(la) - float(lb)) <= 1e-6 * max(1.0, abs(float(lb)))
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("p", [0.2, 0.98])
+def test_ode_loss_mix_matches_torch(p):
+    """ODELossMixFn (fiode_ode_loss_mix) = loss * (1 - p) + nll(log y_hat) * p (pl_modules.py:494-500),
+    value and gradients w.r.t. loss and y_hat."""
+    import torch.nn.functional as F
+    from fiode_amd.lyapunov import ODELossMixFn
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(7)
+    yh = torch.softmax(torch.randn(128, 10, generator=g), -1).to(dev)
+    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    l0 = torch.tensor(0.731, device=dev)
+    a, la = yh.clone().requires_grad_(True), l0.clone().requires_grad_(True)
+    b, lb = yh.clone().requires_grad_(True), l0.clone().requires_grad_(True)
+    ta, ode_a = ODELossMixFn.apply(la, a, y, p)
+    ode_b = F.nll_loss(torch.log(b), y)
+    tb = lb * (1.0 - p) + ode_b * p
+    (ta * 1.3).backward()
+    (tb * 1.3).backward()
+    torch.cuda.synchronize()
+    assert abs(float(ta) - float(tb)) <= 2e-6 * max(1.0, abs(float(tb)))
+    assert abs(float(ode_a) - float(ode_b)) <= 1e-6 * max(1.0, abs(float(ode_b)))
+    torch.testing.assert_close(la.grad, lb.grad, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
