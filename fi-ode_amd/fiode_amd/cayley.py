@@ -368,9 +368,11 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
 # Backward placement of the prefetched maps.  autograd runs a node's backward on the stream its
 # forward ran on (a side stream); with these flags the backward of the spectral / dense maps runs
 # on the stream the step was launched from instead (set by LyapunovLearning.compute_loss), which
-# the hipGraph executor places on another hardware queue.
+# the hipGraph executor places on another hardware queue.  With the executor on 2 internal
+# streams (bench.py) the dense maps' backward on the step stream measured 2.28 -> 2.24 ms per step
+# in the interleaved A/B (tools/ab_step.py); the spectral maps' is slower there (2.35 ms).
 SPECTRAL_BWD_ON_MAIN = False
-DENSE_BWD_ON_MAIN = False
+DENSE_BWD_ON_MAIN = True
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 
 

@@ -79,9 +79,42 @@ def grouped_ai_linfirst(m):
     m.prefetch_schedule = {"after_input": True, "order": "lin_first"}
 
 
-VARIANTS = {"default(after_input)": lambda m: None, "grouped": grouped_ai, "grouped_lin_first": grouped_ai_linfirst}
+def lin_first(m):
+    m.prefetch_schedule = {"after_input": True, "order": "lin_first"}
+
+
+def dense_bwd_main(m):
+    from fiode_amd import cayley
+    cayley.DENSE_BWD_ON_MAIN = True
+
+
+def dense_bwd_side(m):
+    from fiode_amd import cayley
+    cayley.DENSE_BWD_ON_MAIN = False
+
+
+def both_bwd_main(m):
+    from fiode_amd import cayley
+    cayley.DENSE_BWD_ON_MAIN = True
+    cayley.SPECTRAL_BWD_ON_MAIN = True
+
+
+def reset(m):
+    from fiode_amd import cayley
+    cayley.DENSE_BWD_ON_MAIN = False
+    cayley.SPECTRAL_BWD_ON_MAIN = False
+
+
+def dense_bwd_side(m):
+    reset(m)
+
+
+VARIANTS = {"default": dense_bwd_side, "dense_bwd_main": dense_bwd_main, "both_bwd_main": both_bwd_main}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
-steps = {k: make(f) for k, f in VARIANTS.items()}
+steps = {}
+for k, f in VARIANTS.items():
+    steps[k] = make(f)
+    reset(None)                     # flags only matter at capture time (inside make)
 times = {k: [] for k in VARIANTS}
 for r in range(rounds):
     for k, gs in steps.items():
