@@ -307,6 +307,10 @@ class _SmallCayleyFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gQ):
+        return _run_on_step_stream(SMALL_BWD_ON_MAIN, lambda: _SmallCayleyFn._backward(ctx, gQ))
+
+    @staticmethod
+    def _backward(ctx, gQ):
         from . import ops, _lib as L
         Wb, al, nrm, inv = ctx.saved_tensors
         wshape, ashape = ctx.shapes
@@ -373,6 +377,7 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
 # in the interleaved A/B (tools/ab_step.py); the spectral maps' is slower there (2.35 ms).
 SPECTRAL_BWD_ON_MAIN = False
 DENSE_BWD_ON_MAIN = True
+SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 
 

@@ -454,7 +454,7 @@ class LyapunovLearning(nn.Module):
         plan = self.ode_plan(static_state.shape[0], masks)
         args = (static_state, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"], w["b3"], h0, plan)
         self.last_ode_plan = plan
-        if static_state.is_cuda and self.parallel_cayley:
+        if static_state.is_cuda and self.parallel_cayley and getattr(self, "ode_side_stream", True):
             from .cayley import _prefetch
             if getattr(self, "_ode_stream", None) is None:
                 self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)

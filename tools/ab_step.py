@@ -109,12 +109,28 @@ def dense_bwd_side(m):
     reset(m)
 
 
-VARIANTS = {"default": dense_bwd_side, "dense_bwd_main": dense_bwd_main, "both_bwd_main": both_bwd_main}
+def reset2(m):
+    from fiode_amd import cayley
+    cayley.DENSE_BWD_ON_MAIN = True
+    cayley.SPECTRAL_BWD_ON_MAIN = False
+    cayley.SMALL_BWD_ON_MAIN = False
+
+
+def small_bwd_main(m):
+    from fiode_amd import cayley
+    cayley.SMALL_BWD_ON_MAIN = True
+
+
+def ode_on_main(m):
+    m.ode_side_stream = False
+
+
+VARIANTS = {"default": reset2, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 steps = {}
 for k, f in VARIANTS.items():
     steps[k] = make(f)
-    reset(None)                     # flags only matter at capture time (inside make)
+    reset2(None)                    # flags only matter at capture time (inside make)
 times = {k: [] for k in VARIANTS}
 for r in range(rounds):
     for k, gs in steps.items():
