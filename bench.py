@@ -33,10 +33,10 @@ for _p in (ROOT, ROOT / "fi-ode_amd"):
         sys.path.insert(0, str(_p))
 
 # The hipGraph executor of this ROCm runs a captured graph's parallel branches on a set of
-# internal streams; 2 of them measured 2 % faster than the default for this step (alternated runs,
-# tools/env_probe.sh: 2.29-2.30 vs 2.32-2.37 ms).  Read when HIP initialises, so set before any
-# torch.cuda call; an explicit setting in the environment wins.
-os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
+# internal streams; 3 of them measured fastest for this step (alternated runs, tools/env_probe.sh:
+# 3: 2.23-2.24 ms, 2: 2.24-2.27, 4: 2.28-2.29, default: 2.32-2.37).  Read when HIP initialises,
+# so set before any torch.cuda call; an explicit setting in the environment wins.
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "3")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
