@@ -67,6 +67,9 @@ struct LyapArgs {
   // outputs
   float* scalars;
   float *h_out, *V, *Vdot, *f, *f_log, *qp_lower, *qp_nominal, *g_ftilde;
+  const float* exp_draws;    // optional given Exp(1) variates (parity), else Philox
+  float* exp_draws_out;      // optional: the variates used
+  uint32_t* kw_out;          // optional: [4][N][4] keep words
   fiode_lyap_grads grads;
 };
 
@@ -78,6 +81,26 @@ __device__ __forceinline__ void draws10(const Rng& rng, uint32_t index, uint32_t
   for (int j = 0; j < C; ++j) e[j] = exp1_from_bits(w[j]);
 }
 
+// The n (<= C) Exp(1) variates of one sampler draw row: read from the caller's draws (parity
+// mode) or drawn from Philox (index, stream); draw_row indexes the reference's draw tensor (see
+// fiode_lyap_io.exp_draws), `publish` = this lane owns the row of exp_draws_out.
+__device__ __forceinline__ void row_draws(const LyapArgs& a, size_t draw_row, int n, bool publish, uint32_t index,
+                                          uint32_t stream, float (&e)[C]) {
+  if (a.exp_draws) {
+    const float* p = a.exp_draws + draw_row * n;
+#pragma unroll
+    for (int j = 0; j < C; ++j) e[j] = j < n ? p[j] : 0.f;
+  } else {
+    draws10(a.rng, index, stream, e);
+  }
+  if (a.exp_draws_out && publish) {
+    float* q = a.exp_draws_out + draw_row * n;
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      if (j < n) q[j] = e[j];
+  }
+}
+
 __device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C]) {
   if (a.sampler == FIODE_SAMPLER_GIVEN) {
     load_row10(a.h_in + (size_t)row * C, h);
@@ -86,14 +109,14 @@ __device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C])
   const int b = row / a.S, s = row - b * a.S;
   if (a.sampler == FIODE_SAMPLER_COMPOSITE || a.sampler == FIODE_SAMPLER_TRAJECTORY) {
     if (s < a.S1) {                      // UniformSimplexSampling, shared over the batch (sampler.py:209-210)
-      draws10(a.rng, (uint32_t)s, RNG_STREAM_UNIFORM, h);
+      row_draws(a, (size_t)s, C, b == 0, (uint32_t)s, RNG_STREAM_UNIFORM, h);
       l1_normalize(h);
     } else if (a.sampler == FIODE_SAMPLER_TRAJECTORY) {
       // TrajectorySampler (sampler.py:156-166): the solve's states at linspace(0, t_max, S - S1),
       // given as [B][S - S1][C] (the per-image trajectory, transpose(0, 1) of odeint's output)
       load_row10(a.h_in + ((size_t)b * (a.S - a.S1) + (s - a.S1)) * C, h);
     } else {                             // CorrectConeSampling (sampler.py:113-128)
-      draws10(a.rng, (uint32_t)row, RNG_STREAM_CONE, h);
+      row_draws(a, (size_t)a.S1 + (size_t)b * (a.S - a.S1) + (s - a.S1), C, true, (uint32_t)row, RNG_STREAM_CONE, h);
       l1_normalize(h);
       int am = 0;
       float mx = h[0];
@@ -111,7 +134,7 @@ __device__ void sample_row(const LyapArgs& a, int row, int label, float (&h)[C])
     }
   } else {                               // DecisionBoundarySampling (sampler.py:139-153)
     float z[C];
-    draws10(a.rng, (uint32_t)row, RNG_STREAM_DB, z);
+    row_draws(a, (size_t)row, C - 1, true, (uint32_t)row, RNG_STREAM_DB, z);
     float raw[C];
     float zm = z[0];
 #pragma unroll
@@ -168,6 +191,8 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
     uint32_t kw[4];
     keep_words(a, row, set, kw);
     a.kw[(size_t)set * a.N + row] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+    if (a.kw_out)
+      reinterpret_cast<uint4*>(a.kw_out)[(size_t)set * a.N + row] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
   }
 }
 
@@ -609,6 +634,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.scalars = io->scalars;
   a.h_out = io->h_out; a.V = io->V; a.Vdot = io->Vdot; a.f = io->f; a.f_log = io->f_log;
   a.qp_lower = io->qp_lower; a.qp_nominal = io->qp_nominal; a.g_ftilde = io->g_ftilde;
+  a.exp_draws = io->exp_draws; a.exp_draws_out = io->exp_draws_out; a.kw_out = io->keep_words_out;
   a.grads = *grads;
 
   hipStream_t st = static_cast<hipStream_t>(stream);

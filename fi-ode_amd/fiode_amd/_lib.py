@@ -47,7 +47,8 @@ class LyapConfig(ct.Structure):
 class LyapIO(ct.Structure):
     _fields_ = [(n, ct.c_void_p) for n in ("x_feat", "y", "h", "masks", "scalars", "h_out", "V", "Vdot",
                                            "f", "f_log", "qp_lower", "qp_nominal", "g_ftilde", "events")] + \
-        [("n_events", ct.c_int32), ("offset_dev", ct.c_void_p)]
+        [("n_events", ct.c_int32), ("offset_dev", ct.c_void_p), ("exp_draws", ct.c_void_p),
+         ("exp_draws_out", ct.c_void_p), ("keep_words_out", ct.c_void_p)]
 
 
 LYAP_KERNELS = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_wgrad", "k_lyap_reduce",

@@ -75,16 +75,33 @@ def _weights_c(w: Dict[str, torch.Tensor], dev) -> tuple:
     return ws, L.DynWeights(*[ws[k].data_ptr() for k in WEIGHT_KEYS])
 
 
+def sampler_draws_count(sampler: int, B: int, S: int, n_uniform: int) -> int:
+    """Number of Exp(1) variates one fiode_lyap_step sampler consumes (fiode_lyap_io.exp_draws):
+    COMPOSITE [S1][C] + [B][S-S1][C]; TRAJECTORY [S1][C]; DECISION_BOUNDARY [B][S][C-1]."""
+    if sampler == L.FIODE_SAMPLER_COMPOSITE:
+        return n_uniform * C + B * (S - n_uniform) * C
+    if sampler == L.FIODE_SAMPLER_TRAJECTORY:
+        return n_uniform * C
+    if sampler == L.FIODE_SAMPLER_DECISION_BOUNDARY:
+        return B * S * (C - 1)
+    return 0
+
+
 def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg, *,
               sample_size: int, n_uniform: int, sampler: int = L.FIODE_SAMPLER_COMPOSITE,
               dropout_mode: int = L.FIODE_DROPOUT_PHILOX, kappa: float = 2.0, seed: int = 0, offset: int = 0,
               h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None, debug: bool = False,
-              out: Optional[dict] = None, events=None, offset_dev: Optional[torch.Tensor] = None):
+              out: Optional[dict] = None, events=None, offset_dev: Optional[torch.Tensor] = None,
+              exp_draws: Optional[torch.Tensor] = None):
     """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict).
     ``events``: optional list of len(_lib.LYAP_KERNELS)+1 torch.cuda.Event(enable_timing=True),
     recorded by the library around each of its kernels on the current stream.
     ``offset_dev``: optional int64 [1] device tensor added to ``offset`` by the kernels (a captured
-    graph of the step advances it on every replay)."""
+    graph of the step advances it on every replay).
+    ``exp_draws``: optional flat float32 Exp(1) variates for the sampler (``sampler_draws_count``
+    of them, the reference's draw shapes) instead of the in-kernel Philox draws.
+    ``debug``: also returns the per-row outputs, the Exp(1) variates the sampler used
+    (``exp_draws``) and the dropout keep words (``keep_words`` int32 [4, N, 4])."""
     dev = x_feat.device
     B = x_feat.shape[0]
     S = int(sample_size)
@@ -93,6 +110,11 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
     y = _need(y, "y", (B,), torch.int64, dev)
     if not (0 <= n_uniform <= S):
         raise ValueError("n_uniform must be in [0, sample_size]")
+    n_draws = sampler_draws_count(sampler, B, S, n_uniform)
+    if exp_draws is not None:
+        if n_draws == 0:
+            raise ValueError("exp_draws needs a drawing sampler (COMPOSITE, TRAJECTORY, DECISION_BOUNDARY)")
+        exp_draws = _need(exp_draws.reshape(-1), "exp_draws", (n_draws,), torch.float32, dev)
     if sampler == L.FIODE_SAMPLER_GIVEN:
         if h is None:
             raise ValueError("sampler GIVEN needs h")
@@ -124,7 +146,10 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
         dbg = dict(h=torch.empty((N, C), device=dev), V=torch.empty(N, device=dev), Vdot=torch.empty(N, device=dev),
                    f=torch.empty((N, C), device=dev), f_log=torch.empty((N, C), device=dev),
                    qp_lower=torch.empty((N, C), device=dev), qp_nominal=torch.empty((2, N, C), device=dev),
-                   g_ftilde=torch.empty((N, C), device=dev))
+                   g_ftilde=torch.empty((N, C), device=dev),
+                   keep_words=torch.empty((4, N, 4), dtype=torch.int32, device=dev))
+        if n_draws:
+            dbg["exp_draws"] = torch.empty(n_draws, dtype=torch.float32, device=dev)
     cfg = L.LyapConfig(B, S, int(n_uniform), int(sampler), int(dropout_mode), float(kappa),
                        int(seed) & (2**64 - 1), int(offset) & (2**64 - 1))
     dc = dyn.to_c()
@@ -142,7 +167,7 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
                   _ptr(dbg.get("h")), _ptr(dbg.get("V")), _ptr(dbg.get("Vdot")), _ptr(dbg.get("f")),
                   _ptr(dbg.get("f_log")), _ptr(dbg.get("qp_lower")), _ptr(dbg.get("qp_nominal")),
                   _ptr(dbg.get("g_ftilde")), ct.cast(ev_arr, ct.c_void_p) if ev_arr is not None else None, n_ev,
-                  _ptr(offset_dev))
+                  _ptr(offset_dev), _ptr(exp_draws), _ptr(dbg.get("exp_draws")), _ptr(dbg.get("keep_words")))
     cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
     lib = L.lib()
     nbytes = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dc))

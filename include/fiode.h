@@ -103,6 +103,14 @@ typedef struct fiode_lyap_io {
    * so a captured hipGraph of the step draws fresh samples / dropout masks on every replay when
    * the graph also advances the counter */
   const uint64_t* offset_dev;
+  /* optional sampler draws (parity checks): NULL = in-kernel Philox.  Exp(1) variates in the
+   * reference's draw shapes (sampler.py:36, 116, 142): COMPOSITE / TRAJECTORY: UniformSimplex
+   * [n_uniform][C] followed by CorrectCone [B][S - n_uniform][C] (TRAJECTORY: the uniform part
+   * only); DECISION_BOUNDARY: [B][S][C - 1]. */
+  const float* exp_draws;
+  float* exp_draws_out;     /* optional out: the Exp(1) variates the sampler used, same layout  */
+  uint32_t* keep_words_out; /* optional out: [4][N][4] dropout keep words of the 4 mask sets
+                               (bit t of word mb = keep hidden unit 32 mb + t)                  */
 } fiode_lyap_io;
 
 /* kernels of one fiode_lyap_step, in launch order (for the profiling events) */
