@@ -260,6 +260,17 @@ __device__ __forceinline__ void qp_backward_row(const float (&g)[FIODE_C], const
   }
 }
 
+// Test hook of the persistent solves' exchanges (host side): FIODE_DEBUG_DROP_PUBLISH=<block> makes
+// that workgroup skip its first publish, as if it were never resident, so tests can exercise the
+// bounded-spin timeout path (status 4, poisoned outputs).  Unset: -1.
+#include <stdlib.h>
+namespace fiode_internal {
+inline int debug_drop_publish() {
+  const char* e = getenv("FIODE_DEBUG_DROP_PUBLISH");
+  return (e && *e) ? atoi(e) : -1;
+}
+}  // namespace fiode_internal
+
 // Return code helpers for the C-ABI layer.
 #define FIODE_HIP_CHECK(expr)                       \
   do {                                              \

@@ -35,6 +35,7 @@ constexpr int OS_XV = 4;         // float64 values per reduction exchange (at mo
 struct OsArgs {
   int B, n_times, method, max_steps;
   int T, ntiles;                 // tiles per workgroup, tiles
+  int drop_block;                // test hook: workgroup that skips its first publish (-1: none)
   double rtol, atol, step_size;
   DynScalars d;
   const float* x_feat;
@@ -42,7 +43,8 @@ struct OsArgs {
   const double* times;
   const float *Q1, *b1, *Qx, *bx, *Q2, *b2, *Q3, *b3;
   float* sol;                    // [n_times][B][C]
-  int32_t* stats;                // [8]: nfe, n_accept, n_reject, status, last exit iter, n_steps
+  int32_t* stats;                // [8]: nfe, n_accept, n_reject, status, last exit iter, n_steps, workgroups,
+                                 //      tiles per workgroup
   double* dstats;                // [4]: final dt, t reached, last error ratio
   // workspace
   float* u;                      // [B][M]
@@ -67,7 +69,7 @@ struct OsShared {
   int K;                         // exit iteration of the current eval
   int kprev;                     // previous eval's exit (speculation)
   int dead;                      // an exchange timed out: stop waiting (status 4 recorded)
-  int pad;
+  int nx;                        // exchanges the current eval used (1, or 2 after a resume)
 };
 
 __device__ __forceinline__ bool owner_lane() { return threadIdx.x < 16; }   // wave 0, q = 0
@@ -77,7 +79,7 @@ __device__ __forceinline__ bool owner_lane() { return threadIdx.x < 16; }   // w
 // exchanges ahead of another, so two buffers suffice).
 __device__ uint32_t xchg_and(const OsArgs& a, OsShared& sh, unsigned ep, uint32_t mine, int lane) {
   unsigned long long* buf = a.xm + (size_t)(ep & 1u) * gridDim.x;
-  if (lane == 0) publish_mask(buf + blockIdx.x, ep, mine);
+  if (lane == 0 && !(ep == 1u && (int)blockIdx.x == a.drop_block)) publish_mask(buf + blockIdx.x, ep, mine);
   uint32_t acc = 0xFFFFFFFFu;
   const int G = gridDim.x;
   for (int base = 0; base < G; base += 64) {
@@ -193,11 +195,73 @@ __device__ void batch_sum(const OsArgs& a, OsShared& sh, unsigned& ep, double (&
   __syncthreads();
 }
 
-// ---- one eval: k[kdst] = eval_dot(input) for every row of the batch ------------------------
-// input(bb, h): the stage input of row bb (every lane of the row computes it from the global state).
-template <class Input>
-__device__ int os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsShared& sh, OsTile* tl, unsigned& ep,
-                       int kdst, Input input) {
+// ---- stage inputs (every lane of a row computes its row's from the global state) ------------
+enum { IN_Y = 0, IN_RK4_2, IN_RK4_3, IN_RK4_4, IN_DP, IN_H0 };
+struct StageIn {
+  int kind;        // IN_*
+  int i;           // dopri5 stage (IN_DP)
+  float dt;        // step (rk4, dopri5) or h0 (IN_H0)
+};
+
+// torchdiffeq 0.2.2 dopri5 tableau (float32 copies, as RKAdaptiveStepsizeODESolver casts it)
+__device__ const float DP_BETA[6][6] = {
+    {1.0f / 5, 0, 0, 0, 0, 0},
+    {3.0f / 40, 9.0f / 40, 0, 0, 0, 0},
+    {(float)(44.0 / 45), (float)(-56.0 / 15), (float)(32.0 / 9), 0, 0, 0},
+    {(float)(19372.0 / 6561), (float)(-25360.0 / 2187), (float)(64448.0 / 6561), (float)(-212.0 / 729), 0, 0},
+    {(float)(9017.0 / 3168), (float)(-355.0 / 33), (float)(46732.0 / 5247), (float)(49.0 / 176),
+     (float)(-5103.0 / 18656), 0},
+    {(float)(35.0 / 384), 0, (float)(500.0 / 1113), (float)(125.0 / 192), (float)(-2187.0 / 6784),
+     (float)(11.0 / 84)}};
+
+// The float32 expression orders of the oracle / torchdiffeq: rk4_alt_step_func (3/8 rule) and the
+// dopri5 stage sums acc = sum_j k_j (beta_ij dt), y_i = y + acc.
+__device__ __forceinline__ void stage_input(const OsArgs& a, const StageIn& in, int bb, float (&h)[C]) {
+  const size_t BC = (size_t)a.B * C;
+  const float* Kr = a.K + (size_t)bb * C;
+  float y[C];
+  load_row10(a.y + (size_t)bb * C, y);
+  const float third = 1.0f / 3.0f, dt = in.dt;
+  if (in.kind == IN_Y) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) h[c] = y[c];
+  } else if (in.kind == IN_DP) {
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+    for (int jj = 0; jj <= in.i; ++jj) {
+      float f[C];
+      load_row10(Kr + (size_t)jj * BC, f);
+      const float co = DP_BETA[in.i][jj] * dt;
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) h[c] = y[c] + acc[c];
+  } else {
+    float f1[C], f2[C], f3[C];
+    load_row10(Kr, f1);
+    if (in.kind == IN_H0 || in.kind == IN_RK4_2) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) h[c] = in.kind == IN_H0 ? y[c] + dt * f1[c] : y[c] + (dt * f1[c]) * third;
+    } else {
+      load_row10(Kr + BC, f2);
+      if (in.kind == IN_RK4_3) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) h[c] = y[c] + dt * (f2[c] - f1[c] * third);
+      } else {
+        load_row10(Kr + 2 * BC, f3);
+#pragma unroll
+        for (int c = 0; c < C; ++c) h[c] = y[c] + dt * ((f1[c] - f2[c]) + f3[c]);
+      }
+    }
+  }
+}
+
+// ---- one eval: k[kdst] = eval_dot(stage input) for every row of the batch -------------------
+// Uses exchange epochs ep (and ep + 1 after a resume); returns the next free epoch.
+__device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsShared& sh, OsTile* tl,
+                                    unsigned ep, int kdst, StageIn in) {
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool own = owner_lane();
@@ -211,7 +275,7 @@ __device__ int os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
     const bool valid = b < a.B;
     const int bb = valid ? b : a.B - 1;
     float h[C];
-    input(bb, h);
+    stage_input(a, in, bb, h);
     f32x4v uacc[8];
 #pragma unroll
     for (int hb = 0; hb < 8; ++hb) {
@@ -244,9 +308,11 @@ __device__ int os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
     const uint32_t all = xchg_and(a, sh, ep, wconv, lane);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
-    if (lane == 0) sh.K = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
+    if (lane == 0) {
+      sh.K = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
+      sh.nx = 1;
+    }
   }
-  ++ep;
   __syncthreads();
   if (sh.K < 0) {             // block-uniform: no speculated iteration converged everywhere
     uint32_t wc2 = 0xFFFFFFFFu;
@@ -264,13 +330,16 @@ __device__ int os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
       wc2 &= qp_bisect_range2(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, q, j);
     }
     if (p == 0) {
-      const uint32_t all = xchg_and(a, sh, ep, wc2, lane);
-      if (lane == 0) sh.K = qp_exit_iter(all, a.d.max_iter);
+      const uint32_t all = xchg_and(a, sh, ep + 1, wc2, lane);
+      if (lane == 0) {
+        sh.K = qp_exit_iter(all, a.d.max_iter);
+        sh.nx = 2;
+      }
     }
-    ++ep;
     __syncthreads();
   }
   const int K = sh.K;
+  const unsigned ep_next = ep + (unsigned)sh.nx;
   // finalize: k = v(mu_K) (barrier_projection.py:251-253 at the exit iteration), owner lanes store
   if (own) {
     for (int t = 0; t < a.T; ++t) {
@@ -294,7 +363,7 @@ __device__ int os_eval(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
     if (blockIdx.x == 0) a.stats[0] += 1;
   }
   __syncthreads();
-  return K;
+  return ep_next;
 }
 
 // iterate the owner lane's valid rows: fn(b)
@@ -313,7 +382,6 @@ __device__ void os_rk4(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
   unsigned ep = 1;
   const float t0 = (float)a.times[0], t1 = (float)a.times[a.n_times - 1], hs = (float)a.step_size;
   const int niters = (int)ceilf((t1 - t0) / hs + 1.0f);
-  const float third = 1.0f / 3.0f;
   const size_t BC = (size_t)a.B * C;
   const float* k1 = a.K;
   const float* k2 = a.K + BC;
@@ -324,31 +392,10 @@ __device__ void os_rk4(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
     const float ta = (float)it * hs + t0;
     const float tb = (it + 2 == niters) ? t1 : (float)(it + 1) * hs + t0;
     const float dt = tb - ta;
-    os_eval(a, Q2s, Q3s, sh, tl, ep, 0, [&](int bb, float (&h)[C]) { load_row10(a.y + (size_t)bb * C, h); });
-    os_eval(a, Q2s, Q3s, sh, tl, ep, 1, [&](int bb, float (&h)[C]) {
-      float y[C], f1[C];
-      load_row10(a.y + (size_t)bb * C, y);
-      load_row10(k1 + (size_t)bb * C, f1);
-#pragma unroll
-      for (int i = 0; i < C; ++i) h[i] = y[i] + (dt * f1[i]) * third;
-    });
-    os_eval(a, Q2s, Q3s, sh, tl, ep, 2, [&](int bb, float (&h)[C]) {
-      float y[C], f1[C], f2[C];
-      load_row10(a.y + (size_t)bb * C, y);
-      load_row10(k1 + (size_t)bb * C, f1);
-      load_row10(k2 + (size_t)bb * C, f2);
-#pragma unroll
-      for (int i = 0; i < C; ++i) h[i] = y[i] + dt * (f2[i] - f1[i] * third);
-    });
-    os_eval(a, Q2s, Q3s, sh, tl, ep, 3, [&](int bb, float (&h)[C]) {
-      float y[C], f1[C], f2[C], f3[C];
-      load_row10(a.y + (size_t)bb * C, y);
-      load_row10(k1 + (size_t)bb * C, f1);
-      load_row10(k2 + (size_t)bb * C, f2);
-      load_row10(k3 + (size_t)bb * C, f3);
-#pragma unroll
-      for (int i = 0; i < C; ++i) h[i] = y[i] + dt * ((f1[i] - f2[i]) + f3[i]);
-    });
+    ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 0, StageIn{IN_Y, 0, dt});
+    ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 1, StageIn{IN_RK4_2, 0, dt});
+    ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 2, StageIn{IN_RK4_3, 0, dt});
+    ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 3, StageIn{IN_RK4_4, 0, dt});
     const int j0 = jo;
     while (jo < a.n_times && tb >= (float)a.times[jo]) ++jo;   // outputs in (ta, tb], uniform
     for_own_rows(a, [&](int b) {
@@ -378,16 +425,6 @@ __device__ void os_rk4(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
   }
 }
 
-// torchdiffeq 0.2.2 dopri5 tableau (float32 copies, as RKAdaptiveStepsizeODESolver casts it)
-__device__ const float DP_BETA[6][6] = {
-    {1.0f / 5, 0, 0, 0, 0, 0},
-    {3.0f / 40, 9.0f / 40, 0, 0, 0, 0},
-    {(float)(44.0 / 45), (float)(-56.0 / 15), (float)(32.0 / 9), 0, 0, 0},
-    {(float)(19372.0 / 6561), (float)(-25360.0 / 2187), (float)(64448.0 / 6561), (float)(-212.0 / 729), 0, 0},
-    {(float)(9017.0 / 3168), (float)(-355.0 / 33), (float)(46732.0 / 5247), (float)(49.0 / 176),
-     (float)(-5103.0 / 18656), 0},
-    {(float)(35.0 / 384), 0, (float)(500.0 / 1113), (float)(125.0 / 192), (float)(-2187.0 / 6784),
-     (float)(11.0 / 84)}};
 __device__ const float DP_CERR[7] = {(float)(35.0 / 384 - 1951.0 / 21600), 0, (float)(500.0 / 1113 - 22642.0 / 50085),
                                      (float)(125.0 / 192 - 451.0 / 720), (float)(-2187.0 / 6784 - -12231.0 / 42400),
                                      (float)(11.0 / 84 - 649.0 / 6300), (float)(-1.0 / 60.0)};
@@ -405,7 +442,7 @@ __device__ void os_dopri5(const OsArgs& a, const float* Q2s, const float* Q3s, O
   const float rtol = (float)a.rtol, atol = (float)a.atol;
   const float* K0 = a.K;
   // ---- _select_initial_step(order - 1 = 4), float32 -------------------------------------------
-  os_eval(a, Q2s, Q3s, sh, tl, ep, 0, [&](int bb, float (&h)[C]) { load_row10(a.y + (size_t)bb * C, h); });
+  ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 0, StageIn{IN_Y, 0, 0.f});
   double s01[2] = {0.0, 0.0};
   for_own_rows(a, [&](int b) {
     float y[C], f0[C];
@@ -423,13 +460,7 @@ __device__ void os_dopri5(const OsArgs& a, const float* Q2s, const float* Q3s, O
   const float d0 = rms_from_sum(s01[0], BC);
   const float d1 = rms_from_sum(s01[1], BC);
   const float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
-  os_eval(a, Q2s, Q3s, sh, tl, ep, 1, [&](int bb, float (&h)[C]) {        // f1 at t0 + h0
-    float y[C], f0[C];
-    load_row10(a.y + (size_t)bb * C, y);
-    load_row10(K0 + (size_t)bb * C, f0);
-#pragma unroll
-    for (int i = 0; i < C; ++i) h[i] = y[i] + h0 * f0[i];
-  });
+  ep = os_eval(a, Q2s, Q3s, sh, tl, ep, 1, StageIn{IN_H0, 0, h0});      // f1 at t0 + h0
   double s2[1] = {0.0};
   for_own_rows(a, [&](int b) {
     float y[C], f0[C], f1[C];
@@ -467,21 +498,7 @@ __device__ void os_dopri5(const OsArgs& a, const float* Q2s, const float* Q3s, O
       ++nsteps;
       const float dt32 = (float)dt;
       for (int i = 0; i < 6; ++i) {
-        os_eval(a, Q2s, Q3s, sh, tl, ep, i + 1, [&](int bb, float (&h)[C]) {
-          float y[C], acc[C];
-          load_row10(a.y + (size_t)bb * C, y);
-#pragma unroll
-          for (int c = 0; c < C; ++c) acc[c] = 0.f;
-          for (int jj = 0; jj <= i; ++jj) {
-            float f[C];
-            load_row10(a.K + (size_t)jj * BC + (size_t)bb * C, f);
-            const float co = DP_BETA[i][jj] * dt32;
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
-          }
-#pragma unroll
-          for (int c = 0; c < C; ++c) h[c] = y[c] + acc[c];
-        });
+        ep = os_eval(a, Q2s, Q3s, sh, tl, ep, i + 1, StageIn{IN_DP, i, dt32});
       }
       // y1 = the stage-6 input (FSAL tableau); batch-global RMS error ratio
       double ps[1] = {0.0};
@@ -623,7 +640,11 @@ __global__ __launch_bounds__(256) void k_ode_tiles(OsArgs a) {
   __syncthreads();
   if (a.method == FIODE_ODE_RK4) os_rk4(a, Q2s, Q3s, sh, tl);
   else os_dopri5(a, Q2s, Q3s, sh, tl);
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.stats[4] = sh.kprev;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.stats[4] = sh.kprev;
+    a.stats[6] = (int)gridDim.x;
+    a.stats[7] = a.T;
+  }
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -696,6 +717,7 @@ extern "C" int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fio
   a.x_feat = x_feat; a.h0 = h0; a.times = times;
   a.Q1 = w->Q1; a.b1 = w->b1; a.Qx = w->Qx; a.bx = w->bx; a.Q2 = w->Q2; a.b2 = w->b2; a.Q3 = w->Q3; a.b3 = w->b3;
   a.sol = solution; a.stats = stats; a.dstats = dstats;
+  a.drop_block = fiode_internal::debug_drop_publish();
   // tiles -> workgroups: one tile per workgroup while they fit the resident capacity, else T each
   a.ntiles = (a.B + TR - 1) / TR;
   const int cap = os_capacity(os_lds_bytes(OS_TMAX));

@@ -38,6 +38,7 @@ struct OTArgs {
   float drop_scale;
   Rng rng;
   const uint64_t* offset_dev;
+  int drop_block;           // test hook: workgroup that skips its first exit publish (-1: none)
   DynScalars d;
   const float* x_feat;
   const float* h0;
@@ -104,7 +105,8 @@ struct OtShared {
   float Q1s[M * C];
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
-  int pad[2];
+  int dead;                   // an exit exchange timed out (status 4): stop waiting, poison y_out
+  int pad;
 };
 
 #ifdef OT_PROFILE
@@ -135,7 +137,7 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][j][0];
   qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
-            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K);
+            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead, a.drop_block);
   OT_MARK(3);
   const int K = sh.K;
   const float mu = sh.mu_rec[p][j][K];
@@ -180,7 +182,10 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   OtShared& sh = *reinterpret_cast<OtShared*>(smem + (M + 32) * LDQ);
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
   for (int t = threadIdx.x; t < M * C; t += blockDim.x) sh.Q1s[t] = a.Q1[t];
-  if (threadIdx.x == 0) sh.Kprev = a.d.max_iter - 1;
+  if (threadIdx.x == 0) {
+    sh.Kprev = a.d.max_iter - 1;
+    sh.dead = 0;
+  }
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x * TR + j;
@@ -249,6 +254,10 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
       const float dy = (((k1[i] + 3.0f * (k2[i] + k3[i])) + k4[i]) * dt) * 0.125f;
       y[i] = y[i] + dy;
     }
+  }
+  if (sh.dead) {              // this tile's QP exits came from a partial AND: make the loss NaN
+#pragma unroll
+    for (int i = 0; i < C; ++i) y[i] = __builtin_nanf("");
   }
   if (p == 0 && valid && q == 0) store_row10(a.y_out + (size_t)b * C, y);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -581,6 +590,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   if (!h0 || !y_out || !stats) return FIODE_EINVAL;
   if (a.dropout_mode == FIODE_DROPOUT_GIVEN && !masks) return FIODE_EINVAL;
   a.h0 = h0; a.masks = masks; a.offset_dev = offset_dev; a.y_out = y_out; a.stats = stats;
+  a.drop_block = fiode_internal::debug_drop_publish();
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int ntiles = (a.B + TR - 1) / TR;
   const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);

@@ -51,9 +51,12 @@ __device__ __forceinline__ void publish_mask(unsigned long long* slot, unsigned 
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...)
+// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...).
+// Bounded: after ~0.5 s without every tag (a tile not resident) it records status 4, sets the
+// workgroup's sticky `dead` flag (LDS) -- later exchanges of this workgroup then stop waiting at
+// once -- and returns the partial AND; the caller poisons its outputs (see k_ot_fwd).
 __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int ntiles, unsigned epoch,
-                                                 int32_t* status, int lane) {
+                                                 int32_t* status, int lane, int& dead) {
   uint32_t acc = 0xFFFFFFFFu;
   for (int base = 0; base < ntiles; base += 64) {
     const int t = base + lane;
@@ -69,8 +72,11 @@ __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int 
         if (t < ntiles) acc &= (uint32_t)x;
         break;
       }
-      if (++spins > (1u << 22)) {           // ~0.5 s: a non-resident tile; record and give up
-        if (lane == 0) atomicMax(status, 4);
+      if (dead || ++spins > (1u << 22)) {   // ~0.5 s: a non-resident tile; record and give up
+        if (lane == 0) {
+          atomicMax(status, 4);
+          dead = 1;
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -241,7 +247,8 @@ __device__ __forceinline__ void ft16_sum(const float (*zpart)[64][4], int j, flo
 // by all 4 waves (identical rows); wave 0 exchanges; shK is an LDS int.  Returns K (uniform).
 __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&nominal)[C], float tol, int max_iter,
                                          int kprev, bool valid, int p, int q, int lane, float* mu_rec_row,
-                                         unsigned long long* slots, unsigned epoch, int32_t* status, int& shK) {
+                                         unsigned long long* slots, unsigned epoch, int32_t* status, int& shK,
+                                         int& dead, int drop_block = -1) {
   const int last = max_iter - 1;
   const int kspec = min(last, kprev + 3);
   float lo, hi;
@@ -250,8 +257,10 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   uint32_t conv = qp_bisect_range2(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, q == 0, valid, q, j);
   const int ntiles = gridDim.x;
   if (p == 0) {
-    if (lane == 0) publish_mask(slots + blockIdx.x, epoch, conv);
-    const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane);
+    // drop_block (test hook, FIODE_DEBUG_DROP_PUBLISH): that workgroup never publishes epoch 1,
+    // as if it were not resident -- exercises the timeout path
+    if (lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block)) publish_mask(slots + blockIdx.x, epoch, conv);
+    const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane, dead);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
     if (lane == 0) shK = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
@@ -261,7 +270,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
     conv |= qp_bisect_range2(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, q == 0, valid, q, j);
     if (p == 0) {
       if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, epoch, conv);
-      const uint32_t all = gather_masks(slots + ntiles, ntiles, epoch, status, lane);
+      const uint32_t all = gather_masks(slots + ntiles, ntiles, epoch, status, lane, dead);
       if (lane == 0) shK = qp_exit_iter(all, max_iter);
     }
     __syncthreads();

@@ -62,7 +62,8 @@ class LyapGrads(ct.Structure):
 FIODE_ODE_RK4, FIODE_ODE_DOPRI5 = 0, 1
 FIODE_DTYPE_F32, FIODE_DTYPE_C64 = 0, 1
 FIODE_INV_MAX_N = 128
-FIODE_ODE_MAX_BATCH = 4096
+FIODE_ODE_MAX_BATCH = 4096          # fiode_odetrain_*
+FIODE_ODEINT_MAX_BATCH = 65536      # fiode_odeint (tile-parallel eval-mode solve)
 FIODE_SMALL_CAYLEY_MAX_K, FIODE_SMALL_CAYLEY_MAX_RK = 16, 8192
 
 

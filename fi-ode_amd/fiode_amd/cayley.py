@@ -231,12 +231,14 @@ class _DenseCayleyFn(torch.autograd.Function):
         Q = _dense_finish(st, inv)
         ctx.save_for_backward(st["Wb"], st["al"], st["nrm"], inv)
         ctx.shapes = (W.shape, alpha.shape)
+        ctx.step_stream = STEP_STREAM
         return Q.reshape(W.shape)
 
     @staticmethod
     def backward(ctx, gQ):
         Wb, al, nrm, inv = ctx.saved_tensors
-        return _run_on_step_stream(DENSE_BWD_ON_MAIN, lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
+        return _run_on_step_stream(DENSE_BWD_ON_MAIN, ctx.step_stream,
+                                   lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
 
 
 class _DenseCayleyGroupFn(torch.autograd.Function):
@@ -303,11 +305,12 @@ class _SmallCayleyFn(torch.autograd.Function):
                 "fiode_small_cayley_forward")
         ctx.save_for_backward(Wb, al, nrm, inv)
         ctx.shapes = (W.shape, alpha.shape)
+        ctx.step_stream = STEP_STREAM
         return Q.reshape(W.shape)
 
     @staticmethod
     def backward(ctx, gQ):
-        return _run_on_step_stream(SMALL_BWD_ON_MAIN, lambda: _SmallCayleyFn._backward(ctx, gQ))
+        return _run_on_step_stream(SMALL_BWD_ON_MAIN, ctx.step_stream, lambda: _SmallCayleyFn._backward(ctx, gQ))
 
     @staticmethod
     def _backward(ctx, gQ):
@@ -371,8 +374,11 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
 
 # Backward placement of the prefetched maps.  autograd runs a node's backward on the stream its
 # forward ran on (a side stream); with these flags the backward of the spectral / dense maps runs
-# on the stream the step was launched from instead (set by LyapunovLearning.compute_loss), which
-# the hipGraph executor places on another hardware queue.  With the executor on 2 internal
+# on the stream the step was launched from instead: STEP_STREAM is set by
+# LyapunovLearning.compute_loss only while it runs (step_stream_scope) and each map records it on
+# its autograd ctx at forward time, so a later eager or non-parallel step never sends work to a
+# stale (e.g. graph-capture) stream.  The hipGraph executor places that stream on another
+# hardware queue.  With the executor on 2 internal
 # streams (bench.py) the dense maps' backward on the step stream measured 2.28 -> 2.24 ms per step
 # in the interleaved A/B (tools/ab_step.py); the spectral maps' is slower there (2.35 ms).
 SPECTRAL_BWD_ON_MAIN = False
@@ -381,8 +387,25 @@ SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 
 
-def _run_on_step_stream(flag: bool, fn):
-    tgt = STEP_STREAM if flag else None
+class step_stream_scope:
+    """Context manager: STEP_STREAM = ``stream`` inside, the previous value restored on exit."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def __enter__(self):
+        global STEP_STREAM
+        self.prev, STEP_STREAM = STEP_STREAM, self.stream
+        return self
+
+    def __exit__(self, *exc):
+        global STEP_STREAM
+        STEP_STREAM = self.prev
+        return False
+
+
+def _run_on_step_stream(flag: bool, step_stream, fn):
+    tgt = step_stream if flag else None
     cur = torch.cuda.current_stream()
     if tgt is None or tgt == cur:
         return fn()
@@ -520,13 +543,14 @@ class _SpectralCayleyFn(torch.autograd.Function):
         Q, inv, ws = ops.spectral_cayley_forward(weight.detach(), alpha.detach(), n)
         ctx.save_for_backward(weight, alpha, inv, ws)
         ctx.n = n
+        ctx.step_stream = STEP_STREAM
         return Q
 
     @staticmethod
     def backward(ctx, gQ):
         from . import ops
         weight, alpha, inv, ws = ctx.saved_tensors
-        gw, ga = _run_on_step_stream(SPECTRAL_BWD_ON_MAIN, lambda: ops.spectral_cayley_backward(
+        gw, ga = _run_on_step_stream(SPECTRAL_BWD_ON_MAIN, ctx.step_stream, lambda: ops.spectral_cayley_backward(
             gQ.contiguous(), weight.detach(), alpha.detach(), ctx.n, inv, ws))
         return gw, ga.reshape(alpha.shape), None
 

@@ -27,11 +27,12 @@ import torch
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
-                 warmup: int = 3, act: str = "relu"):
+                 warmup: int = 3, act: str = "relu", check_every: int = 200):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
         self.module, self.opt, self.reducer, self.world, self.act = module, optimizer, reducer, world, act
+        self.check_every, self.n_replays = int(check_every), 0
         dyn = module.dyn_fun
         if module.global_step < dyn.kappa_length:
             raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
@@ -52,6 +53,11 @@ class GraphTrainStep:
                     p.grad = torch.zeros_like(p)
         self._grad_ptrs = [p.grad.data_ptr() for p in self.params] if self.persistent else None
 
+        # Warm-up iterations (lazy optimizer state, library handles, workspaces) run real updates on
+        # the constructor's batch; the reference's Lightning loop makes no such updates, so the
+        # parameters, the optimizer state and the Philox counter are restored afterwards (in place:
+        # the captured graph must see the tensors the warm-up created).
+        snap = self._snapshot()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -60,6 +66,8 @@ class GraphTrainStep:
                 self._between()
                 self.opt.step()
         torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self._restore(snap)
         torch.cuda.synchronize(dev)
 
         self.single = world == 1
@@ -76,6 +84,39 @@ class GraphTrainStep:
         if self.persistent and [p.grad.data_ptr() for p in self.params] != self._grad_ptrs:
             raise RuntimeError("autograd re-allocated .grad during capture; cannot replay into the bucket")
         self.scalars = module.last_plan["scalars"]
+
+    def _snapshot(self):
+        """Copies of what a warm-up iteration changes: parameters, optimizer state (None where a
+        parameter has none yet), the device Philox counter."""
+        with torch.no_grad():
+            params = [p.detach().clone() for p in self.params]
+            state = []
+            for p in self.params:
+                st = self.opt.state.get(p)
+                state.append(None if not st else {k: (v.detach().clone() if torch.is_tensor(v) else v)
+                                                  for k, v in st.items()})
+            counter = self.module.rng_counter.detach().clone()
+        return params, state, counter
+
+    def _restore(self, snap):
+        params, state, counter = snap
+        with torch.no_grad():
+            for p, v in zip(self.params, params):
+                p.copy_(v)
+            for p, old in zip(self.params, state):
+                st = self.opt.state.get(p)
+                if not st:
+                    continue
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        if old is not None and k in old:
+                            st[k] = old[k]
+                        continue
+                    if old is not None and k in old and torch.is_tensor(old[k]):
+                        v.copy_(old[k])
+                    else:
+                        v.zero_()        # state created by the warm-up: its initial value (Adam: 0)
+            self.module.rng_counter.copy_(counter)
 
     def _fwd_bwd(self):
         m = self.module
@@ -110,4 +151,13 @@ class GraphTrainStep:
             self._between()
             self.g_opt.replay()
         m.global_step += 1
+        self.n_replays += 1
+        if self.check_every > 0 and self.n_replays % self.check_every == 0:
+            self.check_status()
         return self.loss
+
+    def check_status(self) -> None:
+        """Raise if a persistent solve of the replayed step timed out on a cross-workgroup exchange
+        (sticky device status; one host read, every ``check_every`` replays and on demand)."""
+        if hasattr(self.module, "check_device_status"):
+            self.module.check_device_status()

@@ -398,11 +398,15 @@ class LyapunovLearning(nn.Module):
 
     def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
         """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""
+        from . import cayley as _cy
+        step_stream = torch.cuda.current_stream(x.device) if x.is_cuda else None
+        with _cy.step_stream_scope(step_stream):
+            return self._compute_loss(x, y, h=h, masks=masks, debug=debug)
+
+    def _compute_loss(self, x, y, h=None, masks=None, debug=False):
         if self.current_epoch == self.epoch_off_scale:
             self.dyn_fun.scale_nominal = False
         if self.parallel_cayley and self.training and x.is_cuda and self.dyn_fun.cayley:
-            from . import cayley as _cy
-            _cy.STEP_STREAM = torch.cuda.current_stream(x.device)
             self._prefetch_weights(x.device)
         static_state, _ = self.init_coordinates(x, self.dyn_fun)
         bb = self.init_coordinates.param_map
@@ -430,6 +434,20 @@ class LyapunovLearning(nn.Module):
             return self._ode_loss(loss, y_hat, y)
         return loss
 
+    def device_status(self) -> int:
+        """Sticky status of the last train_ode solve (fiode_odetrain_forward stats[3]): 0 ok, 4 = a
+        workgroup's QP-exit exchange timed out (its rows of y_hat were poisoned with NaN).  One host
+        read: call it every few hundred steps or at the epoch end, not per step."""
+        plan = getattr(self, "last_ode_plan", None)
+        st = plan.get("stats") if plan else None
+        return int(st[3]) if st is not None else 0
+
+    def check_device_status(self) -> None:
+        status = self.device_status()
+        if status:
+            raise RuntimeError(f"train_ode solve: cross-workgroup QP-exit exchange timed out (status {status}); "
+                               "the step's loss is NaN")
+
     def ode_plan(self, batch: int, masks: Optional[torch.Tensor] = None) -> dict:
         """Solver plan of the train_ode solve (make_solver_params(train_ode_solver, train_ode_tol))."""
         if self.use_adjoint:
@@ -452,6 +470,11 @@ class LyapunovLearning(nn.Module):
         launched on a side stream and overlaps the fan-out kernels."""
         h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
         plan = self.ode_plan(static_state.shape[0], masks)
+        # leaf parameters (the biases) enter the side-stream solve through views taken here, on the
+        # step stream: their AccumulateGrad nodes then receive every gradient on the step stream
+        # (a leaf used directly on two streams gets gradients from both: torch warns that this can
+        # break graph capture)
+        w = {k: (v.view_as(v) if v.is_leaf and v.requires_grad else v) for k, v in w.items()}
         args = (static_state, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"], w["b3"], h0, plan)
         self.last_ode_plan = plan
         if static_state.is_cuda and self.parallel_cayley and getattr(self, "ode_side_stream", True):

@@ -31,11 +31,15 @@ def make_solver_params(solver_name, ode_tol):
 
 
 def _native_target(func):
-    """The IVP whose h_dot ``func`` is, if its dynamics runs on libfiode."""
+    """The HIP-backed dynamics behind ``func``: an IVP's ``h_dot`` (models.py:200-201) or the
+    dynamics' own ``ode_forward`` (classification.py:128-132), else None."""
     from .dynamics import OrthoClassDynProjectSimplexLips
     owner = getattr(func, "__self__", None)
+    name = getattr(func, "__name__", "")
+    if isinstance(owner, OrthoClassDynProjectSimplexLips) and name == "ode_forward":
+        return owner
     dyn = getattr(owner, "dyn_fun", None)
-    if isinstance(dyn, OrthoClassDynProjectSimplexLips) and getattr(func, "__name__", "") == "h_dot":
+    if isinstance(dyn, OrthoClassDynProjectSimplexLips) and name == "h_dot":
         return dyn
     return None
 
@@ -72,6 +76,13 @@ def _odeint_native(dyn, h0, t, rtol, atol, method, options):
                                             step_size=options.get("step_size"),
                                             max_steps=int(options.get("max_num_steps", 100000)))
     dyn.last_solve_stats = (stats, dstats)
+    status = int(stats[3])        # one host read per solve (torchdiffeq raises here too)
+    if status == 2:
+        raise RuntimeError(f"max_num_steps exceeded ({int(stats[5])} steps)")
+    if status == 3:
+        raise AssertionError(f"underflow in dt {float(dstats[0])}")
+    if status:
+        raise RuntimeError(f"fiode_odeint: cross-workgroup exchange timed out (status {status}); results invalid")
     return sol
 
 

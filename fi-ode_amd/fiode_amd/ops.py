@@ -240,8 +240,8 @@ def odeint_dyn(x_feat: torch.Tensor, h0: torch.Tensor, times: torch.Tensor, weig
     Returns (solution [T,B,C], stats int32[8], dstats float64[4]) -- all on the device."""
     dev = h0.device
     B = h0.shape[0]
-    if B > L.FIODE_ODE_MAX_BATCH:
-        raise ValueError(f"batch {B} > FIODE_ODE_MAX_BATCH")
+    if B > L.FIODE_ODEINT_MAX_BATCH:
+        raise ValueError(f"batch {B} > FIODE_ODEINT_MAX_BATCH")
     h0 = _need(h0, "h0", (B, C), torch.float32, dev)
     x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
     T = times.shape[0]

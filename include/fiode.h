@@ -157,11 +157,12 @@ FIODE_API int fiode_dyn_eval(void* stream, const fiode_dyn_config* dyn, const fi
 
 /* ---- ODE solves (models.py:211-242 IVP.integrate -> torchdiffeq.odeint) ------------------- */
 enum { FIODE_ODE_RK4 = 0, FIODE_ODE_DOPRI5 = 1 };
-#define FIODE_ODE_MAX_BATCH 4096
+#define FIODE_ODE_MAX_BATCH 4096          /* the differentiable train_ode solve (fiode_odetrain_*) */
+#define FIODE_ODEINT_MAX_BATCH 65536      /* the eval-mode solve (fiode_odeint); also <= 256 x CUs */
 
 typedef struct fiode_ode_config {
   int32_t method;        /* FIODE_ODE_RK4 (fixed grid, 3/8 rule) or FIODE_ODE_DOPRI5          */
-  int32_t batch;         /* B rows (one per image), <= FIODE_ODE_MAX_BATCH                     */
+  int32_t batch;         /* B rows (one per image), <= FIODE_ODEINT_MAX_BATCH                  */
   int32_t n_times;       /* >= 2 output times (device float64 array, increasing)              */
   int32_t max_steps;     /* dopri5 step cap (<= 0: 100000)                                     */
   double rtol, atol;     /* dopri5 (make_solver_params: rtol = atol = ode_tol, pl_modules.py:26) */
@@ -173,9 +174,11 @@ FIODE_API size_t fiode_odeint_workspace_bytes(int32_t batch);
 /* odeint(IVP.h_dot, (h0,), times, method, rtol/atol | step_size) with f = ode_forward in eval
  * mode (no dropout), static_state = x_feat.  solution: [n_times][B][C] (solution[0] = h0).
  * stats (device int32[8]): nfe, n_accept (rk4: steps), n_reject, status (0 ok, 2 max_steps,
- * 3 dt underflow), last QP exit iteration, dopri5 attempted steps.  dstats (device double[4]):
- * next dt, final t, last error ratio.  One persistent workgroup per solve (batch-global QP exit
- * and RMS error norm are workgroup reductions). */
+ * 3 dt underflow, 4 a cross-workgroup exchange timed out: results invalid), last QP exit
+ * iteration, dopri5 attempted steps, workgroups of the solve, 16-row tiles per workgroup.  dstats
+ * (device double[4]): next dt, final t, last error ratio.  One persistent workgroup per 16-row tile (several tiles each past the chip's resident
+ * capacity); the batch-global QP exit and the dopri5 RMS error norm are exchanged between
+ * workgroups on the device (no host sync). */
 FIODE_API int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fiode_dyn_config* dyn,
                            const fiode_dyn_weights* w, const float* x_feat, const float* h0,
                            const double* times, float* solution, int32_t* stats, double* dstats,

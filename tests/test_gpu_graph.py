@@ -12,6 +12,7 @@ def _dev():
     return torch.device("cuda:0")
 
 
+@pytest.mark.filterwarnings("error:.*AccumulateGrad node's stream.*:UserWarning")
 @pytest.mark.parametrize("train_ode", [False, True])
 def test_graph_replay_matches_eager_step(train_ode):
     import bench
@@ -44,3 +45,41 @@ def test_graph_replay_matches_eager_step(train_ode):
     before = float(loss)
     after = float(gs.step())
     assert after != before
+
+
+def test_graph_warmup_leaves_no_updates():
+    """Constructing GraphTrainStep (warm-up iterations + capture) leaves the parameters, the Adam
+    state and the Philox counter as they were; the first replay then equals one eager training
+    step (compute_loss + backward + Adam) from the same state."""
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    mod = bench.build_module(dev, seed=0, train_ode=False)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    before = {k: v.detach().clone() for k, v in mod.state_dict().items()}
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y, warmup=3)
+    torch.cuda.synchronize()
+    for k, v in mod.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert int(mod.rng_counter) == 0
+    for st in opt.state.values():
+        for k, v in st.items():
+            if torch.is_tensor(v):
+                assert int(torch.count_nonzero(v)) == 0, k
+    # one replay == one eager step from the same state
+    twin = bench.build_module(dev, seed=1, train_ode=False)
+    twin.load_state_dict(before)
+    twin.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    twin.seed = mod.seed
+    topt = twin.configure_optimizers(capturable=True)[0][0]
+    gs.step()
+    topt.zero_grad(set_to_none=True)
+    twin.compute_loss(x, y, 32, "relu").backward()
+    topt.step()
+    torch.cuda.synchronize()
+    for (k, a), b in zip(mod.named_parameters(), twin.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=k)

@@ -165,3 +165,45 @@ def test_ode_loss_mix_matches_torch(p):
     assert abs(float(ode_a) - float(ode_b)) <= 1e-6 * max(1.0, abs(float(ode_b)))
     torch.testing.assert_close(la.grad, lb.grad, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_philox_keep_rate_p05():
+    """The train_ode solve's Philox dropout words keep half of the hidden units: over the 40
+    evals x B rows x 2 layers, the fraction of kept units in the saved post-activation layout
+    (a kept unit can still be 0 after the ReLU, so measured on pre-ReLU-independent data: the
+    keep words themselves, read back through the saved a1 of a zero-bias, all-positive probe)."""
+    from fiode_amd import _lib as L
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(128, 0.1, False, 11)
+    w = {k: v.clone() for k, v in w.items()}
+    # probe: layer-1 pre-activations all > 0 (u = b1 + bx large, Q1 = 0), so a1 = keep * 2 * z1
+    w["Q1"].zero_(); w["Qx"].zero_(); w["b1"].fill_(1.0); w["bx"].fill_(1.0)
+    c = ops.odetrain_config(128, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=3, offset=7)
+    y, st, ws = ops.odetrain_forward(torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev), w, dyn, c)
+    torch.cuda.synchronize()
+    a1 = ops.odetrain_saved(ws, c)["a1"]                    # [B, E, M]
+    rate = float((a1 > 0).float().mean())
+    assert abs(rate - 0.5) < 3e-3, rate                     # 655k Bernoulli(1/2) draws: std 6e-4
+    per_eval = (a1 > 0).float().mean(dim=(0, 2)).cpu()
+    assert float((per_eval - 0.5).abs().max()) < 0.02
+
+
+def test_exchange_timeout_poisons_output(monkeypatch):
+    """A workgroup that never publishes its QP-exit mask (FIODE_DEBUG_DROP_PUBLISH test hook: as if
+    it were not resident): the bounded spin ends, status 4 is recorded, y_hat is NaN for the tiles
+    that used a partial AND, and the module's sticky status check raises."""
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(64, 0.25, True, 12)
+    monkeypatch.setenv("FIODE_DEBUG_DROP_PUBLISH", "1")
+    y, st, ws = ops.odetrain_forward(torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev), w, dyn, cfg,
+                                     masks=torch.from_numpy(masks).to(dev))
+    torch.cuda.synchronize()
+    assert int(st[3]) == 4
+    assert torch.isnan(y).any()
+    import bench
+    mod = bench.build_module(dev, seed=0, train_ode=True)
+    xb = torch.rand(32, 3, 32, 32, device=dev)
+    yb = torch.randint(0, 10, (32,), device=dev)
+    loss = mod.compute_loss(xb, yb, 32, "relu")
+    torch.cuda.synchronize()
+    assert mod.device_status() == 4 and torch.isnan(loss)
+    with pytest.raises(RuntimeError, match="timed out"):
+        mod.check_device_status()

@@ -15,7 +15,7 @@ def ev():
     return torch.cuda.Event(enable_timing=True)
 
 # config 3: dopri5 tol 1e-3 validation solve, B=128 (and 4096)
-for B in (128, 4096):
+for B in (128, 1024, 4096, 8192):
     x = torch.randn(B, 10, device=dev); h0 = torch.full((B, 10), 0.1, device=dev)
     times = torch.tensor([0.0, 1.0], dtype=torch.float64, device=dev)
     dyn = ops.DynCfg(scale_nominal=False, dropout=0.0)
@@ -25,7 +25,7 @@ for B in (128, 4096):
     sol, st, dst = ops.odeint_dyn(x, h0, times, w, dyn, method="dopri5", rtol=1e-3, atol=1e-3)
     b.record(); torch.cuda.synchronize()
     s = st.cpu().tolist()
-    out[f"dopri5_B{B}"] = {"ms": round(a.elapsed_time(b), 3), "nfe": s[0], "accepted": s[1], "rejected": s[2]}
+    out[f"dopri5_B{B}"] = {"ms": round(a.elapsed_time(b), 3), "nfe": s[0], "accepted": s[1], "rejected": s[2], "status": s[3], "workgroups": s[6], "tiles_per_wg": s[7]}
     print(out[f"dopri5_B{B}"], flush=True)
 
 # config 4: certification of one image on the T=40 grid (G = 41,320,837 rows)
