@@ -204,6 +204,9 @@ class LyapunovLearning(nn.Module):
         self.rng_counter: Optional[torch.Tensor] = None   # device step counter (graph replay)
         self.parallel_cayley = True     # Cayley maps of the step on side streams (training, ROCm)
         self.lyap_after_ode = False     # fan-out kernels start after the train_ode forward (see compute_loss)
+        # train_ode branch: reuse the step's backbone features (True) or re-run the backbone as the
+        # reference's self.model(x) does (False); DESIGN.md section 5 (common-subexpression reuse)
+        self.ode_reuse_features = True
         self._side_streams = None
         self.logged: Dict[str, float] = {}
         self._out = None
@@ -416,7 +419,12 @@ class LyapunovLearning(nn.Module):
         w = self.dyn_fun.effective_weights()
         ode_on = self.train_ode and self.current_epoch > self.train_ode_epoch
         if ode_on:        # launched first: on ROCm it runs on a side stream beside the fan-out kernels
-            y_hat = self._ode_launch(static_state.float(), w)
+            feat_ode = static_state
+            if not self.ode_reuse_features:
+                # reference order: self.model(x, ...) re-runs the backbone (pl_modules.py:491); the
+                # default reuses the features (the backbone is deterministic: same value, one pass)
+                feat_ode, _ = self.init_coordinates(x, self.dyn_fun)
+            y_hat = self._ode_launch(feat_ode.float(), w)
             if isinstance(y_hat, tuple) and self.lyap_after_ode:
                 # k_ot_fwd is a persistent latency chain whose 8 workgroups exchange QP exit masks:
                 # dispatched beside the fan-out kernels, some of its workgroups wait for CUs while the

@@ -102,9 +102,9 @@ def _odeint_torch(f, y0, t, rtol, atol, method, options, tuple_out=False):
 
     if method == "rk4":
         h = options.get("step_size")
-        if h is None:
-            raise ValueError("rk4 needs options.step_size")
-        grid = _rk4_grid(t[0], t[-1], h, t.dtype)
+        # torchdiffeq 0.2.2 FixedGridODESolver: options.step_size builds the grid
+        # (_grid_constructor_from_step_size); without it the grid is t itself
+        grid = t if h is None else _rk4_grid(t[0], t[-1], h, t.dtype)
         sol = [y0]
         j = 1
         y = y0

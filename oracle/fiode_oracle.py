@@ -631,6 +631,29 @@ def rk4_fixed_grid(func, y0: np.ndarray, t0: float, t1: float, step_size: float,
     return np.stack(sol), len(grid) - 1
 
 
+def rk4_on_grid(func, y0: np.ndarray, grid: np.ndarray) -> np.ndarray:
+    """torchdiffeq method='rk4' WITHOUT options.step_size: the solver grid is the output times
+    themselves (FixedGridODESolver's default grid constructor), so the solution is the grid
+    states [T, ...] -- the call of BASELINE configs[0] (control/certify_segway.py:108-109,
+    ts = linspace(0, 50, 10000)).  Same float32 3/8-rule expressions as rk4_fixed_grid."""
+    y = np.asarray(y0, F32)
+    g = np.asarray(grid, F32)
+    third = F32(1.0 / 3.0)
+    sol = [y.copy()]
+    for a, b in zip(g[:-1], g[1:]):
+        dt = F32(b - a)
+        k1 = np.asarray(func(float(a), y), F32)
+        k2 = np.asarray(func(float(a + dt * third), (y + (dt * k1).astype(F32) * third).astype(F32)), F32)
+        k3 = np.asarray(func(float(a + dt * F32(2.0 / 3.0)),
+                             (y + dt * (k2 - (k1 * third).astype(F32)).astype(F32)).astype(F32)), F32)
+        k4 = np.asarray(func(float(b), (y + dt * ((k1 - k2).astype(F32) + k3).astype(F32)).astype(F32)), F32)
+        dy = ((((k1 + F32(3) * (k2 + k3).astype(F32)).astype(F32) + k4).astype(F32) * dt).astype(F32)
+              * F32(0.125)).astype(F32)
+        y = (y + dy).astype(F32)
+        sol.append(y.copy())
+    return np.stack(sol)
+
+
 def rk4_train(x_feat: np.ndarray, h0: np.ndarray, P: DynParams, cfg: DynConfig, t0: float, t1: float,
               step_size: float, masks: Optional[np.ndarray] = None, p: Optional[float] = None):
     """The train_ode forward (pl_modules.py:490-493): odeint with method='rk4' and the dynamics in

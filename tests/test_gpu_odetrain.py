@@ -207,3 +207,46 @@ def test_exchange_timeout_poisons_output(monkeypatch):
     assert mod.device_status() == 4 and torch.isnan(loss)
     with pytest.raises(RuntimeError, match="timed out"):
         mod.check_device_status()
+
+
+def test_feature_reuse_equals_reference_order():
+    """The train_ode branch reuses the step's backbone features (one backbone pass); the reference
+    re-runs the backbone inside self.model(x) (pl_modules.py:491).  With both backbone passes on
+    the same stream (no Cayley-map prefetch) they give bit-identical features, so the loss and
+    every dynamics gradient are identical and the backbone gradients agree up to float32 summation
+    order (the two branches' feature gradients meet before the backbone instead of inside it).
+
+    (With the prefetch on, the first pass's Cayley maps come from side streams whose library GEMMs
+    round differently: the features then differ by ~1e-6, and the QP backward's active set -- a
+    sign test on rounding noise, DESIGN.md section 5 -- flips for a few rows, which moves the
+    gradients by a few percent: a property of the reference's gradient, tools/probes/cse_probe.py.)"""
+    import bench
+    dev = _dev()
+    x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+    out = {}
+    for reuse in (True, False):
+        mod = bench.build_module(dev, seed=0, train_ode=True)
+        mod.parallel_cayley = False
+        mod.ode_reuse_features = reuse
+        mod._rng_offset = 0
+        feats = []
+        hook = mod.init_coordinates.param_map.register_forward_hook(lambda m, i, o: feats.append(o.detach().clone()))
+        loss = mod.compute_loss(x, yb, 32, "relu")
+        hook.remove()
+        loss.backward()
+        torch.cuda.synchronize()
+        assert len(feats) == (1 if reuse else 2)
+        if not reuse:
+            assert torch.equal(feats[0], feats[1])
+        out[reuse] = (loss.detach().clone(), {n: p.grad.detach().clone() for n, p in mod.named_parameters()
+                                              if p.requires_grad})
+    (la, ga), (lb, gb) = out[True], out[False]
+    assert torch.equal(la, lb)
+    for n in ga:
+        if n.startswith("model.dyn_fun."):
+            assert torch.equal(ga[n], gb[n]), n
+        else:
+            scale = float(gb[n].abs().max()) + 1e-12
+            err = float((ga[n] - gb[n]).abs().max()) / scale
+            assert err <= 1e-4, (n, err)

@@ -37,8 +37,8 @@ def short(name: str) -> str:
     return name[:90]
 
 
-def pmc(path: pathlib.Path, counter: str):
-    f = path / f"pmc_{counter}" / "run_counter_collection.csv"
+def pmc(path: pathlib.Path, counter: str, pass_dir: str = None):
+    f = path / f"pmc_{pass_dir or counter}" / "run_counter_collection.csv"
     if not f.exists():
         return {}
     acc = defaultdict(list)
@@ -47,6 +47,44 @@ def pmc(path: pathlib.Path, counter: str):
             if row["Counter_Name"] == counter:
                 acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+# MFMA issue cycles per launch expected from the kernels' instruction counts at the bench shape
+# (B = 128, S = 256: N = 32,768 rows; train_ode E = 40 evals of 8 tiles), per SIMD:
+# v_mfma_f32_32x32x2_f32 = 64 cycles, v_mfma_f32_16x16x4_f32 = 32 cycles (MI355X_MICROARCH.md).
+#   k_lyap_fwd   (20 + 256 + 64) MFMA32 per 32-row tile per pass x 2 passes x 1,024 tiles
+#   k_lyap_bwd   (20 + 256) MFMA32 per tile x 1,024 tiles
+#   k_lyap_wgrad 6 MFMA32 per wave per row pair x 4 waves x N / 2
+#   k_ot_fwd     96 MFMA16 per wave per eval x 4 waves x 8 tiles x 40 evals (k_ot_bwd the same)
+EXPECTED_MFMA_SIMD_CYCLES = {
+    "k_lyap_fwd": 340 * 2 * 1024 * 64, "k_lyap_bwd": 276 * 1024 * 64, "k_lyap_wgrad": 24 * 16384 * 64,
+    "k_ot_fwd": 96 * 4 * 8 * 40 * 32, "k_ot_bwd": 96 * 4 * 8 * 40 * 32}
+N_CU, N_SIMD, N_XCD = 256, 4, 8
+
+
+def mfma_lds(src_p: pathlib.Path) -> dict:
+    """Per-kernel MFMA-busy fraction and LDS bank-conflict share from the MFMA pass."""
+    c = {n: pmc(src_p, n, "MFMA") for n in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_LDS_BANK_CONFLICT",
+                                          "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE")}
+    out = {}
+    for k in c["SQ_VALU_MFMA_BUSY_CYCLES"]:
+        if not k.startswith("k_"):
+            continue
+        busy = c["SQ_VALU_MFMA_BUSY_CYCLES"][k]
+        gui = c["GRBM_GUI_ACTIVE"].get(k)
+        d = {"mfma_busy_cycles": busy, "grbm_gui_active": gui, "sq_busy_cu_cycles": c["SQ_BUSY_CU_CYCLES"].get(k)}
+        if gui:
+            cyc = gui / N_XCD                          # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
+            d["kernel_cycles"] = cyc
+            d["mfma_busy_frac"] = busy / (cyc * N_CU * N_SIMD)
+        if k in EXPECTED_MFMA_SIMD_CYCLES:
+            d["expected_mfma_simd_cycles"] = EXPECTED_MFMA_SIMD_CYCLES[k]
+            d["busy_over_expected"] = busy / EXPECTED_MFMA_SIMD_CYCLES[k]
+        bc, ia = c["SQ_LDS_BANK_CONFLICT"].get(k), c["SQ_LDS_IDX_ACTIVE"].get(k)
+        if bc is not None and ia:
+            d["lds_bank_conflict_frac"] = bc / ia
+        out[k] = d
+    return out
 
 
 def main(src: str, dst: str):
@@ -79,19 +117,36 @@ def main(src: str, dst: str):
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['Percentage']):.2f} |")
     fetch, write = pmc(src_p, "FETCH_SIZE"), pmc(src_p, "WRITE_SIZE")
+    ml = mfma_lds(src_p)
     summ = {}
-    for k in sorted(set(fetch) | set(write)):
+    for k in sorted(set(fetch) | set(write) | set(ml)):
         if not k.startswith("k_"):
             continue
         fr, wr = fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
         summ[k] = {"fetch_bytes_raw": fr, "write_bytes": wr, "hbm_bytes_per_launch": 2 * fr + wr,
                    "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes"}
+        summ[k].update(ml.get(k, {}))
     if summ:
         lines += ["", "## HBM traffic per launch (separate --pmc passes)", "",
                   "| kernel | FETCH raw MB | WRITE MB | corrected total MB |", "|---|---|---|---|"]
         for k, v in summ.items():
             lines.append(f"| {k} | {v['fetch_bytes_raw'] / 1e6:.2f} | {v['write_bytes'] / 1e6:.2f} | "
                          f"{v['hbm_bytes_per_launch'] / 1e6:.2f} |")
+        if ml:
+            lines += ["", "## MFMA busy and LDS bank conflicts per launch (--pmc SQ_VALU_MFMA_BUSY_CYCLES "
+                      "SQ_BUSY_CU_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE)", "",
+                      "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs); "
+                      "busy/expected = the counter over the MFMA issue cycles the kernel's instruction count implies "
+                      "(unit check of the counter).", "",
+                      "| kernel | MFMA busy | busy / expected | LDS bank-conflict share |", "|---|---|---|---|"]
+            for k, v in summ.items():
+                if "mfma_busy_cycles" not in v:
+                    continue
+                f = lambda x: "-" if x is None else f"{x:.4f}"
+                lines.append(f"| {k} | {f(v.get('mfma_busy_frac'))} | {f(v.get('busy_over_expected'))} | "
+                             f"{f(v.get('lds_bank_conflict_frac'))} |")
+        summ["_source"] = (f"rocprofv3 --pmc passes of `bench.py --steps 2 --warmup 1` ({src_p.name}; "
+                           "tools/gpu_profile.sh), not the timed run")
         (dst_p.parent / "pmc_summary.json").write_text(json.dumps(summ, indent=1))
     bj = src_p / "bench.json"
     if bj.exists():
