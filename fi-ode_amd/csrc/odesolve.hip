@@ -64,6 +64,7 @@ struct OsTile {                  // one tile's QP state kept across the exit exc
 
 struct OsShared {
   float zpart[4][64][4];         // [part][lane][layer-3 accumulator registers]
+  float xt[2][TR][16];           // bisection tree exchange (qp_bisect_tree), double-buffered
   float Q1s[M * C];
   double red[OS_XV];             // broadcast of the last reduction exchange
   int K;                         // exit iteration of the current eval
@@ -268,6 +269,9 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
   const int last = a.d.max_iter - 1;
   const int kspec = min(last, sh.kprev + 3);
   const uint32_t ones[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  T16W w;                     // this wave's weight operands, from the workgroup's LDS images
+  load_t16w(sh.Q1s, Q2s, LDQ, Q3s, LDQ, a.b2, a.b3, p, q, j, w);
+  int xbuf = 0;               // qp_bisect_tree's LDS buffer (every eval starts after barriers)
   uint32_t wconv = 0xFFFFFFFFu;
   for (int t = 0; t < a.T; ++t) {
     const int tile = blockIdx.x * a.T + t;
@@ -282,8 +286,7 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
       const f32x4 uv = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 16 * hb + 4 * q);
       uacc[hb] = f32x4v{uv[0], uv[1], uv[2], uv[3]};
     }
-    mlp16_part(sh.Q1s, Q2s, Q3s, a.b2, a.b3, uacc, h, ones, 0xFFFFFFFFu, 1.0f, p, q, j, nullptr, nullptr,
-               &sh.zpart[p][lane][0]);
+    mlp16_part(w, uacc, h, ones, 0xFFFFFFFFu, 1.0f, p, q, nullptr, nullptr, &sh.zpart[p][lane][0]);
     __syncthreads();
     float ft[C];
     ft16_sum(sh.zpart, j, ft);
@@ -291,7 +294,8 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
     float lo, hi;
     qp_bracket(lower, nominal, lo, hi);
-    wconv &= qp_bisect_range2(lower, nominal, 0, kspec, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, q, j);
+    wconv &= qp_bisect_tree(lower, nominal, 0, kspec, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, p, q, j, sh.xt,
+                            xbuf);
     if (own) {
 #pragma unroll
       for (int i = 0; i < C; ++i) {
@@ -327,7 +331,8 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
       }
       barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
       float lo = tl[t].lo[j], hi = tl[t].hi[j];
-      wc2 &= qp_bisect_range2(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, q, j);
+      wc2 &= qp_bisect_tree(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, p, q, j,
+                            sh.xt, xbuf);
     }
     if (p == 0) {
       const uint32_t all = xchg_and(a, sh, ep + 1, wc2, lane);

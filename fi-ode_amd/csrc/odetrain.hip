@@ -57,6 +57,7 @@ struct OTArgs {
   float* vw;                // [B][E][C] QP outputs (the stage derivatives k_i)
   float* muw;               // [B][E]
   float* nomw;              // [B][E][C] QP nominal (for checkers: the QP active-set test input)
+  float* loww;              // [B][E][C] QP lower bound (for checkers)
   float* a1;                // [B][E][M]
   float* a2;                // [B][E][M]
   float* gz2;               // [B][E][M]
@@ -102,7 +103,7 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 struct OtShared {
   float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
   float mu_rec[4][TR][33];    // [wave][row][bisection iteration] (padded)
-  float Q1s[M * C];
+  float xt[2][TR][16];        // bisection tree exchange (qp_bisect_tree), double-buffered
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
   int dead;                   // an exit exchange timed out (status 4): stop waiting, poison y_out
@@ -117,27 +118,49 @@ struct OtShared {
 #endif
 
 // one eval for this workgroup's tile: stage input h (per lane, its row) -> k (per lane)
-__device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtShared& sh, int e, int p, int b,
-                        bool valid, int lane, int q, int j, const f32x4v (&uacc)[8], const uint32_t (&kw1)[4],
-                        uint32_t kw2p, const float (&h)[C], float (&k)[C]) {
+__device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int p, int b, bool valid, int lane, int q,
+                        int j, const f32x4v (&uacc)[8], const uint32_t (&kw1)[4], uint32_t kw2p, const float (&h)[C],
+                        float (&k)[C], int& xbuf) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
 #ifdef OT_PROFILE
   uint64_t t_prev = wall_clock64();
 #endif
   if (p == 0 && valid && q == 0) store_row10(a.hs + r * C, h);
-  mlp16_part(sh.Q1s, Q2s, Q3s, a.b2, a.b3, uacc, h, kw1, kw2p, a.drop_scale, p, q, j, valid ? a.a1 + r * M : nullptr,
+  // the barrier's lower bound depends on h only: issued ahead of the MLP so the VALU work overlaps
+  // the MFMA chain (same float32 expressions as barrier_nominal, common.h)
+  float lower[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) lower[i] = -a.d.alpha_1 * (expf(a.d.sigma_1 * h[i]) - 1.0f);
+  mlp16_part(w, uacc, h, kw1, kw2p, a.drop_scale, p, q, valid ? a.a1 + r * M : nullptr,
              valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0]);
   OT_MARK(1);
   __syncthreads();
   float ft[C];
   ft16_sum(sh.zpart, j, ft);
-  float lower[C], nominal[C], sig[C], span[C];
-  barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+  float nominal[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    const float upper = a.d.alpha_2 * (1.0f - h[i]);
+    const float span = upper - lower[i];
+    if (a.d.scale_nominal) {
+      const float sig = 1.0f / (1.0f + expf(-ft[i]));
+      nominal[i] = span * sig + lower[i];
+    } else {
+      nominal[i] = ft[i];
+    }
+  }
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][j][0];
   qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
-            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead, a.drop_block);
+            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead, sh.xt, xbuf,
+            a.drop_block,
+#ifdef OT_PROFILE
+            a.prof
+#else
+            nullptr
+#endif
+  );
   OT_MARK(3);
   const int K = sh.K;
   const float mu = sh.mu_rec[p][j][K];
@@ -146,6 +169,7 @@ __device__ void ot_eval(const OTArgs& a, const float* Q2s, const float* Q3s, OtS
   if (p == 0 && valid && q == 0) {
     store_row10(a.ftw + r * C, ft);
     store_row10(a.nomw + r * C, nominal);
+    store_row10(a.loww + r * C, lower);
     store_row10(a.vw + r * C, k);
     a.muw[r] = mu;
   }
@@ -177,11 +201,7 @@ __global__ __launch_bounds__(256) void k_ot_masks(OTArgs a) {
 
 __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Q2s = smem;
-  float* Q3s = smem + M * LDQ;
-  OtShared& sh = *reinterpret_cast<OtShared*>(smem + (M + 32) * LDQ);
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
-  for (int t = threadIdx.x; t < M * C; t += blockDim.x) sh.Q1s[t] = a.Q1[t];
+  OtShared& sh = *reinterpret_cast<OtShared*>(smem);
   if (threadIdx.x == 0) {
     sh.Kprev = a.d.max_iter - 1;
     sh.dead = 0;
@@ -191,6 +211,8 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   const int b = blockIdx.x * TR + j;
   const bool valid = b < a.B;
   const int bb = valid ? b : a.B - 1;
+  T16W w;                     // this wave's weight operands, in registers for the whole solve
+  load_t16w(a.Q1, a.Q2, M, a.Q3, M, a.b2, a.b3, p, q, j, w);
   // u[b] = U_x x_b + bx + b1 for this tile's rows
   for (int t = threadIdx.x; t < TR * M; t += blockDim.x) {
     const int rb = blockIdx.x * TR + t / M, i = t % M;
@@ -224,6 +246,7 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   uint32_t kc1[4], kc2, kn1[4], kn2;
   fetch(0, kc1, kc2);
   float y[C], k1[C], k2[C], k3[C], k4[C], hin[C];
+  int xbuf = 0;
   load_row10(a.h0 + (size_t)bb * C, y);
   const float third = 1.0f / 3.0f;
   const int eN = 4 * (a.niters - 1);
@@ -234,7 +257,7 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
 #define OT_STAGE(E_, H_, K_)                                                             \
     {                                                                                    \
       if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                      \
-      ot_eval(a, Q2s, Q3s, sh, (E_), p, b, valid, lane, q, j, uacc, kc1, kc2, H_, K_);   \
+      ot_eval(a, w, sh, (E_), p, b, valid, lane, q, j, uacc, kc1, kc2, H_, K_, xbuf);     \
       _Pragma("unroll") for (int t = 0; t < 4; ++t) kc1[t] = kn1[t];                   \
       kc2 = kn2;                                                                         \
     }
@@ -298,7 +321,15 @@ __device__ __forceinline__ void load_vjp_in(const OTArgs& a, int p, int e, int b
   for (int o = 0; o < 2; ++o) in.a1[o] = *reinterpret_cast<const f32x4*>(a.a1 + r * M + 16 * (2 * p + o) + 4 * q);
 }
 
-__device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, const float (&q3t)[8][3],
+// The backward's weight operands of one wave (part p), in registers for the whole kernel: q2t[o][hb]
+// = Q2^T[16 (2p + o) + j][16 hb + 4q ..] = Q2[16 hb + 4q + t][16 (2p + o) + j]; q1t[o] =
+// Q1^T[j][16 (2p + o) + 4q ..] (0 for j >= C).
+struct VjpW {
+  f32x4 q2t[2][8];
+  f32x4 q1t[2];
+};
+
+__device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3],
                        OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int q, int j,
                        const VjpIn& in, const float (&g)[C], float (&gy_out)[C]) {
   const int bb = valid ? b : a.B - 1;
@@ -360,9 +391,8 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
   for (int hb = 0; hb < 8; ++hb) {
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-      const f32x4 qv = *reinterpret_cast<const f32x4*>(Q2Ts + (16 * (2 * p + o) + j) * LDQ + 16 * hb + 4 * q);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) gb[o] = mfma16(qv[t], ga[hb][t], gb[o]);
+      for (int t = 0; t < 4; ++t) gb[o] = mfma16(wv.q2t[o][hb][t], ga[hb][t], gb[o]);
     }
   }
 #pragma unroll
@@ -377,9 +407,8 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
   f32x4v gh = z4();
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
-    const f32x4 qv = *reinterpret_cast<const f32x4*>(Q1Ts + j * LDQ + 16 * (2 * p + o) + 4 * q);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) gh = mfma16(qv[t], gb[o][t], gh);
+    for (int t = 0; t < 4; ++t) gh = mfma16(wv.q1t[o][t], gb[o][t], gh);
   }
   *reinterpret_cast<f32x4*>(&sh.gpart[buf][p][lane][0]) = f32x4{gh[0], gh[1], gh[2], gh[3]};
   __syncthreads();
@@ -394,17 +423,19 @@ __device__ void ot_vjp(const OTArgs& a, const float* Q2Ts, const float* Q1Ts, co
 
 __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Q2Ts = smem;                 // Q2^T image [128][LDQ]
-  float* Q1Ts = smem + M * LDQ;       // Q1^T image [32][LDQ] (rows >= 10 zero)
-  OtBwdShared& sh = *reinterpret_cast<OtBwdShared*>(smem + (M + 32) * LDQ);
-  load_weight_images(a.Q2, nullptr, Q2Ts, nullptr, true);
-  for (int t = threadIdx.x; t < 32 * M; t += blockDim.x) {
-    const int c = t >> 7, i = t & 127;
-    Q1Ts[c * LDQ + i] = c < C ? a.Q1[i * C + c] : 0.f;
-  }
-  __syncthreads();
+  OtBwdShared& sh = *reinterpret_cast<OtBwdShared*>(smem);
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  VjpW wv;
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+#pragma unroll
+    for (int hb = 0; hb < 8; ++hb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wv.q2t[o][hb][t] = a.Q2[(16 * hb + 4 * q + t) * M + 16 * (2 * p + o) + j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wv.q1t[o][t] = j < C ? a.Q1[(16 * (2 * p + o) + 4 * q + t) * C + j] : 0.f;
+  }
   float q3t[8][3];                    // A operand of g_a2^T: Q3^T[16hb + j][4s + q] = Q3[4s + q][16hb + j]
 #pragma unroll
   for (int hb = 0; hb < 8; ++hb)
@@ -424,7 +455,7 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   // evals are visited E-1, E-2, ..., 0: each VJP first issues the loads of the next one
 #define OT_VJP(E_, G_)                                                                  \
   load_vjp_in(a, p, (E_) - 1, b, valid, q, nxt);                                        \
-  ot_vjp(a, Q2Ts, Q1Ts, q3t, sh, buf, p, (E_), b, valid, lane, q, j, cur, G_, gY);     \
+  ot_vjp(a, wv, q3t, sh, buf, p, (E_), b, valid, lane, q, j, cur, G_, gY);               \
   cur = nxt;                                                                            \
   buf ^= 1;
   for (int it = a.niters - 2; it >= 0; --it) {
@@ -482,7 +513,7 @@ int grid_iters(const fiode_odetrain_config* cfg) {
 }
 
 struct OtLayout {
-  size_t u, y, k, hs, ftw, vw, muw, nomw, a1, a2, gz2, gz1, gft, xs, kw, wg, total;
+  size_t u, y, k, hs, ftw, vw, muw, nomw, loww, a1, a2, gz2, gz1, gft, xs, kw, wg, total;
 };
 OtLayout ot_layout(int B, int E) {
   OtLayout L;
@@ -496,6 +527,7 @@ OtLayout ot_layout(int B, int E) {
   L.vw = o; o += al(R * C * 4);
   L.muw = o; o += al(R * 4);
   L.nomw = o; o += al(R * C * 4);
+  L.loww = o; o += al(R * C * 4);
   L.a1 = o; o += al(R * M * 4);
   L.a2 = o; o += al(R * M * 4);
   L.gz2 = o; o += al(R * M * 4);
@@ -542,6 +574,7 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.vw = reinterpret_cast<float*>(ws + L.vw);
   a.muw = reinterpret_cast<float*>(ws + L.muw);
   a.nomw = reinterpret_cast<float*>(ws + L.nomw);
+  a.loww = reinterpret_cast<float*>(ws + L.loww);
   a.a1 = reinterpret_cast<float*>(ws + L.a1);
   a.a2 = reinterpret_cast<float*>(ws + L.a2);
   a.gz2 = reinterpret_cast<float*>(ws + L.gz2);
@@ -575,8 +608,8 @@ extern "C" int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, in
   const int n = grid_iters(cfg);
   if (n < 0) return FIODE_EINVAL;
   const OtLayout L = ot_layout(cfg->batch, 4 * (n - 1));
-  const size_t o[8] = {L.hs, L.ftw, L.vw, L.muw, L.nomw, L.a1, L.a2, L.gft};
-  for (int i = 0; i < 8; ++i) offsets[i] = (int64_t)o[i];
+  const size_t o[FIODE_ODETRAIN_NSAVED] = {L.hs, L.ftw, L.vw, L.muw, L.nomw, L.a1, L.a2, L.gft, L.loww};
+  for (int i = 0; i < FIODE_ODETRAIN_NSAVED; ++i) offsets[i] = (int64_t)o[i];
   return FIODE_OK;
 }
 
@@ -593,7 +626,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   a.drop_block = fiode_internal::debug_drop_publish();
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int ntiles = (a.B + TR - 1) / TR;
-  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtShared);
+  const size_t lds = sizeof(OtShared);     // the weights live in registers (tile16.h T16W)
   // k_ot_masks zeroes the exchange granules (tags) and the status words before every forward, and
   // draws the dropout keep words when dropout is on
   a.nslots = (int)(((size_t)a.E * 2 * ntiles * 8 + 256) / 8);
@@ -617,7 +650,7 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
     return FIODE_EINVAL;
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = (size_t)(M + 32) * LDQ * sizeof(float) + sizeof(OtBwdShared);
+  const size_t lds = sizeof(OtBwdShared);     // weight operands in registers (VjpW)
   hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const OtLayout L = ot_layout(a.B, a.E);

@@ -318,14 +318,14 @@ def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, 
 def odetrain_saved(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> Dict[str, torch.Tensor]:
     """Views of the forward's saved arrays in an odetrain workspace (for checkers)."""
     B, E = int(cfg.batch), odetrain_evals(cfg)
-    off = (ct.c_int64 * 8)()
+    off = (ct.c_int64 * 9)()
     L.check(L.lib().fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)),
             "fiode_odetrain_saved_offsets")
     f = lambda i, n: ws[off[i]:off[i] + 4 * n].view(torch.float32)
     R = B * E
     return dict(h=f(0, R * C).view(B, E, C), ftilde=f(1, R * C).view(B, E, C), v=f(2, R * C).view(B, E, C),
                 mu=f(3, R).view(B, E), nominal=f(4, R * C).view(B, E, C), a1=f(5, R * M).view(B, E, M),
-                a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C))
+                a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C), lower=f(8, R * C).view(B, E, C))
 
 
 def odetrain_backward(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,

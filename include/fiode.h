@@ -206,10 +206,12 @@ FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* 
                                      const fiode_dyn_weights* w, const float* x_feat, const float* h0,
                                      const uint8_t* masks, const uint64_t* offset_dev, float* y_out,
                                      int32_t* stats, void* workspace, size_t workspace_bytes);
-/* Byte offsets inside the workspace of the forward's saved arrays, for checkers:
- * [0] stage inputs [B][E][C], [1] MLP outputs [B][E][C], [2] QP outputs v [B][E][C], [3] QP mu
- * [B][E], [4] QP nominal [B][E][C], [5] a1 [B][E][M], [6] a2 [B][E][M], [7] dL/d mlp output
- * [B][E][C] (after the backward).  Row (b, e) = b*E + e. */
+/* Byte offsets inside the workspace of the forward's saved arrays, for checkers (offsets:
+ * int64[FIODE_ODETRAIN_NSAVED]): [0] stage inputs [B][E][C], [1] MLP outputs [B][E][C], [2] QP
+ * outputs v [B][E][C], [3] QP mu [B][E], [4] QP nominal [B][E][C], [5] a1 [B][E][M], [6] a2
+ * [B][E][M], [7] dL/d mlp output [B][E][C] (after the backward), [8] QP lower bound [B][E][C].
+ * Row (b, e) = b*E + e. */
+#define FIODE_ODETRAIN_NSAVED 9
 FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets);
 /* Given g_y = dL/dy(t1) [B][C]: all weight gradients and dL/dx_feat (overwritten).  Must follow
  * fiode_odetrain_forward on the same workspace.  dbg_gft: optional [B][E][C] dL/d mlp output. */

@@ -228,6 +228,8 @@ def test_feature_reuse_equals_reference_order():
     for reuse in (True, False):
         mod = bench.build_module(dev, seed=0, train_ode=True)
         mod.parallel_cayley = False
+        with torch.no_grad():          # the first forward initialises the conv alphas (a different path)
+            mod.init_coordinates(x, mod.dyn_fun)
         mod.ode_reuse_features = reuse
         mod._rng_offset = 0
         feats = []
@@ -250,3 +252,26 @@ def test_feature_reuse_equals_reference_order():
             scale = float(gb[n].abs().max()) + 1e-12
             err = float((ga[n] - gb[n]).abs().max()) / scale
             assert err <= 1e-4, (n, err)
+
+
+@pytest.mark.parametrize("scale_nominal,mode", [(False, "philox"), (True, "given")])
+def test_forward_qp_bit_exact_per_eval(scale_nominal, mode):
+    """Every eval's QP in the train_ode forward (three bisection iterations per round over the row's
+    lanes, speculation to the previous exit + 3, the cross-tile exit exchange) equals the sequential
+    reference bisection with the batch-global exit (barrier_projection.py:232-255) on the device's
+    own (lower, nominal), bit for bit: mu, v and therefore the exit iteration of all 40 evals."""
+    from fiode_amd import _lib as L
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(128, 0.1, scale_nominal, 21)
+    if mode == "philox":
+        cfg = ops.odetrain_config(128, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=4, offset=2)
+        y, st, ws = ops.odetrain_forward(torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev), w, dyn, cfg)
+    else:
+        y, st, ws = ops.odetrain_forward(torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev), w, dyn, cfg,
+                                         masks=torch.from_numpy(masks).to(dev))
+    torch.cuda.synchronize()
+    sv = {k: v.cpu().numpy() for k, v in ops.odetrain_saved(ws, cfg).items()}
+    for e in range(E):
+        q = O.qp_forward(sv["lower"][:, e], sv["nominal"][:, e], 30, 1e-4)
+        assert np.array_equal(sv["mu"][:, e], q.mu), e
+        assert np.array_equal(sv["v"][:, e], q.v), e
+    assert int(st[2]) == q.iters

@@ -20,13 +20,14 @@ for B in (128, 1024):
     off = ct.c_int64 * 8
     # prof array sits after the exchange granules
     lib = L.lib()
-    offs = (ct.c_int64 * 8)()
+    offs = (ct.c_int64 * 9)()
     # xslots offset = gft offset + al(R*C*4)
     lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
     al = lambda v: (v + 255) & ~255
     xs = offs[7] + al(B * E * 10 * 4)
-    prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 16) * 8].view(torch.int64).cpu().numpy()
-    ticks = prof[:6] / E          # 100 MHz wall clock -> 10 ns per tick
-    print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): layer1 {ticks[0]*0.01:.2f} "
-          f"layer2+3 {ticks[1]*0.01:.2f} barrier+sum+nominal {ticks[5]*0.01:.2f} bisect {ticks[2]*0.01:.2f} "
-          f"exchange {ticks[3]*0.01:.2f} final {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
+    prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 17) * 8].view(torch.int64).cpu().numpy()
+    ticks = prof[:8] / E          # 100 MHz wall clock -> 10 ns per tick
+    print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): mlp {ticks[1]*0.01:.2f} "
+          f"partial sums+nominal {ticks[5]*0.01:.2f} bisection+exit exchange {ticks[3]*0.01:.2f} "
+          f"(bisection {ticks[6]*0.01:.2f}, exchange wait {ticks[7]*0.01:.2f}, resumes {int(prof[8])}/{E}) "
+          f"finalize {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
