@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "gj.h"
+#include "gjb.h"
 #include "fiode.h"
 
 namespace {
@@ -37,6 +38,27 @@ __global__ void __launch_bounds__(NT) k_inv_gj(int n, const typename Ops::T* __r
   G::store(a, out + (int64_t)blockIdx.x * out_stride, n, n);
 }
 
+// Real n in (16, 128]: the blocked Gauss-Jordan of gjb.h (16-wide pivot blocks inverted in one
+// wave's registers, MFMA rank-16 updates, matrix in LDS), one workgroup per matrix.
+template <int NP, int NW>
+__global__ void __launch_bounds__(64 * NW) k_inv_gjb(int n, const float* __restrict__ in, int64_t in_stride,
+                                                     float* __restrict__ out, int64_t out_stride) {
+  typedef fiode_gjb::GJB<NP, NW> G;
+  extern __shared__ __attribute__((aligned(16))) char gjb_smem[];
+  typename G::Smem& sm = *reinterpret_cast<typename G::Smem*>(gjb_smem);
+  G::load(sm, in + (int64_t)blockIdx.x * in_stride, n, n);
+  __syncthreads();
+  G::invert(sm);
+  G::store(sm, out + (int64_t)blockIdx.x * out_stride, n, n);
+}
+
+template <int NP, int NW>
+void launch_gjb(hipStream_t s, int batch, int n, const float* x, int64_t in_stride, float* y, int64_t out_stride) {
+  typedef fiode_gjb::GJB<NP, NW> G;
+  hipLaunchKernelGGL((k_inv_gjb<NP, NW>), dim3(batch), dim3(G::NT), sizeof(typename G::Smem), s, n, x, in_stride, y,
+                     out_stride);
+}
+
 // Tile shapes measured on MI355X (tools/gj_bench.hip): us per launch, old 2x2-pivot kernel ->
 // this one: real 128: 74.6 -> 58.9 (8x4, 512 threads); real 64: 23.0 -> 16.3; real 32: 11.8 -> 6.5;
 // complex 64 x 40: 60.5 -> 48.5 (2x4, 512 threads); complex 32 x 144: 22.4 -> 12.0 (2x2, 256).
@@ -49,9 +71,9 @@ int launch_inv<RealOps>(hipStream_t s, int batch, int n, const void* in, int64_t
   const float* x = (const float*)in;
   float* y = (float*)out;
   if (n <= 16) k_inv_gj<RealOps, 16, 2, 2, 64><<<batch, 64, 0, s>>>(n, x, in_stride, y, out_stride);
-  else if (n <= 32) k_inv_gj<RealOps, 32, 2, 2, 256><<<batch, 256, 0, s>>>(n, x, in_stride, y, out_stride);
-  else if (n <= 64) k_inv_gj<RealOps, 64, 4, 4, 256><<<batch, 256, 0, s>>>(n, x, in_stride, y, out_stride);
-  else k_inv_gj<RealOps, 128, 8, 4, 512><<<batch, 512, 0, s>>>(n, x, in_stride, y, out_stride);
+  else if (n <= 32) launch_gjb<32, 4>(s, batch, n, x, in_stride, y, out_stride);
+  else if (n <= 64) launch_gjb<64, 8>(s, batch, n, x, in_stride, y, out_stride);
+  else launch_gjb<128, 16>(s, batch, n, x, in_stride, y, out_stride);
   return 0;
 }
 
@@ -70,11 +92,11 @@ int launch_inv<ComplexOps>(hipStream_t s, int batch, int n, const void* in, int6
 // ---- large real inverses: block Gauss-Jordan over 64-wide panels --------------------------------
 // For n > 64 (the 512 x 512 backbone CayleyLinears, the 128 x 128 dynamics map) the matrix lives in
 // HBM (padded with I to a multiple of 64) and each of the n/64 panel steps is two launches:
-//   k_panel_pivot   one workgroup: P = X_KK^-1 by the register Gauss-Jordan above (16 us at 64);
+//   k_panel_pivot   one workgroup: P = X_KK^-1 by the blocked Gauss-Jordan of gjb.h;
 //   k_panel_update  one workgroup per 64 x 64 output tile, ping-pong buffers (no read/write race):
 //                   R_Kj = P X_Kj,  X_ij -= X_iK R_Kj,  X_iK <- -X_iK P,  X_Kj <- R_Kj,  X_KK <- P.
 // Smaller pivot blocks are cheaper per eliminated column (a Gauss-Jordan round costs ~0.25 us at
-// 64, ~0.9 us at 128), and the update is a few us of LDS-tiled FMA on 64 workgroups.
+// 64, ~0.9 us at 128), and the update is a few us of MFMA on 64 workgroups.
 constexpr int PB = 64;
 
 // Batched over matrices m = blockIdx.y (pad, pivot) / blockIdx.z (update): matrix m's buffers sit
@@ -90,103 +112,110 @@ __global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* _
   out[idx] = (i < n && j < n) ? in[(int64_t)i * n + j] : (i == j ? 1.0f : 0.0f);
 }
 
-__global__ void __launch_bounds__(256) k_panel_pivot(int np, int k0, const float* __restrict__ X, float* __restrict__ P,
-                                                     int64_t wstride) {
-  typedef fiode_gj::GJ<RealOps, PB, 4, 4> G;
-  __shared__ typename G::Smem sm;
-  float a[4][4];
+typedef fiode_gjb::GJB<PB, 8> PivotGJ;
+__global__ void __launch_bounds__(PivotGJ::NT) k_panel_pivot(int np, int k0, const float* __restrict__ X,
+                                                            float* __restrict__ P, int64_t wstride) {
+  extern __shared__ __attribute__((aligned(16))) char piv_smem[];
+  PivotGJ::Smem& sm = *reinterpret_cast<PivotGJ::Smem*>(piv_smem);
   const int64_t m = blockIdx.x;
-  G::load(a, X + m * wstride + (int64_t)k0 * np + k0, PB, np);
-  G::invert(a, PB, sm);
-  G::store(a, P + m * wstride, PB, PB);
+  PivotGJ::load(sm, X + m * wstride + (int64_t)k0 * np + k0, PB, np);
+  __syncthreads();
+  PivotGJ::invert(sm);
+  PivotGJ::store(sm, P + m * wstride, PB, PB);
 }
 
-// out tile (ib, jb) of the next buffer; 256 threads, 4 x 4 outputs each
+// out tile (ib, jb) of the next buffer: 256 threads, MFMA 16x16x4 (wave w: output rows 16w..16w+15,
+// all 4 column blocks), operands in LDS as row-major A / column-major B so every k-chunk of 4 is
+// one ds_read_b128 (k order permuted: step s of chunk kc uses k = 16 kc + 4q + s at lane q).
+constexpr int LDT = PB + 4;
+typedef fiode_gjb::f4v f4v;
+
+// acc[bj] += A[16w + i][:] . B^T[16bj + j][:]  (A row-major, BT = B column-major, both [PB][LDT])
+__device__ __forceinline__ void tile_gemm(const float (*A)[LDT], const float (*BT)[LDT], int w, int i, int q,
+                                          f4v (&acc)[4], float sign) {
+#pragma unroll 4
+  for (int kc = 0; kc < PB / 16; ++kc) {
+    const f4v a4 = *reinterpret_cast<const f4v*>(&A[16 * w + i][16 * kc + 4 * q]) * sign;
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj) {
+      const f4v b4 = *reinterpret_cast<const f4v*>(&BT[16 * bj + i][16 * kc + 4 * q]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[bj] = fiode_gjb::mfma(a4[s], b4[s], acc[bj]);
+    }
+  }
+}
+
+// 64 x 64 block at (r0, c0) of a row-major matrix (row stride ld) -> LDS, row-major or transposed
+__device__ __forceinline__ void tile_load(float (*dst)[LDT], const float* __restrict__ src, int64_t ld, bool transpose) {
+#pragma unroll
+  for (int u = 0; u < PB * PB / 4 / 256; ++u) {
+    const int t = threadIdx.x + 256 * u;
+    const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
+    const f4v v = *reinterpret_cast<const f4v*>(src + (int64_t)r * ld + c4);
+    if (transpose) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[c4 + e][r] = v[e];
+    } else {
+      *reinterpret_cast<f4v*>(&dst[r][c4]) = v;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
                                                       const float* __restrict__ P, float* __restrict__ Y,
                                                       float* __restrict__ final_out, int n, int64_t wstride) {
-  __shared__ float sP[PB][PB + 4];
-  __shared__ float sA[PB][PB + 4];      // X_iK (rows of the tile, pivot columns)
-  __shared__ float sB[PB][PB + 4];      // X_Kj, then R_Kj
-  const int ib = blockIdx.x * PB, jb = blockIdx.y * PB, tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float sA[PB][LDT];    // P, or X_iK (row-major A operands)
+  __shared__ __attribute__((aligned(16))) float sX[PB][LDT];    // X_iK for the second product
+  __shared__ __attribute__((aligned(16))) float sB[PB][LDT];    // column-major B: X_Kj^T or P^T, then R^T
+  const int ib = blockIdx.x * PB, jb = blockIdx.y * PB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
   const int64_t m = blockIdx.z;
   X += m * wstride;
   P += m * wstride;
   Y += m * wstride;
   if (final_out) final_out += m * (int64_t)n * n;
   const bool piv_r = ib == k0, piv_c = jb == k0;
-#pragma unroll 16
-  for (int idx = tid; idx < PB * PB; idx += 256) {     // 16 trips: all loads in flight together
-    const int r = idx / PB, c = idx % PB;
-    sP[r][c] = P[idx];
-    sA[r][c] = X[(int64_t)(ib + r) * np + k0 + c];
-    sB[r][c] = X[(int64_t)(k0 + r) * np + jb + c];
-  }
-  __syncthreads();
-  const int tr = (tid / 16) * 4, tc = (tid % 16) * 4;
-  float acc[4][4];
-  auto gemm = [&](float (*A)[PB + 4], float (*B)[PB + 4]) {
+  f4v acc[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+  for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
+  if (piv_r && piv_c) {                       // X_KK <- P
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < PB; ++k) {
-      float x[4], y[4];
+    for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[r] = A[tr + r][k];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) y[c] = B[k][tc + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(x[r], y[c], acc[r][c]);
-    }
-  };
-  float o[4][4];
-  if (piv_c) {
-    if (piv_r) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[r][c] = sP[tr + r][tc + c];
-    } else {
-      gemm(sA, sP);                       // -X_iK P
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[r][c] = -acc[r][c];
-    }
+      for (int r = 0; r < 4; ++r) acc[bj][r] = P[(16 * w + 4 * q + r) * PB + 16 * bj + i];
+  } else if (piv_c) {                         // X_iK <- -X_iK P
+    tile_load(sA, X + (int64_t)ib * np + k0, np, false);
+    tile_load(sB, P, PB, true);
+    __syncthreads();
+    tile_gemm(sA, sB, w, i, q, acc, -1.0f);
   } else {
-    gemm(sP, sB);                         // R_Kj = P X_Kj
-    if (piv_r) {
+    tile_load(sA, P, PB, false);              // R_Kj = P X_Kj
+    tile_load(sB, X + (int64_t)k0 * np + jb, np, true);
+    if (!piv_r) tile_load(sX, X + (int64_t)ib * np + k0, np, false);
+    __syncthreads();
+    tile_gemm(sA, sB, w, i, q, acc, 1.0f);
+    if (!piv_r) {                             // X_ij - X_iK R_Kj
+      __syncthreads();                        // every wave is done reading sB
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[r][c] = acc[r][c];
-    } else {
+      for (int bj = 0; bj < 4; ++bj)          // sB[col][row] = R[row][col]: rows 16w + 4q + r, col 16bj + i
+        *reinterpret_cast<f4v*>(&sB[16 * bj + i][16 * w + 4 * q]) = acc[bj];
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) sB[tr + r][tc + c] = acc[r][c];
-      __syncthreads();
-      gemm(sA, sB);                       // X_ij - X_iK R_Kj
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[r][c] = X[(int64_t)(ib + tr + r) * np + jb + tc + c] - acc[r][c];
+        for (int r = 0; r < 4; ++r) acc[bj][r] = X[(int64_t)(ib + 16 * w + 4 * q + r) * np + jb + 16 * bj + i];
+      tile_gemm(sX, sB, w, i, q, acc, -1.0f);
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int i = ib + tr + r, j = jb + tc + c;
+    for (int r = 0; r < 4; ++r) {
+      const int gi = ib + 16 * w + 4 * q + r, gj = jb + 16 * bj + i;
       if (final_out) {
-        if (i < n && j < n) final_out[(int64_t)i * n + j] = o[r][c];
+        if (gi < n && gj < n) final_out[(int64_t)gi * n + gj] = acc[bj][r];
       } else {
-        Y[(int64_t)i * np + j] = o[r][c];
+        Y[(int64_t)gi * np + gj] = acc[bj][r];
       }
     }
 }
@@ -228,7 +257,8 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
                      n, np, in, A, wstride);
   for (int kb = 0; kb < nb; ++kb) {
     const int k0 = kb * PB;
-    hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(256), 0, st, np, k0, A, P, wstride);
+    hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, k0, A,
+                       P, wstride);
     const bool last = kb == nb - 1;
     hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, P, B,
                        last ? out : nullptr, n, wstride);

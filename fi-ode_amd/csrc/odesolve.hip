@@ -64,7 +64,6 @@ struct OsTile {                  // one tile's QP state kept across the exit exc
 
 struct OsShared {
   float zpart[4][64][4];         // [part][lane][layer-3 accumulator registers]
-  float xt[2][TR][16];           // bisection tree exchange (qp_bisect_tree), double-buffered
   float Q1s[M * C];
   double red[OS_XV];             // broadcast of the last reduction exchange
   int K;                         // exit iteration of the current eval
@@ -271,7 +270,6 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
   const uint32_t ones[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   T16W w;                     // this wave's weight operands, from the workgroup's LDS images
   load_t16w(sh.Q1s, Q2s, LDQ, Q3s, LDQ, a.b2, a.b3, p, q, j, w);
-  int xbuf = 0;               // qp_bisect_tree's LDS buffer (every eval starts after barriers)
   uint32_t wconv = 0xFFFFFFFFu;
   for (int t = 0; t < a.T; ++t) {
     const int tile = blockIdx.x * a.T + t;
@@ -294,8 +292,7 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
     float lo, hi;
     qp_bracket(lower, nominal, lo, hi);
-    wconv &= qp_bisect_tree(lower, nominal, 0, kspec, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, p, q, j, sh.xt,
-                            xbuf);
+    wconv &= qp_bisect_seq(lower, nominal, 0, kspec, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid);
     if (own) {
 #pragma unroll
       for (int i = 0; i < C; ++i) {
@@ -331,8 +328,7 @@ __device__ __noinline__ unsigned os_eval(const OsArgs& a, const float* Q2s, cons
       }
       barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
       float lo = tl[t].lo[j], hi = tl[t].hi[j];
-      wc2 &= qp_bisect_tree(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid, p, q, j,
-                            sh.xt, xbuf);
+      wc2 &= qp_bisect_seq(lower, nominal, kspec + 1, last, a.d.tol, lo, hi, &tl[t].mu_rec[j][0], own, valid);
     }
     if (p == 0) {
       const uint32_t all = xchg_and(a, sh, ep + 1, wc2, lane);

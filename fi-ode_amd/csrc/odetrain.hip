@@ -103,7 +103,6 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 struct OtShared {
   float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
   float mu_rec[4][TR][33];    // [wave][row][bisection iteration] (padded)
-  float xt[2][TR][16];        // bisection tree exchange (qp_bisect_tree), double-buffered
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
   int dead;                   // an exit exchange timed out (status 4): stop waiting, poison y_out
@@ -120,7 +119,7 @@ struct OtShared {
 // one eval for this workgroup's tile: stage input h (per lane, its row) -> k (per lane)
 __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int p, int b, bool valid, int lane, int q,
                         int j, const f32x4v (&uacc)[8], const uint32_t (&kw1)[4], uint32_t kw2p, const float (&h)[C],
-                        float (&k)[C], int& xbuf) {
+                        float (&k)[C]) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
 #ifdef OT_PROFILE
@@ -153,7 +152,7 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][j][0];
   qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
-            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead, sh.xt, xbuf,
+            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
             a.drop_block,
 #ifdef OT_PROFILE
             a.prof
@@ -246,7 +245,6 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
   uint32_t kc1[4], kc2, kn1[4], kn2;
   fetch(0, kc1, kc2);
   float y[C], k1[C], k2[C], k3[C], k4[C], hin[C];
-  int xbuf = 0;
   load_row10(a.h0 + (size_t)bb * C, y);
   const float third = 1.0f / 3.0f;
   const int eN = 4 * (a.niters - 1);
@@ -257,7 +255,7 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
 #define OT_STAGE(E_, H_, K_)                                                             \
     {                                                                                    \
       if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                      \
-      ot_eval(a, w, sh, (E_), p, b, valid, lane, q, j, uacc, kc1, kc2, H_, K_, xbuf);     \
+      ot_eval(a, w, sh, (E_), p, b, valid, lane, q, j, uacc, kc1, kc2, H_, K_);     \
       _Pragma("unroll") for (int t = 0; t < 4; ++t) kc1[t] = kn1[t];                   \
       kc2 = kn2;                                                                         \
     }

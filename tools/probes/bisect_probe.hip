@@ -3,7 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include tools/probes/bisect_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
-#include "../../fi-ode_amd/csrc/tile16.h"
+#include "bisect_variants.h"
 
 using namespace fiode_t16;
 
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k(const float* in, unsigned long long* cy
     qp_bracket(lower, nom, lo, hi);
     if (V == 0) acc += qp_bisect_tree(lower, nom, 0, 19, 1e-4f, lo, hi, &mu_rec[j][0], q == 0, true, p, q, j, xt, xbuf);
     if (V == 1) acc += qp_bisect_range2(lower, nom, 0, 19, 1e-4f, lo, hi, &mu_rec[j][0], q == 0, true, q, j);
-    if (V == 2) acc += qp_bisect_range(lower, nom, 0, 19, 1e-4f, lo, hi, &mu_rec[j][0], q == 0, true);
+    if (V == 2) acc += qp_bisect_seq(lower, nom, 0, 19, 1e-4f, lo, hi, &mu_rec[j][0], q == 0, true);
     if (V == 3) {   // eps evaluations only (20 per call), no exchange
       float e = 0.f;
       for (int it = 0; it < 20; ++it) e += qp_eps(lower, nom, lo + 1e-3f * it + e * 1e-9f);
