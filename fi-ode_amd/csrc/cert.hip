@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_cert_fwd(CertArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];

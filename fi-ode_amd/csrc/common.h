@@ -200,6 +200,15 @@ __device__ __forceinline__ void barrier_nominal(const DynScalars& d, const float
   }
 }
 
+// max(a, b) as one bare v_max_f32: fmaxf's result for every non-signalling input, without the
+// operand re-quieting the compiler adds to fmaxf in IEEE mode when an operand is defined in another
+// basic block (the loop-invariant QP bounds: +1 VALU per term per bisection iteration).
+__device__ __forceinline__ float vmax_f32(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Bisection of FastBarrierProjectionNoUpper (barrier_projection.py:232-255) for one row.
 // Runs iterations 0..last (inclusive) and returns the per-iteration convergence bits of the
 // iterations run; v/mu hold the state of iteration `last`.
@@ -217,7 +226,7 @@ __device__ __forceinline__ uint32_t qp_bisect(const float (&lower)[FIODE_C], con
     float eps = 0.f;
 #pragma unroll
     for (int j = 0; j < FIODE_C; ++j) {
-      v[j] = fmaxf(nom[j] - mu, lower[j]);
+      v[j] = vmax_f32(nom[j] - mu, lower[j]);
       eps = eps + v[j];
     }
     conv |= (fabsf(eps) < tol ? 1u : 0u) << it;

@@ -60,10 +60,13 @@ struct LyapArgs {
   float *a1, *a2, *gz2, *gz1;   // [N][M]
   float* gft;          // [N][C]
   uint4* kw;           // [4][N] dropout keep words (bit t of word mb = keep hidden 32mb+t)
-  float* Q2T;          // [M][M] mlp_to_mlp transposed (written by k_static_proj)
   float* tile_sc;      // [ntiles][4]
-  float* slabs;        // [B*parts][SLAB]
+  float* slabs;        // [nslab][SLAB]
+  int nslab;           // partial slabs summed by k_lyap_reduce
   float* g_u;          // [B][M]
+  float* gu_tiles;     // fused backward: per-(tile, image segment) partial g_u [ntiles][nseg][M] (else null)
+  double* xslabs;      // fused backward, XCD mode: [8][SLAB] per-XCD sums (L2 float64 atomics), else null
+  int nseg;            // image segments per 32-row tile (images a tile's rows can span)
   // outputs
   float* scalars;
   float *h_out, *V, *Vdot, *f, *f_log, *qp_lower, *qp_nominal, *g_ftilde;
@@ -162,7 +165,6 @@ __device__ __forceinline__ void keep_words(const LyapArgs& a, int row, int set, 
 __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
   const int b = blockIdx.x, i = threadIdx.x;
   if (b == 0 && i < 2) a.conv[i] = 0xFFFFFFFFu;
-  if (b < M) a.Q2T[b * M + i] = a.Q2[i * M + b];   // Q2^T for the backward's LDS image (coalesced stores)
   if (b >= a.B) return;
   float s = 0.f;
   const float* xb = a.x_feat + (size_t)b * FIODE_X;
@@ -174,6 +176,8 @@ __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
 // Per-row preparation: sampler fan-out (h -> h_ws) and the dropout keep words of the 4 mask sets.
 __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.xslabs)             // the per-XCD sums the backward adds into
+    for (int e = row; e < 8 * SLAB; e += gridDim.x * blockDim.x) a.xslabs[e] = 0.0;
   if (row >= a.N) return;
   if (a.offset_dev) {            // graph replay: the step counter lives in device memory
     const uint64_t o = (((uint64_t)a.rng.off_hi << 32) | a.rng.off_lo) + *a.offset_dev;
@@ -196,13 +200,16 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   }
 }
 
-// 2 workgroups per CU where the grid has them (LDS 72.9 KB, <= 256 registers): one wave's QP
-// (VALU) overlaps the other's MFMA on each SIMD.
+// One wave per (32-row tile, pass): the loss pass (pass 0) and the logging pass (pass 1) of a tile
+// are independent, so a workgroup's 4 waves are 2 tiles x 2 passes and 2 workgroups share a CU
+// (LDS 72.9 KB each, <= 256 registers): one wave's QP (VALU) overlaps another's MFMA on every
+// SIMD.  Per wave: layers 1-3, ft -> HBM, the QP to max_iter - 1 for its convergence bits, AND-ed
+// per pass into one word (the batch-global exit, barrier_projection.py:247-249).
 __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false, C);
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, C);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];
@@ -211,166 +218,318 @@ __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
 #pragma unroll
     for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
   const int ntiles = (a.N + 31) / 32;
-  for (int tile = blockIdx.x * FIODE_WAVES + wave; tile < ntiles; tile += gridDim.x * FIODE_WAVES) {
+  const int pass = wave & 1;
+  for (int tile = 2 * blockIdx.x + (wave >> 1); tile < ntiles; tile += 2 * gridDim.x) {
     const int row = tile * 32 + col;
     const bool valid = row < a.N;
     const int rr = valid ? row : a.N - 1;
     const int b = rr / a.S;
     float h[C];
     load_row10(((a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws) + (size_t)rr * C, h);
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-      const uint4 k1 = a.kw[(size_t)(2 * pass) * a.N + rr], k2 = a.kw[(size_t)(2 * pass + 1) * a.N + rr];
-      const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w}, kw2[4] = {k2.x, k2.y, k2.z, k2.w};
-      f32x16 z1[4], z2[4];
-      const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
-                                 col, half, z1, z2);
-      if (pass == 0 && valid) {
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-          store_acc_rows(a.a1 + (size_t)row * M, mb, half, z1[mb]);
-          store_acc_rows(a.a2 + (size_t)row * M, mb, half, z2[mb]);
-        }
-      }
-      float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-      gather_ft(z3, half, ft);
-      barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-      uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
-      if (!valid) conv = 0xFFFFFFFFu;
-      conv = wave_and(conv);
-      if (lane == 0) atomicAnd(a.conv + pass, conv);
-      if (valid && half == 0) {
-        store_row10(a.ft_ws + ((size_t)pass * a.N + row) * C, ft);
-        if (a.qp_nominal) store_row10(a.qp_nominal + ((size_t)pass * a.N + row) * C, nominal);
-        if (pass == 0 && a.qp_lower) store_row10(a.qp_lower + (size_t)row * C, lower);
-      }
+    const uint4 k1 = a.kw[(size_t)(2 * pass) * a.N + rr], k2 = a.kw[(size_t)(2 * pass + 1) * a.N + rr];
+    const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w}, kw2[4] = {k2.x, k2.y, k2.z, k2.w};
+    f32x16 z1[4], z2[4];
+    const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
+                               col, half, z1, z2);
+    float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
+    gather_ft(z3, half, ft);
+    barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+    uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
+    if (!valid) conv = 0xFFFFFFFFu;
+    conv = wave_and(conv);
+    if (lane == 0) atomicAnd(a.conv + pass, conv);
+    if (valid && half == 0) {
+      store_row10(a.ft_ws + ((size_t)pass * a.N + row) * C, ft);
+      if (a.qp_nominal) store_row10(a.qp_nominal + ((size_t)pass * a.N + row) * C, nominal);
+      if (pass == 0 && a.qp_lower) store_row10(a.qp_lower + (size_t)row * C, lower);
     }
   }
 }
 
-__global__ __launch_bounds__(256, 2) void k_lyap_bwd(LyapArgs a) {
+// One tile's operands of the backward's second half and of the weight gradients, staged
+// row-major (row n = sample of the tile): the samples are the K dimension of dQ2 = gz2^T a1,
+// dQ3 = gft^T a2, dQ1 = gz1^T h; g_a1 = Q2^T g_z2 reads gz2 of all 128 units from here.
+struct BwdStage {
+  float g2[32][LDQ];    // gz2[n][i]
+  float a1[32][LDQ];    // a1[n][k]
+  float a2[32][LDQ];    // a2[n][k]
+  float g1[32][LDQ];    // gz1[n][i]
+  float gf[4][32][12];  // gft[n][c] of the round's 4 tiles (phase A)
+  float hh[4][32][12];  // h[n][c]
+};
+constexpr size_t BWD_LDS = (size_t)(M + C) * LDQ * sizeof(float) + sizeof(BwdStage);
+
+// Backward of the loss pass fused with the weight gradients: no activation reaches HBM.
+// A workgroup takes 4 consecutive 32-row tiles per round.
+//   Phase A (wave w, tile w; VALU): the loss-pass QP to the global exit K0 (ft from the forward),
+//     V / V-dot / hinge, the QP backward -> g_ft; the logging-pass QP to K1; g_ft and h -> LDS.
+//   Phase B (each tile in turn, all 4 waves; wave w owns hidden units 32w..32w+31): recompute
+//     layer 1 (all units) and wave w's block of layer 2 (a1, a2), g_a2 = Q3^T g_ft and
+//     g_z2 = g_a2 [a2 > 0] / (1 - p) for its block -> LDS; g_a1 = Q2^T g_z2 for its block (the A
+//     operand Q2[i][k] read transposed from the one Q2 image, g_z2 of all units from LDS) -> g_z1;
+//     then its quarter of the weight gradients over the staged tile (dQ2 rows 32w.. : 4 blocks,
+//     dQ3 columns 32w.., dQ1 rows 32w..; MFMA with K = the tile's samples); db2 / db3 ride on the
+//     A operand reads; the tile's per-image g_u partial (fixed-order sum) -> gu_tiles.
+// One partial slab per workgroup (k_lyap_reduce sums them in a fixed order).
+__global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Q2Ts = smem;      // Q2Ts[i][k] = Q2[k][i], staged from the pre-transposed copy (no LDS bank conflicts)
-  load_weight_images(a.Q2T, nullptr, Q2Ts, nullptr, false);
+  float* Q2s = smem;                         // Q2[i][k] (not transposed)
+  float* Q3s = smem + M * LDQ;               // Q3 rows 0..C-1 (unused here: the layout of k_lyap_fwd)
+  (void)Q3s;
+  BwdStage& st = *reinterpret_cast<BwdStage*>(smem + (M + C) * LDQ);
+  load_weight_images(a.Q2, nullptr, Q2s, nullptr);
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
-  float q3t[4][5];         // A operand of g_a2^T = Q3^T g_ft^T: Q3[2s+half][32mb+col]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
+  float q1[4][5], q3t[5];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int s = 0; s < 5; ++s) q3t[mb][s] = a.Q3[(2 * s + half) * M + 32 * mb + col];
+    for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
+#pragma unroll
+  for (int s = 0; s < 5; ++s) q3t[s] = a.Q3[(2 * s + half) * M + 32 * w + col];   // A operand of Q3^T g_ft^T, block w
+  f32x4 b2w[4];                              // b2 of block w in accumulator order
+#pragma unroll
+  for (int g = 0; g < 4; ++g) b2w[g] = *reinterpret_cast<const f32x4*>(a.b2 + 32 * w + 8 * g + 4 * half);
   const int K0 = qp_exit_iter(a.conv[0], a.d.max_iter);
   const int K1 = qp_exit_iter(a.conv[1], a.d.max_iter);
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
   const int ntiles = (a.N + 31) / 32;
-  for (int tile = blockIdx.x * FIODE_WAVES + wave; tile < ntiles; tile += gridDim.x * FIODE_WAVES) {
-    const int row = tile * 32 + col;
-    const bool valid = row < a.N;
-    const int rr = valid ? row : a.N - 1;
-    const int b = rr / a.S;
-    const int label = (int)a.y[b];
-    float h[C], ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-    load_row10(hsrc + (size_t)rr * C, h);
-    // ---- loss pass: QP to the global exit K0
-    load_row10(a.ft_ws + (size_t)rr * C, ft);
-    barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-    qp_bisect(lower, nominal, K0, a.d.tol, v, mu);
-    // V = (1 + max_{j != y} h_j) - h_y ; j* first index (lya_cands.py:84-94)
-    int js = label == 0 ? 1 : 0;
-    float hm = h[js];
+  f32x16 dq2[4], dq3 = f16_zero(), dq1 = f16_zero();
 #pragma unroll
-    for (int j = 0; j < C; ++j)
-      if (j != label && h[j] > hm) { hm = h[j]; js = j; }
-    float hy = 0.f, fy = 0.f, fj = 0.f;
-#pragma unroll
-    for (int j = 0; j < C; ++j) {
-      hy = (j == label) ? h[j] : hy;
-      fy = (j == label) ? v[j] : fy;
-      fj = (j == js) ? v[j] : fj;
-    }
-    const float Vv = (1.0f + hm) - hy;
-    const float Vd = fj - fy;                    // jvp of the piecewise-linear V along f
-    const float pre = Vd + a.kappa * Vv;         // vdot + kappa * V.detach() (pl_modules.py:455-457)
-    const float viol = pre > 0.f ? pre : 0.f;
-    const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
-    float g[C], g_nom[C], g_low[C], gft[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) g[j] = (j == js) ? gp : ((j == label) ? -gp : 0.f);
-    qp_backward_row(g, v, mu, nominal, g_nom, g_low);
-#pragma unroll
-    for (int j = 0; j < C; ++j)
-      gft[j] = a.d.scale_nominal ? ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j] : g_nom[j];
-    if (valid && half == 0) {
-      store_row10(a.gft + (size_t)row * C, gft);
-      if (a.V) a.V[row] = Vv;
-      if (a.Vdot) a.Vdot[row] = Vd;
-      if (a.f) store_row10(a.f + (size_t)row * C, v);
-      if (a.g_ftilde) store_row10(a.g_ftilde + (size_t)row * C, gft);
-    }
-    // ---- logging pass: QP to K1, active-constraint count (pl_modules.py:476-482)
-    float fl[C], nom1[C], mu1;
-    load_row10(a.ft_ws + ((size_t)a.N + rr) * C, ft);
-    barrier_nominal(a.d, h, ft, lower, nom1, sig, span);
-    qp_bisect(lower, nom1, K1, a.d.tol, fl, mu1);
-    float active = 0.f;
-#pragma unroll
-    for (int j = 0; j < C; ++j) {
-      const float lin = -a.d.alpha_1 * h[j];
-      const float up = a.d.alpha_2 * (1.0f - h[j]);
-      active += (fabsf(fl[j] - lin) <= 1e-6f || fabsf(fl[j] - up) <= 1e-6f) ? 1.f : 0.f;
-    }
-    if (valid && half == 0 && a.f_log) store_row10(a.f_log + (size_t)row * C, fl);
+  for (int kb = 0; kb < 4; ++kb) dq2[kb] = f16_zero();
+  float db2 = 0.f, db3 = 0.f;
+  for (int base = 4 * blockIdx.x; base < ntiles; base += 4 * gridDim.x) {
+    // ---------------- phase A: wave w, tile base + w: the row math of the loss and logging passes
     {
-      const bool cnt = valid && half == 0;
-      const float s0 = wave_sum(cnt ? viol : 0.f);
-      const float s1 = wave_sum(cnt && viol > 0.f ? 1.f : 0.f);
-      const float s2 = wave_sum(cnt ? active : 0.f);
-      if (lane == 0) *reinterpret_cast<f32x4*>(a.tile_sc + 4 * tile) = f32x4{s0, s1, s2, 0.f};
-    }
-    // ---- g_a2^T = Q3^T g_ft^T ; g_z2 = g_a2 * [a2 > 0] * scale
-    f32x16 ga[4];
+      const int tile = base + w;
+      const int row = tile * 32 + col;
+      const bool valid = row < a.N;
+      const int rr = valid ? row : a.N - 1;
+      float h[C], gft[C];
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) ga[mb] = f16_zero();
+      for (int j = 0; j < C; ++j) gft[j] = 0.f;
+      load_row10(hsrc + (size_t)rr * C, h);
+      if (tile < ntiles) {
+        const int label = (int)a.y[rr / a.S];
+        float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
+        load_row10(a.ft_ws + (size_t)rr * C, ft);
+        barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+        qp_bisect(lower, nominal, K0, a.d.tol, v, mu);
+        // V = (1 + max_{j != y} h_j) - h_y ; j* first index (lya_cands.py:84-94)
+        int js = label == 0 ? 1 : 0;
+        float hm = h[js];
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const float bs = half ? gft[2 * s + 1] : gft[2 * s];
+        for (int j = 0; j < C; ++j)
+          if (j != label && h[j] > hm) { hm = h[j]; js = j; }
+        float hy = 0.f, fy = 0.f, fj = 0.f;
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) ga[mb] = mfma32(q3t[mb][s], bs, ga[mb]);
-    }
-    const float* a2r = a.a2 + (size_t)rr * M;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      f32x16 act;
-      load_acc_rows(a2r, mb, half, act);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ga[mb][r] = act[r] > 0.f ? ga[mb][r] * a.drop_scale : 0.f;
-      if (valid) store_acc_rows(a.gz2 + (size_t)row * M, mb, half, ga[mb]);
-    }
-    // ---- g_a1^T = Q2^T g_z2^T ; g_z1 = g_a1 * [a1 > 0] * scale
-    f32x16 gb[4];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) gb[mb] = f16_zero();
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg)
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(Q2Ts + (32 * mb + col) * LDQ + 32 * kb + 8 * gg + 4 * half);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) gb[mb] = mfma32(q[t], ga[kb][4 * gg + t], gb[mb]);
+        for (int j = 0; j < C; ++j) {
+          hy = (j == label) ? h[j] : hy;
+          fy = (j == label) ? v[j] : fy;
+          fj = (j == js) ? v[j] : fj;
         }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const float* a1r = a.a1 + (size_t)rr * M;
+        const float Vv = (1.0f + hm) - hy;
+        const float Vd = fj - fy;                  // jvp of the piecewise-linear V along f
+        const float pre = Vd + a.kappa * Vv;       // vdot + kappa * V.detach() (pl_modules.py:455-457)
+        const float viol = pre > 0.f ? pre : 0.f;
+        const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
+        float g[C], g_nom[C], g_low[C];
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      f32x16 act;
-      load_acc_rows(a1r, mb, half, act);
+        for (int j = 0; j < C; ++j) g[j] = (j == js) ? gp : ((j == label) ? -gp : 0.f);
+        qp_backward_row(g, v, mu, nominal, g_nom, g_low);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) gb[mb][r] = act[r] > 0.f ? gb[mb][r] * a.drop_scale : 0.f;
-      if (valid) store_acc_rows(a.gz1 + (size_t)row * M, mb, half, gb[mb]);
+        for (int j = 0; j < C; ++j)
+          gft[j] = a.d.scale_nominal ? ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j] : g_nom[j];
+        if (valid && half == 0) {
+          if (a.V) a.V[row] = Vv;
+          if (a.Vdot) a.Vdot[row] = Vd;
+          if (a.f) store_row10(a.f + (size_t)row * C, v);
+          if (a.g_ftilde) store_row10(a.g_ftilde + (size_t)row * C, gft);
+        }
+        // logging pass: QP to K1, active-constraint count (pl_modules.py:476-482)
+        float fl[C], nom1[C], mu1;
+        load_row10(a.ft_ws + ((size_t)a.N + rr) * C, ft);
+        barrier_nominal(a.d, h, ft, lower, nom1, sig, span);
+        qp_bisect(lower, nom1, K1, a.d.tol, fl, mu1);
+        float active = 0.f;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          const float lin = -a.d.alpha_1 * h[j];
+          const float up = a.d.alpha_2 * (1.0f - h[j]);
+          active += (fabsf(fl[j] - lin) <= 1e-6f || fabsf(fl[j] - up) <= 1e-6f) ? 1.f : 0.f;
+        }
+        if (valid && half == 0 && a.f_log) store_row10(a.f_log + (size_t)row * C, fl);
+        const bool cnt = valid && half == 0;
+        const float s0 = wave_sum(cnt ? viol : 0.f);
+        const float s1 = wave_sum(cnt && viol > 0.f ? 1.f : 0.f);
+        const float s2 = wave_sum(cnt ? active : 0.f);
+        if (lane == 0) *reinterpret_cast<f32x4*>(a.tile_sc + 4 * tile) = f32x4{s0, s1, s2, 0.f};
+      }
+      if (half == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          st.gf[w][col][c] = gft[c];
+          st.hh[w][col][c] = valid ? h[c] : 0.f;
+        }
+      }
     }
+    __syncthreads();
+    // ---------------- phase B: the round's tiles in turn, all waves
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+      const int tile = base + t;
+      if (tile >= ntiles) break;                   // block-uniform
+      const int row = tile * 32 + col;
+      const int rr = row < a.N ? row : a.N - 1;
+      const int b = rr / a.S;
+      float h[C];
+      load_row10(hsrc + (size_t)rr * C, h);
+      const uint4 k1 = a.kw[rr], k2 = a.kw[(size_t)a.N + rr];
+      const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w};
+      const uint32_t kw2w = w == 0 ? k2.x : (w == 1 ? k2.y : (w == 2 ? k2.z : k2.w));
+      // layer 1 (all units): z1 = u[b] + Q1 h, dropout-ReLU
+      f32x16 z1[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)b * M, mb, half, z1[mb]);
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const float bs = half ? h[2 * s + 1] : h[2 * s];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) z1[mb] = mfma32(q1[mb][s], bs, z1[mb]);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) dropout_relu(z1[mb], kw1[mb], half, a.drop_scale);
+      f32x16 z1w;                                  // this wave's block of a1 (w is wave-uniform)
+      if (w == 0) z1w = z1[0];
+      else if (w == 1) z1w = z1[1];
+      else if (w == 2) z1w = z1[2];
+      else z1w = z1[3];
+      // layer 2, block w: z2 = b2 + Q2 a1
+      f32x16 z2;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z2[4 * g + e] = b2w[g][e];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(Q2s + (32 * w + col) * LDQ + 32 * kb + 8 * g + 4 * half);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) z2 = mfma32(q[e], z1[kb][4 * g + e], z2);
+        }
+      dropout_relu(z2, kw2w, half, a.drop_scale);
+      // g_a2^T block w = Q3^T g_ft^T ; g_z2 = g_a2 [a2 > 0] * scale
+      f32x16 ga = f16_zero();
+#pragma unroll
+      for (int s = 0; s < 5; ++s) ga = mfma32(q3t[s], st.gf[t][col][2 * s + half], ga);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ga[r] = z2[r] > 0.f ? ga[r] * a.drop_scale : 0.f;
+      store_acc_rows(&st.a1[col][0], w, half, z1w);
+      store_acc_rows(&st.a2[col][0], w, half, z2);
+      store_acc_rows(&st.g2[col][0], w, half, ga);
+      __syncthreads();
+      // g_a1^T block w = Q2^T g_z2^T: A = Q2[32kb + 8g + 4half + e][32w + col], B = g_z2[n = col][32kb + 8g + 4half + e]
+      f32x16 gb = f16_zero();
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 gz = *reinterpret_cast<const f32x4*>(&st.g2[col][32 * kb + 8 * g + 4 * half]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            gb = mfma32(Q2s[(32 * kb + 8 * g + 4 * half + e) * LDQ + 32 * w + col], gz[e], gb);
+        }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb[r] = z1w[r] > 0.f ? gb[r] * a.drop_scale : 0.f;
+      store_acc_rows(&st.g1[col][0], w, half, gb);
+      __syncthreads();
+      // weight gradients of this tile: wave w's quarter
+#pragma unroll 4
+      for (int s = 0; s < 16; ++s) {
+        const int n = 2 * s + half;
+        const float av = st.g2[n][32 * w + col];
+        db2 += av;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) dq2[kb] = mfma32(av, st.a1[n][32 * kb + col], dq2[kb]);
+        const float fv = col < C ? st.gf[t][n][col] : 0.f;
+        if (w == 0) db3 += fv;
+        dq3 = mfma32(fv, st.a2[n][32 * w + col], dq3);
+        dq1 = mfma32(st.g1[n][32 * w + col], col < C ? st.hh[t][n][col] : 0.f, dq1);
+      }
+      // this tile's per-image partial of g_u: rows in order, one segment per image (threads 0..127)
+      if (threadIdx.x < M) {
+        const int i = threadIdx.x;
+        const int r0 = tile * 32;
+        const int nrow = a.N - r0 < 32 ? a.N - r0 : 32;
+        float g[32];
+#pragma unroll
+        for (int n = 0; n < 32; ++n) g[n] = st.g1[n][i];
+        int next = (r0 / a.S + 1) * a.S - r0;        // first row of the next image
+        float acc = 0.f;
+        int seg = 0;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) {
+          if (n < nrow) {
+            if (n == next) {
+              a.gu_tiles[((size_t)tile * a.nseg + seg) * M + i] = acc;
+              acc = 0.f;
+              ++seg;
+              next += a.S;
+            }
+            acc += g[n];
+          }
+        }
+        a.gu_tiles[((size_t)tile * a.nseg + seg) * M + i] = acc;
+      }
+      __syncthreads();
+    }
+  }
+  // ---- this workgroup's partial: added into its XCD's float64 sum with L2 atomics (the XCD id
+  // from the hardware register, so every address of a per-XCD sum is touched by one L2 only;
+  // workgroup scope keeps the atomic in that L2: no HBM traffic but the final write-back of
+  // 8 x 154 KB).  The 32 float partials of an element add EXACTLY in float64 unless their
+  // exponents span more than ~29 binades, so the sum -- and the float gradient rounded from it --
+  // does not depend on the order the workgroups arrive in.  Or (FIODE_DETERMINISTIC=1) its own
+  // slab, summed by k_lyap_reduce in a fixed order.
+  db2 += shfl_xor32(db2);
+  db3 += shfl_xor32(db3);
+  if (a.xslabs) {
+    const unsigned xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;     // hwreg(HW_REG_XCC_ID, 0, 4)
+    double* xs = a.xslabs + (size_t)xcd * SLAB;
+    auto add = [](double* p, float v) {
+      __hip_atomic_fetch_add(p, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) add(xs + SLAB_Q2 + (32 * w + acc_row(r, half)) * M + 32 * kb + col, dq2[kb][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, half);
+      if (i < C) add(xs + SLAB_Q3 + i * M + 32 * w + col, dq3[r]);
+      if (col < C) add(xs + SLAB_Q1 + (32 * w + i) * C + col, dq1[r]);
+    }
+    if (half == 0) {
+      add(xs + SLAB_B2 + 32 * w + col, db2);
+      if (w == 0 && col < C) add(xs + SLAB_B3 + col, db3);
+    }
+    return;
+  }
+  float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) slab[SLAB_Q2 + (32 * w + acc_row(r, half)) * M + 32 * kb + col] = dq2[kb][r];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = acc_row(r, half);
+    if (i < C) slab[SLAB_Q3 + i * M + 32 * w + col] = dq3[r];
+    if (col < C) slab[SLAB_Q1 + (32 * w + i) * C + col] = dq1[r];
+  }
+  if (half == 0) {
+    slab[SLAB_B2 + 32 * w + col] = db2;
+    if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
   }
 }
 
@@ -436,10 +595,23 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
   __shared__ float part[4][RED_COLS];
   __shared__ double dpart[3][256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nwg = a.B * a.parts;
+  const int nwg = a.nslab;
   const int n_el_blocks = (SLAB + RED_COLS - 1) / RED_COLS;
   const int n_gu_blocks = (a.B * M + RED_COLS - 1) / RED_COLS;
-  if ((int)blockIdx.x < n_el_blocks) {
+  if ((int)blockIdx.x < n_el_blocks && a.xslabs) {     // the 8 per-XCD float64 sums, fixed order
+    const int e = blockIdx.x * RED_COLS + lane;
+    if (wv == 0 && e < SLAB) {
+      double d = 0.0;
+#pragma unroll
+      for (int x = 0; x < 8; ++x) d += a.xslabs[(size_t)x * SLAB + e];
+      const float t = (float)d;
+      if (e < SLAB_Q3) a.grads.Q2[e] = t;
+      else if (e < SLAB_Q1) a.grads.Q3[e - SLAB_Q3] = t;
+      else if (e < SLAB_B2) a.grads.Q1[e - SLAB_Q1] = t;
+      else if (e < SLAB_B1) a.grads.b2[e - SLAB_B2] = t;
+      else if (e >= SLAB_B3 && e < SLAB_B3 + C) a.grads.b3[e - SLAB_B3] = t;
+    }
+  } else if ((int)blockIdx.x < n_el_blocks) {
     const int e = blockIdx.x * RED_COLS + lane;
     float s = 0.f;
     if (e < SLAB) {
@@ -467,7 +639,15 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
     if (threadIdx.x < RED_COLS && q < a.B * M) {
       const int b = q / M, i = q - b * M;
       float s = 0.f;
-      for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
+      if (a.gu_tiles) {           // fused backward: the tiles holding rows of image b, in order
+        const int t0 = (int)(((size_t)b * a.S) / 32), t1 = (int)(((size_t)(b + 1) * a.S - 1) / 32);
+        for (int t = t0; t <= t1; ++t) {
+          const int seg = b - (int)(((size_t)t * 32) / a.S);
+          s += a.gu_tiles[((size_t)t * a.nseg + seg) * M + i];
+        }
+      } else {
+        for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
+      }
       a.g_u[q] = s;
     }
   } else if (a.tile_sc) {                                           // scalars
@@ -526,8 +706,18 @@ __global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
 
 // ---- workspace ----------------------------------------------------------------------------------
 struct WsLayout {
-  size_t conv, u, h, ft, a1, a2, gz2, gz1, gft, kw, tsc, slabs, gu, q2t, total;
+  size_t conv, u, h, ft, kw, tsc, slabs, gut, gu, total;
+  int nslab, nseg;
+  bool xcd;                 // per-XCD atomic sums instead of per-workgroup slabs
 };
+// FIODE_DETERMINISTIC=1: the fused backward writes one partial slab per workgroup and the reduce
+// sums them in a fixed float order (bit-reproducible by construction, ~39 MB more HBM traffic per
+// step); default: per-XCD float64 sums by L2 atomics (exact, hence order-free, unless an element's
+// partials span > ~29 binades).
+inline bool deterministic_grads() {
+  const char* e = getenv("FIODE_DETERMINISTIC");
+  return e && *e && *e != '0';
+}
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline void parts_for(int B, int S, int& parts, int& chunk) {
   parts = (256 + B - 1) / B;
@@ -537,26 +727,31 @@ inline void parts_for(int B, int S, int& parts, int& chunk) {
   chunk = (S + parts - 1) / parts;
   chunk = (chunk + 1) & ~1;
 }
+// fused backward: one workgroup per 4 tiles up to one per CU (BWD_LDS: one resident per CU); its
+// partial slab count is the grid size
+constexpr int BWD_MAX_WG = 256;
+inline int bwd_grid(size_t N) {
+  const int ntiles = (int)((N + 31) / 32);
+  const int g = (ntiles + 3) / 4;
+  return g < BWD_MAX_WG ? g : BWD_MAX_WG;
+}
 inline WsLayout ws_layout(int B, int S) {
   const size_t N = (size_t)B * S;
-  int parts, chunk;
-  parts_for(B, S, parts, chunk);
+  const size_t ntiles = (N + 31) / 32;
   WsLayout L;
+  L.nslab = bwd_grid(N);
+  L.xcd = !deterministic_grads();
+  L.nseg = S >= 32 ? 2 : (31 / S + 2 > 32 ? 32 : 31 / S + 2);   // images one 32-row tile can span
   size_t o = 0;
   L.conv = o; o = al(o + 16);
   L.u = o; o = al(o + (size_t)B * M * 4);
   L.h = o; o = al(o + N * C * 4);
   L.ft = o; o = al(o + 2 * N * C * 4);
-  L.a1 = o; o = al(o + N * M * 4);
-  L.a2 = o; o = al(o + N * M * 4);
-  L.gz2 = o; o = al(o + N * M * 4);
-  L.gz1 = o; o = al(o + N * M * 4);
-  L.gft = o; o = al(o + N * C * 4);
   L.kw = o; o = al(o + 4 * N * 16);
-  L.tsc = o; o = al(o + ((N + 31) / 32) * 16);
-  L.slabs = o; o = al(o + (size_t)B * parts * SLAB * 4);
+  L.tsc = o; o = al(o + ntiles * 16);
+  L.slabs = o; o = al(o + (size_t)(L.xcd ? 16 : L.nslab) * SLAB * 4);   // XCD mode: 8 float64 sums
+  L.gut = o; o = al(o + ntiles * L.nseg * M * 4);
   L.gu = o; o = al(o + (size_t)B * M * 4);
-  L.q2t = o; o = al(o + (size_t)M * M * 4);
   L.total = o;
   return L;
 }
@@ -621,16 +816,14 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.u = reinterpret_cast<float*>(ws + L.u);
   a.h_ws = reinterpret_cast<float*>(ws + L.h);
   a.ft_ws = reinterpret_cast<float*>(ws + L.ft);
-  a.a1 = reinterpret_cast<float*>(ws + L.a1);
-  a.a2 = reinterpret_cast<float*>(ws + L.a2);
-  a.gz2 = reinterpret_cast<float*>(ws + L.gz2);
-  a.gz1 = reinterpret_cast<float*>(ws + L.gz1);
-  a.gft = reinterpret_cast<float*>(ws + L.gft);
   a.kw = reinterpret_cast<uint4*>(ws + L.kw);
   a.tile_sc = reinterpret_cast<float*>(ws + L.tsc);
   a.slabs = reinterpret_cast<float*>(ws + L.slabs);
+  a.nslab = L.nslab;
+  a.xslabs = L.xcd ? reinterpret_cast<double*>(a.slabs) : nullptr;
+  a.gu_tiles = reinterpret_cast<float*>(ws + L.gut);
+  a.nseg = L.nseg;
   a.g_u = reinterpret_cast<float*>(ws + L.gu);
-  a.Q2T = reinterpret_cast<float*>(ws + L.q2t);
   a.scalars = io->scalars;
   a.h_out = io->h_out; a.V = io->V; a.Vdot = io->Vdot; a.f = io->f; a.f_log = io->f_log;
   a.qp_lower = io->qp_lower; a.qp_nominal = io->qp_nominal; a.g_ftilde = io->g_ftilde;
@@ -648,11 +841,10 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
     return 0;
   };
   const int ntiles = (a.N + 31) / 32;
-  const int fwd_blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
+  const int fwd_blocks = (ntiles + 1) / 2;                // 2 tiles x 2 passes per workgroup
   const size_t lds_fwd = (size_t)(M + C) * LDQ * sizeof(float);
-  const size_t lds_bwd = (size_t)M * LDQ * sizeof(float);
   if ((rc = mark())) return rc;
-  hipLaunchKernelGGL(k_static_proj, dim3(B > M ? B : M), dim3(128), 0, st, a);
+  hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_prep, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
@@ -661,10 +853,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   hipLaunchKernelGGL(k_lyap_fwd, dim3(fwd_blocks), dim3(256), lds_fwd, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
-  hipLaunchKernelGGL(k_lyap_bwd, dim3(fwd_blocks), dim3(256), lds_bwd, st, a);
-  FIODE_HIP_CHECK(hipGetLastError());
-  if ((rc = mark())) return rc;
-  hipLaunchKernelGGL(k_lyap_wgrad, dim3(B * a.parts), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_lyap_bwd, dim3(L.nslab), dim3(256), BWD_LDS, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
   const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (B * M + RED_COLS - 1) / RED_COLS + 1;
@@ -698,6 +887,8 @@ int launch_wgrad(hipStream_t st, const WgradIO& io) {
   a.slabs = reinterpret_cast<float*>(ws);
   a.g_u = reinterpret_cast<float*>(ws + al((size_t)a.B * a.parts * SLAB * 4));
   a.tile_sc = nullptr;
+  a.nslab = a.B * a.parts;
+  a.gu_tiles = nullptr;
   a.grads = io.grads;
   hipLaunchKernelGGL(k_lyap_wgrad, dim3(a.B * a.parts), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());

@@ -617,7 +617,7 @@ __global__ __launch_bounds__(256) void k_ode_tiles(OsArgs a) {
   float* Q3s = smem + M * LDQ;
   OsShared& sh = *reinterpret_cast<OsShared*>(smem + (M + 32) * LDQ);
   OsTile* tl = reinterpret_cast<OsTile*>(reinterpret_cast<char*>(&sh) + sizeof(OsShared));
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, false);
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s);
   for (int t = threadIdx.x; t < M * C; t += blockDim.x) sh.Q1s[t] = a.Q1[t];
   if (threadIdx.x == 0) {
     sh.kprev = a.d.max_iter - 1;

@@ -66,7 +66,7 @@ struct OTArgs {
   unsigned long long* xslots;  // [E][2 phases][ntiles] {epoch, mask} granules of the QP exit exchange
   uint32_t* kw;                // [E][2][B] uint4 dropout keep words
 #ifdef OT_PROFILE
-  unsigned long long* prof;    // [8] wall-clock ticks per phase (workgroup 0, lane 0)
+  unsigned long long* prof;    // [9] wall-clock ticks per phase (workgroup 0, lane 0); [16 + e] eval e's exit K
 #endif
 };
 
@@ -173,6 +173,9 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
     a.muw[r] = mu;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) a.stats[2] = K;
+#ifdef OT_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0 && e < 96) a.prof[16 + e] = (unsigned long long)K;
+#endif
   if (threadIdx.x == 0) sh.Kprev = K;
   __syncthreads();            // zpart / mu_rec / K reused by the next eval
   OT_MARK(4);
@@ -531,7 +534,7 @@ OtLayout ot_layout(int B, int E) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  L.xs = o; o += al((size_t)E * 2 * ((B + TR - 1) / TR) * 8 + 256);
+  L.xs = o; o += al((size_t)E * 2 * ((B + TR - 1) / TR) * 8 + 1024);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
   L.total = o;
@@ -627,7 +630,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   const size_t lds = sizeof(OtShared);     // the weights live in registers (tile16.h T16W)
   // k_ot_masks zeroes the exchange granules (tags) and the status words before every forward, and
   // draws the dropout keep words when dropout is on
-  a.nslots = (int)(((size_t)a.E * 2 * ntiles * 8 + 256) / 8);
+  a.nslots = (int)(((size_t)a.E * 2 * ntiles * 8 + 1024) / 8);
   const int nthreads = a.nslots > a.E * a.B ? a.nslots : a.E * a.B;
   hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());

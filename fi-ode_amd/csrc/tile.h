@@ -62,12 +62,12 @@ __device__ __forceinline__ void gather_ft(const f32x16& z3, int half, float (&ft
   }
 }
 
-// The MLP of one wave tile: layers 1-3, returns the layer-3 accumulator; z1/z2 hold the
-// post-dropout-ReLU activations a1^T, a2^T.  q1: hoisted layer-1 A operands.
-__device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, const float (&q1)[4][5],
-                                           const float* u_row, const float* b2, const float* b3,
-                                           const float (&h)[C], const uint32_t (&kw1)[4], const uint32_t (&kw2)[4],
-                                           float scale, int col, int half, f32x16 (&z1)[4], f32x16 (&z2)[4]) {
+// Layers 1-2 of the MLP of one wave tile: z1/z2 become the post-dropout-ReLU activations a1^T,
+// a2^T.  q1: hoisted layer-1 A operands.
+__device__ __forceinline__ void mlp12_tile(const float* Q2s, const float (&q1)[4][5], const float* u_row,
+                                           const float* b2, const float (&h)[C], const uint32_t (&kw1)[4],
+                                           const uint32_t (&kw2)[4], float scale, int col, int half, f32x16 (&z1)[4],
+                                           f32x16 (&z2)[4]) {
   // layer 1: z1 = u[b] + Q1 h   (hidden_to_mlp(h) + U_x(x), classification.py:97)
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) load_acc_rows(u_row, mb, half, z1[mb]);
@@ -96,6 +96,14 @@ __device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, c
   }
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) dropout_relu(z2[mb], kw2[mb], half, scale);
+}
+
+// The MLP of one wave tile: layers 1-3, returns the layer-3 accumulator (mlp12_tile + layer 3).
+__device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, const float (&q1)[4][5],
+                                           const float* u_row, const float* b2, const float* b3,
+                                           const float (&h)[C], const uint32_t (&kw1)[4], const uint32_t (&kw2)[4],
+                                           float scale, int col, int half, f32x16 (&z1)[4], f32x16 (&z2)[4]) {
+  mlp12_tile(Q2s, q1, u_row, b2, h, kw1, kw2, scale, col, half, z1, z2);
   // layer 3: z3 = b3 + Q3 a2 (rows >= 10 of the 32-row tile are zero weights)
   f32x16 z3;
 #pragma unroll
@@ -116,19 +124,32 @@ __device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, c
   return z3;
 }
 
-// Stage the 128x128 mlp_to_mlp weight (optionally transposed) and the 10x128 mlp_to_hidden weight
-// (zero-padded to 32 rows) into padded LDS images.
+// Stage the 128x128 mlp_to_mlp weight and the 10x128 mlp_to_hidden weight (zero rows up to
+// q3_rows) into padded LDS images: 16-byte global loads, all of a thread's loads in flight
+// together (a dependent 4-byte load loop took ~15 us of L2 latency at kernel start).
 __device__ __forceinline__ void load_weight_images(const float* Q2, const float* Q3, float* Q2s, float* Q3s,
-                                                   bool transpose_q2, int q3_rows = 32) {
-  for (int e = threadIdx.x; e < M * M; e += blockDim.x) {
-    const int i = e >> 7, k = e & 127;
-    if (transpose_q2) Q2s[k * LDQ + i] = Q2[e];
-    else Q2s[i * LDQ + k] = Q2[e];
-  }
-  if (Q3s)
-    for (int e = threadIdx.x; e < q3_rows * M; e += blockDim.x) {
-      const int i = e >> 7, k = e & 127;
-      Q3s[i * LDQ + k] = i < C ? Q3[i * M + k] : 0.f;
+                                                   int q3_rows = 32) {
+  const f32x4* Q2v = reinterpret_cast<const f32x4*>(Q2);
+  constexpr int N2 = M * M / 4;                        // 4096 float4
+  for (int e0 = threadIdx.x; e0 < N2; e0 += 8 * blockDim.x) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * blockDim.x;
+      if (e < N2) v[u] = Q2v[e];
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * blockDim.x;
+      if (e < N2) *reinterpret_cast<f32x4*>(Q2s + (e >> 5) * LDQ + (e & 31) * 4) = v[u];
+    }
+  }
+  if (Q3s) {
+    const f32x4* Q3v = reinterpret_cast<const f32x4*>(Q3);
+    for (int e = threadIdx.x; e < q3_rows * M / 4; e += blockDim.x) {
+      const int i = e >> 5;
+      *reinterpret_cast<f32x4*>(Q3s + i * LDQ + (e & 31) * 4) = i < C ? Q3v[e] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 }
 }  // namespace fiode_tile

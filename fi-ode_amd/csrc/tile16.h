@@ -137,13 +137,7 @@ __device__ __forceinline__ void qp_bracket(const float (&lower)[C], const float 
 }
 // eps(mu) = sum_j max(nom_j - mu, lower_j) in the reference's order.  Only its comparisons with 0
 // and tol are used, so the sum starts at term 0 (0 + t0 differs from t0 only in the sign of a zero)
-// and max is a bare v_max_f32 (fmaxf's result for every non-signalling input; the compiler's fmaxf
-// re-quiets `lower` at every use when the operand comes from another basic block: +10 VALU / eps).
-__device__ __forceinline__ float vmax_f32(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+// and max is vmax_f32 (common.h).
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float qp_eps(const float (&lower)[C], const float (&nom)[C], float mu) {
   const f2v m2 = f2v{mu, mu};

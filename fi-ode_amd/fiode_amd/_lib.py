@@ -51,8 +51,7 @@ class LyapIO(ct.Structure):
          ("exp_draws_out", ct.c_void_p), ("keep_words_out", ct.c_void_p)]
 
 
-LYAP_KERNELS = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_wgrad", "k_lyap_reduce",
-                "k_lyap_static_grads")
+LYAP_KERNELS = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_reduce", "k_lyap_static_grads")
 
 
 class LyapGrads(ct.Structure):

@@ -156,8 +156,10 @@ class UniformInitFun(nn.Module):
 # Capture order of the Cayley-map prefetch in the training step: after the step's input kernels
 # (the hipGraph executor dispatches in capture order; maps captured ahead of the input
 # normalisation held the conv stack back): 2.41 -> 2.32 ms per step in the interleaved A/B of
-# tools/ab_step.py, better than every deferral of the linear / dynamics maps tried.
-DEFAULT_PREFETCH_SCHEDULE = {"after_input": True}
+# tools/ab_step.py, better than every deferral of the linear / dynamics maps tried.  The linear /
+# dynamics maps captured ahead of the conv maps ("lin_first"): 2.143 -> 2.090 ms (round 2 A/B, 6
+# interleaved rounds; one batched launch sequence for both 512 x 512 maps: 2.209).
+DEFAULT_PREFETCH_SCHEDULE = {"after_input": True, "order": "lin_first"}
 
 
 class LyapunovLearning(nn.Module):

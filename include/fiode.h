@@ -114,9 +114,9 @@ typedef struct fiode_lyap_io {
 } fiode_lyap_io;
 
 /* kernels of one fiode_lyap_step, in launch order (for the profiling events) */
-#define FIODE_LYAP_NKERNELS 7
+#define FIODE_LYAP_NKERNELS 6
 /* static_proj, prep (sampler + dropout words), fwd (2 eval_dot passes), bwd (QP finalize + loss +
- * activation grads), wgrad (weight-gradient GEMMs), reduce, static_grads */
+ * activation grads + weight-gradient GEMMs, one partial slab per workgroup), reduce, static_grads */
 
 typedef struct fiode_lyap_grads {  /* outputs, overwritten: d loss / d (effective weights) */
   float *Q1, *b1, *Qx, *bx, *Q2, *b2, *Q3, *b3;

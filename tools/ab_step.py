@@ -1,7 +1,7 @@
 """Interleaved A/B of step variants (not a test): every variant's hipGraph step is captured first,
 then replayed round-robin (R rounds x K steps each), so box-level drift hits all variants alike.
 
-python tools/ab_step.py [rounds]  ->  one JSON line: median ms per step per variant
+python tools/ab_step.py [rounds] [variant,variant,...]  ->  one JSON line: median ms per step per variant
 """
 import json
 import pathlib
@@ -125,8 +125,11 @@ def ode_on_main(m):
     m.ode_side_stream = False
 
 
-VARIANTS = {"default": reset2, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main}
+ALL = {"default": reset2, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
+       "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "small_bwd_main", "ode_on_main"]
+VARIANTS = {k: ALL[k] for k in names}
 steps = {}
 for k, f in VARIANTS.items():
     steps[k] = make(f)

@@ -9,10 +9,10 @@ from tests._util import make_params
 dev = torch.device("cuda:0")
 P = make_params(1)
 w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
-for B in (128, 1024):
+for B, sn in ((128, False), (128, True), (1024, False)):
     x = torch.randn(B, 10, device=dev); h0 = torch.full((B, 10), 0.1, device=dev)
     cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=3)
-    dyn = ops.DynCfg(scale_nominal=False, dropout=0.5)
+    dyn = ops.DynCfg(scale_nominal=sn, dropout=0.5)
     for rep in range(3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(); y, st, ws = ops.odetrain_forward(x, h0, w, dyn, cfg); e1.record(); torch.cuda.synchronize()
@@ -25,9 +25,10 @@ for B in (128, 1024):
     lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
     al = lambda v: (v + 255) & ~255
     xs = offs[7] + al(B * E * 10 * 4)
-    prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 17) * 8].view(torch.int64).cpu().numpy()
+    prof = ws[xs + (2 * E * nt + 8) * 8: xs + (2 * E * nt + 8 + 16 + E) * 8].view(torch.int64).cpu().numpy()
+    Ks = prof[16:16 + E].tolist()               # the last rep's exit K of every eval
     ticks = prof[:8] / E          # 100 MHz wall clock -> 10 ns per tick
     print(f"B={B} total {e0.elapsed_time(e1)*1e3:.0f} us, per eval (us): mlp {ticks[1]*0.01:.2f} "
           f"partial sums+nominal {ticks[5]*0.01:.2f} bisection+exit exchange {ticks[3]*0.01:.2f} "
           f"(bisection {ticks[6]*0.01:.2f}, exchange wait {ticks[7]*0.01:.2f}, resumes {int(prof[8])}/{E}) "
-          f"finalize {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()}", flush=True)
+          f"finalize {ticks[4]*0.01:.2f}  status {st.cpu().numpy().tolist()} scale_nominal={sn}\n  exit K per eval: {Ks}", flush=True)
