@@ -33,6 +33,24 @@
 namespace {
 using namespace fiode_tile;
 
+// Phase timing (OT_PROFILE builds, tools/lyap_probe.py): lane 0 of every wave of workgroups 0..7
+// adds the wall-clock ticks (100 MHz) of each phase into prof[i] (a sample: all workgroups' atomics
+// on one word would time their own contention); LY_COUNT(i) counts the sampled waves.
+#ifdef OT_PROFILE
+#define LY_T0() uint64_t ly_t_ = wall_clock64()
+#define LY_T(i) do { const uint64_t n_ = wall_clock64(); if ((threadIdx.x & 63) == 0 && blockIdx.x < 8) \
+    atomicAdd(a.prof + (i), (unsigned long long)(n_ - ly_t_)); ly_t_ = n_; } while (0)
+#define LY_COUNT(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 8) atomicAdd(a.prof + (i), 1ull); } while (0)
+// per-workgroup start / end stamps of wave 0 (slot base: fwd 64, bwd 64 + 2 * 1024)
+#define LY_STAMP(base, k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
+    a.prof[(base) + 2 * blockIdx.x + (k)] = wall_clock64(); } while (0)
+#else
+#define LY_STAMP(base, k) do { } while (0)
+#define LY_T0() do { } while (0)
+#define LY_T(i) do { } while (0)
+#define LY_COUNT(i) do { } while (0)
+#endif
+
 constexpr int SLAB = 16384 + 1280 + 1280 + 128 + 128 + 16;   // floats per wgrad partial slab
 constexpr int SLAB_Q2 = 0, SLAB_Q3 = 16384, SLAB_Q1 = 16384 + 1280, SLAB_B2 = 16384 + 2560,
               SLAB_B1 = 16384 + 2560 + 128, SLAB_B3 = 16384 + 2560 + 256;
@@ -65,6 +83,7 @@ struct LyapArgs {
   int nslab;           // partial slabs summed by k_lyap_reduce
   float* g_u;          // [B][M]
   float* gu_tiles;     // fused backward: per-(tile, image segment) partial g_u [ntiles][nseg][M] (else null)
+  unsigned long long* prof;   // OT_PROFILE builds: per-phase wall-clock ticks summed over waves
   double* xslabs;      // fused backward, XCD mode: [8][SLAB] per-XCD sums (L2 float64 atomics), else null
   int nseg;            // image segments per 32-row tile (images a tile's rows can span)
   // outputs
@@ -165,6 +184,7 @@ __device__ __forceinline__ void keep_words(const LyapArgs& a, int row, int set, 
 __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
   const int b = blockIdx.x, i = threadIdx.x;
   if (b == 0 && i < 2) a.conv[i] = 0xFFFFFFFFu;
+  if (b == 0 && a.prof && i < 64) a.prof[i] = 0ull;
   if (b >= a.B) return;
   float s = 0.f;
   const float* xb = a.x_feat + (size_t)b * FIODE_X;
@@ -207,10 +227,14 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
 // per pass into one word (the batch-global exit, barrier_projection.py:247-249).
 __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  LY_T0();
+  LY_COUNT(6);
+  LY_STAMP(64, 0);
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, C);
   __syncthreads();
+  LY_T(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];
 #pragma unroll
@@ -228,13 +252,17 @@ __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
     load_row10(((a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws) + (size_t)rr * C, h);
     const uint4 k1 = a.kw[(size_t)(2 * pass) * a.N + rr], k2 = a.kw[(size_t)(2 * pass + 1) * a.N + rr];
     const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w}, kw2[4] = {k2.x, k2.y, k2.z, k2.w};
+    LY_T(1);
     f32x16 z1[4], z2[4];
     const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
                                col, half, z1, z2);
+    LY_T(2);
     float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
     gather_ft(z3, half, ft);
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+    LY_T(3);
     uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
+    LY_T(4);
     if (!valid) conv = 0xFFFFFFFFu;
     conv = wave_and(conv);
     if (lane == 0) atomicAnd(a.conv + pass, conv);
@@ -243,7 +271,9 @@ __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
       if (a.qp_nominal) store_row10(a.qp_nominal + ((size_t)pass * a.N + row) * C, nominal);
       if (pass == 0 && a.qp_lower) store_row10(a.qp_lower + (size_t)row * C, lower);
     }
+    LY_T(5);
   }
+  LY_STAMP(64, 1);
 }
 
 // One tile's operands of the backward's second half and of the weight gradients, staged
@@ -277,8 +307,12 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   float* Q3s = smem + M * LDQ;               // Q3 rows 0..C-1 (unused here: the layout of k_lyap_fwd)
   (void)Q3s;
   BwdStage& st = *reinterpret_cast<BwdStage*>(smem + (M + C) * LDQ);
+  LY_T0();
+  LY_COUNT(18);
+  LY_STAMP(64 + 2048, 0);
   load_weight_images(a.Q2, nullptr, Q2s, nullptr);
   __syncthreads();
+  LY_T(8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5], q3t[5];
 #pragma unroll
@@ -374,6 +408,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       }
     }
     __syncthreads();
+    LY_T(9);
     // ---------------- phase B: the round's tiles in turn, all waves
 #pragma unroll 1
     for (int t = 0; t < 4; ++t) {
@@ -428,7 +463,9 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       store_acc_rows(&st.a1[col][0], w, half, z1w);
       store_acc_rows(&st.a2[col][0], w, half, z2);
       store_acc_rows(&st.g2[col][0], w, half, ga);
+      LY_T(10);
       __syncthreads();
+      LY_T(11);
       // g_a1^T block w = Q2^T g_z2^T: A = Q2[32kb + 8g + 4half + e][32w + col], B = g_z2[n = col][32kb + 8g + 4half + e]
       f32x16 gb = f16_zero();
 #pragma unroll
@@ -443,7 +480,9 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) gb[r] = z1w[r] > 0.f ? gb[r] * a.drop_scale : 0.f;
       store_acc_rows(&st.g1[col][0], w, half, gb);
+      LY_T(12);
       __syncthreads();
+      LY_T(13);
       // weight gradients of this tile: wave w's quarter
 #pragma unroll 4
       for (int s = 0; s < 16; ++s) {
@@ -457,6 +496,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
         dq3 = mfma32(fv, st.a2[n][32 * w + col], dq3);
         dq1 = mfma32(st.g1[n][32 * w + col], col < C ? st.hh[t][n][col] : 0.f, dq1);
       }
+      LY_T(14);
       // this tile's per-image partial of g_u: rows in order, one segment per image (threads 0..127)
       if (threadIdx.x < M) {
         const int i = threadIdx.x;
@@ -482,7 +522,9 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
         }
         a.gu_tiles[((size_t)tile * a.nseg + seg) * M + i] = acc;
       }
+      LY_T(15);
       __syncthreads();
+      LY_T(16);
     }
   }
   // ---- this workgroup's partial: added into its XCD's float64 sum with L2 atomics (the XCD id
@@ -514,6 +556,8 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       add(xs + SLAB_B2 + 32 * w + col, db2);
       if (w == 0 && col < C) add(xs + SLAB_B3 + col, db3);
     }
+    LY_T(17);
+    LY_STAMP(64 + 2048, 1);
     return;
   }
   float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
@@ -752,6 +796,9 @@ inline WsLayout ws_layout(int B, int S) {
   L.slabs = o; o = al(o + (size_t)(L.xcd ? 16 : L.nslab) * SLAB * 4);   // XCD mode: 8 float64 sums
   L.gut = o; o = al(o + ntiles * L.nseg * M * 4);
   L.gu = o; o = al(o + (size_t)B * M * 4);
+#ifdef OT_PROFILE
+  o += (64 + 4096) * 8;                      // phase timers + per-workgroup stamps (the tail)
+#endif
   L.total = o;
   return L;
 }
@@ -821,6 +868,9 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.slabs = reinterpret_cast<float*>(ws + L.slabs);
   a.nslab = L.nslab;
   a.xslabs = L.xcd ? reinterpret_cast<double*>(a.slabs) : nullptr;
+#ifdef OT_PROFILE
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.total - (64 + 4096) * 8);
+#endif
   a.gu_tiles = reinterpret_cast<float*>(ws + L.gut);
   a.nseg = L.nseg;
   a.g_u = reinterpret_cast<float*>(ws + L.gu);

@@ -126,13 +126,24 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
   uint64_t t_prev = wall_clock64();
 #endif
   if (p == 0 && valid && q == 0) store_row10(a.hs + r * C, h);
-  // the barrier's lower bound depends on h only: issued ahead of the MLP so the VALU work overlaps
-  // the MFMA chain (same float32 expressions as barrier_nominal, common.h)
+  // the barrier's lower bound depends on h only: interleaved with the MLP's 96 MFMAs (explicit
+  // issue groups in one scheduling region), so its exp VALU work leaves the critical path
+  // (same float32 expressions as barrier_nominal, common.h)
   float lower[C];
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int i = 0; i < C; ++i) lower[i] = -a.d.alpha_1 * (expf(a.d.sigma_1 * h[i]) - 1.0f);
+  for (int i = 0; i < C; ++i) {
+    lower[i] = -a.d.alpha_1 * (expf(a.d.sigma_1 * h[i]) - 1.0f);
+    asm volatile("" ::"v"(lower[i]));          // keep it here (IR passes would sink it to its use)
+  }
   mlp16_part(w, uacc, h, kw1, kw2p, a.drop_scale, p, q, valid ? a.a1 + r * M : nullptr,
              valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0]);
+#pragma unroll
+  for (int i = 0; i < 96; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // one MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);     // then up to three VALU
+  }
+  __builtin_amdgcn_sched_barrier(0);
   OT_MARK(1);
   __syncthreads();
   float ft[C];
@@ -330,44 +341,66 @@ struct VjpW {
   f32x4 q1t[2];
 };
 
-__device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3],
-                       OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int q, int j,
-                       const VjpIn& in, const float (&g)[C], float (&gy_out)[C]) {
-  const int bb = valid ? b : a.B - 1;
-  const size_t r = (size_t)bb * a.E + e;
-  float h[C], ft[C], v[C], lower[C], nominal[C], sig[C], span[C];
+// The adjoint-independent row math of one VJP (barrier terms of the saved stage input and MLP
+// output): computed for the NEXT VJP inside the current one, between its MFMA chains, so the
+// exp / sigmoid VALU work leaves the adjoint's dependent chain.
+struct VjpRow {
+  float nominal[C], sig[C], span[C], es[C];     // es = exp(sigma_1 h)
+};
+template <bool SN>
+__device__ __forceinline__ void vjp_row_math(const OTArgs& a, const VjpIn& in, VjpRow& rw) {
+  // the expressions of barrier_nominal (common.h), branch-free for a compile-time scale_nominal
 #pragma unroll
   for (int i = 0; i < C; ++i) {
-    h[i] = in.h[i];
-    ft[i] = in.ft[i];
-    v[i] = in.v[i];
+    rw.es[i] = expf(a.d.sigma_1 * in.h[i]);
+    const float lower = -a.d.alpha_1 * (rw.es[i] - 1.0f);
+    const float upper = a.d.alpha_2 * (1.0f - in.h[i]);
+    rw.span[i] = upper - lower;
+    if constexpr (SN) {
+      rw.sig[i] = 1.0f / (1.0f + expf(-in.ft[i]));
+      rw.nominal[i] = rw.span[i] * rw.sig[i] + lower;
+    } else {
+      rw.sig[i] = 0.f;
+      rw.nominal[i] = in.ft[i];
+    }
   }
-  const float mu = in.mu;
-  barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
+}
+
+template <bool SN>
+__device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3],
+                       OtBwdShared& sh, int buf, int p, int e, int b, bool valid, int lane, int q, int j,
+                       const VjpIn& in, const VjpRow& rw, const VjpIn& nin, VjpRow& nrw, const float (&g)[C],
+                       float (&gy_out)[C]) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + e;
+#ifdef OT_PROFILE
+  uint64_t t_prev = wall_clock64();
+#endif
   float g_nom[C], g_low[C], gft[C], ghb[C];
   float gin[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) gin[i] = valid ? g[i] : 0.f;
-  qp_backward_row(gin, v, mu, nominal, g_nom, g_low);
+  qp_backward_row(gin, in.v, in.mu, rw.nominal, g_nom, g_low);
 #pragma unroll
   for (int i = 0; i < C; ++i) {
     float g_lo = g_low[i], g_up = 0.f;
-    if (a.d.scale_nominal) {
+    if constexpr (SN) {
       // nominal = span * sig + lower, span = upper - lower
-      gft[i] = ((g_nom[i] * span[i]) * (1.0f - sig[i])) * sig[i];
-      const float g_span = g_nom[i] * sig[i];
+      gft[i] = ((g_nom[i] * rw.span[i]) * (1.0f - rw.sig[i])) * rw.sig[i];
+      const float g_span = g_nom[i] * rw.sig[i];
       g_lo = (g_lo + g_nom[i]) - g_span;
       g_up = g_span;
     } else {
       gft[i] = g_nom[i];
     }
     // lower = -a1 (exp(s1 h) - 1), upper = a2 (1 - h)
-    ghb[i] = ((g_lo * -a.d.alpha_1) * expf(a.d.sigma_1 * h[i])) * a.d.sigma_1 + g_up * -a.d.alpha_2;
+    ghb[i] = ((g_lo * -a.d.alpha_1) * rw.es[i]) * a.d.sigma_1 + g_up * -a.d.alpha_2;
   }
   if (p == 0 && valid && q == 0) {
     store_row10(a.gft + r * C, gft);
     if (a.dbg_gft) store_row10(a.dbg_gft + r * C, gft);
   }
+  OT_MARK(10);
   // g_a2^T = Q3^T g_ft^T (all 128 hidden, 8 blocks, K = 10 in 3 k-steps), masked by the saved a2
   f32x4v ga[8];
 #pragma unroll
@@ -386,7 +419,11 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
     if (valid && (hb >> 1) == p)
       *reinterpret_cast<f32x4*>(a.gz2 + r * M + 16 * hb + 4 * q) = f32x4{ga[hb][0], ga[hb][1], ga[hb][2], ga[hb][3]};
   }
-  // hidden blocks 2p, 2p+1 of g_a1^T = Q2^T g_z2^T (two independent accumulators)
+  OT_MARK(11);
+  // hidden blocks 2p, 2p+1 of g_a1^T = Q2^T g_z2^T (two independent accumulators), with the next
+  // VJP's row math (VALU) interleaved between the 64 MFMAs: one region, explicit issue groups
+  __builtin_amdgcn_sched_barrier(0);
+  vjp_row_math<SN>(a, nin, nrw);
   f32x4v gb[2] = {z4(), z4()};
 #pragma unroll
   for (int hb = 0; hb < 8; ++hb) {
@@ -397,6 +434,12 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
     }
   }
 #pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // one MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);     // then up to six VALU
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
   for (int o = 0; o < 2; ++o) {
     const f32x4 act = in.a1[o];
 #pragma unroll
@@ -404,6 +447,7 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
     if (valid)
       *reinterpret_cast<f32x4*>(a.gz1 + r * M + 16 * (2 * p + o) + 4 * q) = f32x4{gb[o][0], gb[o][1], gb[o][2], gb[o][3]};
   }
+  OT_MARK(12);
   // partial g_h^T over hidden blocks 2p, 2p+1 (Q1^T image, rows >= 10 zero)
   f32x4v gh = z4();
 #pragma unroll
@@ -412,7 +456,9 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
     for (int t = 0; t < 4; ++t) gh = mfma16(wv.q1t[o][t], gb[o][t], gh);
   }
   *reinterpret_cast<f32x4*>(&sh.gpart[buf][p][lane][0]) = f32x4{gh[0], gh[1], gh[2], gh[3]};
+  OT_MARK(13);
   __syncthreads();
+  OT_MARK(14);
 #pragma unroll
   for (int i = 0; i < C; ++i) {
     const int ln = 16 * (i >> 2) + j, rg = i & 3;
@@ -420,8 +466,10 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
                       sh.gpart[buf][3][ln][rg];
     gy_out[i] = ghm + ghb[i];
   }
+  OT_MARK(15);
 }
 
+template <bool SN>
 __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   OtBwdShared& sh = *reinterpret_cast<OtBwdShared*>(smem);
@@ -452,12 +500,16 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
   const float third = 1.0f / 3.0f;
   int buf = 0;
   VjpIn cur, nxt;
+  VjpRow crw, nrw;
   load_vjp_in(a, p, a.E - 1, b, valid, q, cur);
-  // evals are visited E-1, E-2, ..., 0: each VJP first issues the loads of the next one
+  vjp_row_math<SN>(a, cur, crw);
+  // evals are visited E-1, E-2, ..., 0: each VJP first issues the loads of the next one and
+  // computes its row math between its own MFMA chains
 #define OT_VJP(E_, G_)                                                                  \
   load_vjp_in(a, p, (E_) - 1, b, valid, q, nxt);                                        \
-  ot_vjp(a, wv, q3t, sh, buf, p, (E_), b, valid, lane, q, j, cur, G_, gY);               \
+  ot_vjp<SN>(a, wv, q3t, sh, buf, p, (E_), b, valid, lane, q, j, cur, crw, nxt, nrw, G_, gY); \
   cur = nxt;                                                                            \
+  crw = nrw;                                                                            \
   buf ^= 1;
   for (int it = a.niters - 2; it >= 0; --it) {
     float ta, dt;
@@ -652,7 +704,8 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t lds = sizeof(OtBwdShared);     // weight operands in registers (VjpW)
-  hipLaunchKernelGGL(k_ot_bwd, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
+  if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(k_ot_bwd<false>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const OtLayout L = ot_layout(a.B, a.E);
   fiode_internal::WgradIO io{};
