@@ -195,6 +195,7 @@ class LyapunovLearning(nn.Module):
         self.train_ode_solver, self.train_ode_tol = train_ode_solver, train_ode_tol
         self.val_ode_solver, self.val_ode_tol = val_ode_solver, val_ode_tol
         self.opt_name, self.lr, self.momentum, self.weight_decay = opt_name, lr, momentum, weight_decay
+        self.fix_backbone = fix_backbone
         self.decay_epochs, self.betas = list(decay_epochs), (beta1, beta2)
         self.scheduler_name, self.max_epochs, self.warmup = scheduler_name, max_epochs, warmup
         self.simplex, self.act, self.eps, self.norm = simplex, act, eps, norm
@@ -280,7 +281,9 @@ class LyapunovLearning(nn.Module):
         elif self.opt_name == "AdamW":
             opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
         elif self.opt_name == "SGD":
-            opt = torch.optim.SGD(params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
+            # fix_backbone: SGD over the dynamics' parameters only (pl_modules.py:110-114)
+            sgd_params = list(self.model.dyn_fun.parameters()) if self.fix_backbone else params
+            opt = torch.optim.SGD(sgd_params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
         else:
             raise RuntimeError(f"[ERROR] Invalid Optimizer Param: {self.opt_name}")
         if self.scheduler_name == "cos_anneal":

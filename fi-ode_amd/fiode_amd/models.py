@@ -3,8 +3,10 @@
 ``Normalize`` + ``make_ortho_KWLarge_Concat`` mirror models.py:17-35 of the reference.  The
 KWLarge_Concat body lives in the absent ``libs/ortho_conv`` submodule; it is restated here from
 the public KWLarge design (4 Cayley convs with GroupSort, 3 Cayley linears) with ``out_dim``
-outputs -- parity unpinned, and it stays PyTorch-ROCm host code (the
-backbone as HIP/MFMA is the next row after the fan-out path).
+outputs -- parity unpinned.  On ROCm tensors its per-layer work runs in libfiode.so (SURVEY.md
+section 8f row f1: spectral Cayley maps, the conv transforms + GroupSort, the dense Cayley stages
+and block inverses; cayley.py); the complex / dense GEMMs stay on hipBLASLt, and host tensors
+take the PyTorch formula.
 """
 from __future__ import annotations
 

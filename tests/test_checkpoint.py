@@ -104,3 +104,20 @@ def test_classmethod_load(tmp_path):
               lya_cand=b.lya_cand, t_max=1.0, simplex=True)
     c = cls.load_from_checkpoint(path, strict=True, **kw)
     assert torch.equal(c.dyn_fun.U_x.alpha, a.dyn_fun.U_x.alpha)
+
+
+def test_sgd_fix_backbone_optimizes_dynamics_only():
+    """pl_modules.py:110-118: with opt_name='SGD', fix_backbone=True optimizes the dynamics'
+    parameters only; False optimizes every parameter."""
+    m = _mod(0)
+    m.opt_name, m.momentum = "SGD", 0.9
+    dyn_ids = {id(p) for p in m.dyn_fun.parameters()}
+    m.fix_backbone = True
+    opt = m.configure_optimizers()[0]
+    opt = opt[0] if isinstance(opt, list) else opt
+    got = {id(p) for g in opt.param_groups for p in g["params"]}
+    assert got == dyn_ids
+    m.fix_backbone = False
+    opt = m.configure_optimizers()[0]
+    opt = opt[0] if isinstance(opt, list) else opt
+    assert {id(p) for g in opt.param_groups for p in g["params"]} == {id(p) for p in m.parameters()}
