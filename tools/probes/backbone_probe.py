@@ -1,6 +1,6 @@
 """Timing probe: where does the backbone's time go (not a test)."""
 import sys, time, pathlib, json
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch
 dev = torch.device("cuda:0")

@@ -2,13 +2,13 @@
 Times the 4096->512 and 512->512 Cayley maps (each a ~200 us latency chain) captured alone, and
 both captured on two side streams of one graph; concurrent branches give ~max, serial ones ~sum.
 
-python tools/branch_probe.py  ->  one JSON line of us per replay
+python tools/probes/branch_probe.py  ->  one JSON line of us per replay
 """
 import json
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

@@ -2,14 +2,14 @@
 time with parts of the work frozen (their outputs precomputed, their backward dropped).  The
 differences against the full step bound each part's exposed (non-overlapped) time.
 
-python tools/critical_probe.py  ->  one JSON line of ms per step per variant
+python tools/probes/critical_probe.py  ->  one JSON line of ms per step per variant
 """
 import json
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

@@ -1,5 +1,5 @@
 # Step time under HIP graph-executor queue settings, alternated A B A B ... (not a test).
-# usage (via gpurun): bash tools/env_probe.sh
+# usage (via gpurun): bash tools/probes/env_probe.sh
 set -u
 mkdir -p gpurun_out/env
 for round in 1 2 3; do

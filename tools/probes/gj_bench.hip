@@ -1,7 +1,7 @@
 // Micro-benchmark: register Gauss-Jordan variants (old k_inv_gj of cayley.hip vs fiode_gj::GJ)
 // on positive-real test matrices; prints us per launch and the max |difference| (not a test).
-#include "../fi-ode_amd/csrc/cayley.hip"  // (k_inv_gj is now the gj.h kernel: old == new)
-#include "../fi-ode_amd/csrc/gj.h"
+#include "../../fi-ode_amd/csrc/cayley.hip"  // (k_inv_gj is now the gj.h kernel: old == new)
+#include "../../fi-ode_amd/csrc/gj.h"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>

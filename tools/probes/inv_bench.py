@@ -1,6 +1,6 @@
 """Micro-benchmark of fiode_batched_inverse (not a test)."""
 import sys, pathlib, time
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch
 from fiode_amd import ops

@@ -1,6 +1,6 @@
 """Per-layer fwd / fwd+bwd GPU time of the backbone + dynamics Cayley maps (not a test)."""
 import sys, pathlib
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch
 import bench

@@ -1,12 +1,12 @@
 """Latency of the backbone CayleyLinear maps, part by part, as hipGraph replays (not a test).
 
-python tools/lin_map_probe.py  ->  one JSON line of us per replay
+python tools/probes/lin_map_probe.py  ->  one JSON line of us per replay
 """
 import json
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

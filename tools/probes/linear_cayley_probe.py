@@ -3,7 +3,7 @@
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

@@ -5,7 +5,7 @@ import os
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 os.environ["FIODE_LIB"] = str(ROOT / "tools" / "libfiode_prof.so")
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import ctypes as ct  # noqa: E402

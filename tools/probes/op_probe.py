@@ -1,6 +1,6 @@
 """Device kernels by aten op for one backbone fwd+bwd (not a test)."""
 import sys, pathlib
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch
 from torch.profiler import profile, ProfilerActivity

@@ -3,14 +3,14 @@ inserted in front of one part of the step (on whatever stream that part runs), a
 the hipGraph step time tells whether that part is on the critical path (growth ~ 200 us) or has
 slack (growth ~ 0).
 
-python tools/slack_probe.py  ->  one JSON line: ms per step per variant
+python tools/probes/slack_probe.py  ->  one JSON line: ms per step per variant
 """
 import json
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

@@ -1,14 +1,14 @@
 """GPU-time decomposition of the configs[1] training step by hipGraph replays of its parts (not a
 test): each part is captured alone and replayed, so the numbers carry no host dispatch cost.
 
-python tools/step_probe.py  ->  one JSON line of per-part ms
+python tools/probes/step_probe.py  ->  one JSON line of per-part ms
 """
 import json
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 

@@ -3,14 +3,14 @@
 queues (GPU_MAX_HW_QUEUES = 4 on the pool's boxes), so independent branches can be serialized;
 each variant assigns the 11 maps (4 conv, 3 linear, dynamics) to side streams differently.
 
-python tools/stream_probe.py  ->  one JSON line of ms per step per variant
+python tools/probes/stream_probe.py  ->  one JSON line of ms per step per variant
 """
 import json
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import torch  # noqa: E402
 
