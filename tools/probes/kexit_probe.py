@@ -1,0 +1,79 @@
+"""How predictable is the train_ode solve's batch-global QP exit?  (not a test)
+
+Runs k_ot_fwd on the bench's configs[1] state (B=128, random-init KWLarge backbone features) for
+several Philox offsets and reads back the exit-exchange granules ({epoch, mask} per eval, phase and
+tile) the forward leaves in its workspace.  Per eval: the global exit K = lowest set bit of the AND
+of the tiles' masks; per tile: its local first converged iteration.  Prints how often a tile's own
+first converged iteration equals K, and the distribution of K - K_prev.
+"""
+import collections
+import ctypes as ct
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fiode_amd import _lib as L, ops  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    mod = bench.build_module(dev, seed=0, train_ode=True)
+    g = torch.Generator().manual_seed(1234)
+    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
+    with torch.no_grad():
+        feat = mod.init_coordinates.param_map(x).float().contiguous()
+        w = {k: v.detach().float().contiguous() for k, v in mod.dyn_fun.effective_weights().items()}
+    B = 128
+    h0 = torch.full((B, 10), 0.1, device=dev)
+    dyn = mod.dyn_fun.dyn_cfg()
+    lib = L.lib()
+    hits = tot = 0
+    dk = collections.Counter()
+    kc = collections.Counter()
+    resumes = 0
+    for off in range(8):
+        cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=7, offset=off)
+        y, st, ws = ops.odetrain_forward(feat, h0, w, dyn, cfg)
+        torch.cuda.synchronize()
+        E = ops.odetrain_evals(cfg)
+        nt = (B + 15) // 16
+        offs = (ct.c_int64 * 9)()
+        lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
+        xs = offs[7] + ((B * E * 10 * 4 + 255) & ~255)
+        slots = ws[xs: xs + E * 2 * nt * 8].view(torch.int64).cpu().numpy().astype(np.uint64).reshape(E, 2, nt)
+        kprev = dyn.qp_max_iter - 1
+        for e in range(E):
+            m0 = (slots[e, 0] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            kspec = min(dyn.qp_max_iter - 1, kprev + 3)
+            allm = np.bitwise_and.reduce(m0)
+            lowm = (1 << (kspec + 1)) - 1
+            bits = int(allm) & lowm
+            if bits:
+                K = (bits & -bits).bit_length() - 1
+            else:
+                resumes += 1
+                m1 = (slots[e, 1] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+                a1 = int(np.bitwise_and.reduce(m1))
+                K = (a1 & -a1).bit_length() - 1 if a1 else dyn.qp_max_iter - 1
+                m0 = m1
+            for t in range(nt):
+                loc = int(m0[t])
+                f = (loc & -loc).bit_length() - 1 if loc else -1
+                hits += f == K
+                tot += 1
+            dk[K - kprev] += 1
+            kc[K] += 1
+            kprev = K
+        print(f"offset {off}: y finite {bool(torch.isfinite(y).all())}, last K {int(st[2])}", flush=True)
+    print(f"tile-local first converged == global K: {hits}/{tot} = {hits / tot:.3f}")
+    print(f"resumes {resumes}; K distribution {sorted(kc.items())}")
+    print(f"K - K_prev distribution {sorted(dk.items())}")
+
+
+if __name__ == "__main__":
+    main()
