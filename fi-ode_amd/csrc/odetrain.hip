@@ -100,9 +100,13 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 // ntiles granules of that eval until every tag matches (relaxed agent-scope loads; the granule
 // IS the flag, so no fence is needed).  The spin is bounded: on timeout the status word records
 // it and the solve completes.
+#ifndef OT_SHARE_L1
+#define OT_SHARE_L1 1         // layer 1 split over the 4 waves (LDS exchange) instead of replicated
+#endif
 struct OtShared {
   float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
   float mu_rec[4][TR][33];    // [wave][row][bisection iteration] (padded)
+  float z1x[8][64][4];        // layer-1 blocks, one pair per wave (mlp16_part)
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
   int dead;                   // an exit exchange timed out (status 4): stop waiting, poison y_out
@@ -137,9 +141,9 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
     asm volatile("" ::"v"(lower[i]));          // keep it here (IR passes would sink it to its use)
   }
   mlp16_part(w, uacc, h, kw1, kw2p, a.drop_scale, p, q, valid ? a.a1 + r * M : nullptr,
-             valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0]);
+             valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0], OT_SHARE_L1 ? sh.z1x : nullptr);
 #pragma unroll
-  for (int i = 0; i < 96; ++i) {
+  for (int i = 0; i < (OT_SHARE_L1 ? 78 : 96); ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // one MFMA
     __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);     // then up to three VALU
   }

@@ -20,6 +20,13 @@ using namespace fiode_tile;
 // accumulation runs >= 2 independent accumulators except the short layer-3 chain.
 constexpr int TR = 16;
 
+// The batch-global QP exit is first exchanged for iterations <= previous exit + this margin; if
+// no such iteration converged everywhere the bisection resumes to max_iter - 1 and exchanges
+// again (same exit either way: the lowest iteration at which every row converged).
+#ifndef FIODE_KSPEC_MARGIN
+#define FIODE_KSPEC_MARGIN 1
+#endif
+
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -207,28 +214,66 @@ __device__ __forceinline__ void load_t16w(const float* Q1, const float* Q2, int 
   for (int t = 0; t < 4; ++t) w.b3[t] = (p == 0 && 4 * q + t < C) ? b3[4 * q + t] : 0.f;
 }
 
+// Layer-1 blocks 2P, 2P+1 of one tile (part P), relu(dropout), saved row, and their LDS copy.
+template <int P>
+__device__ __forceinline__ void l1_pair(const T16W& w, const f32x4v (&uacc)[8], const float (&h)[C],
+                                        const uint32_t (&kw1)[4], float scale, int q, int lane, float* a1row,
+                                        float (*z1x)[64][4]) {
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    constexpr int hb0 = 2 * P;
+    const int hb = hb0 + o;
+    f32x4v z = uacc[hb0 + o];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) z = mfma16(w.q1[hb0 + o][s], sel4(h, s, q), z);
+    dropout_relu16(z, kw1[P], hb, q, scale);
+    if (a1row) *reinterpret_cast<f32x4*>(a1row + 16 * hb + 4 * q) = f32x4{z[0], z[1], z[2], z[3]};
+    *reinterpret_cast<f32x4*>(&z1x[hb][lane][0]) = f32x4{z[0], z[1], z[2], z[3]};
+  }
+}
+
 // The MLP of one tile for hidden part p (of 4): layer 1 in full (24 MFMA), layer-2 output blocks
 // 2p, 2p+1 (64 MFMA), their layer-3 partial (8 MFMA; bias on part 0) -> zpart_lane[4] (LDS).
 // a1row / a2row (nullable): the row's saved post-activations (part p stores its blocks).
+// z1x (nullable, LDS [8][64][4], all 4 waves call with the same choice): layer 1 split over the
+// waves -- wave p computes blocks 2p, 2p+1 (6 MFMA instead of 24), they meet in LDS behind one
+// workgroup barrier and every wave reads the 8 blocks back; bit-identical to the replicated layer 1.
 __device__ __forceinline__ void mlp16_part(const T16W& w, const f32x4v (&uacc)[8], const float (&h)[C],
                                            const uint32_t (&kw1)[4], uint32_t kw2p, float scale, int p, int q,
-                                           float* a1row, float* a2row, float* zpart_lane) {
+                                           float* a1row, float* a2row, float* zpart_lane,
+                                           float (*z1x)[64][4] = nullptr) {
   f32x4v z1[8];
+  if (z1x) {
+    const int lane = threadIdx.x & 63;
+    switch (p) {              // wave-uniform: static register indices in each case
+      case 0: l1_pair<0>(w, uacc, h, kw1, scale, q, lane, a1row, z1x); break;
+      case 1: l1_pair<1>(w, uacc, h, kw1, scale, q, lane, a1row, z1x); break;
+      case 2: l1_pair<2>(w, uacc, h, kw1, scale, q, lane, a1row, z1x); break;
+      default: l1_pair<3>(w, uacc, h, kw1, scale, q, lane, a1row, z1x); break;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int hb = 0; hb < 8; ++hb) z1[hb] = uacc[hb];
+    for (int hb = 0; hb < 8; ++hb) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(&z1x[hb][lane][0]);
+      z1[hb] = f32x4v{v[0], v[1], v[2], v[3]};
+    }
+  } else {
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const float bs = sel4(h, s, q);
+    for (int hb = 0; hb < 8; ++hb) z1[hb] = uacc[hb];
 #pragma unroll
-    for (int hb = 0; hb < 8; ++hb) z1[hb] = mfma16(w.q1[hb][s], bs, z1[hb]);
-  }
+    for (int s = 0; s < 3; ++s) {
+      const float bs = sel4(h, s, q);
 #pragma unroll
-  for (int hb = 0; hb < 8; ++hb) dropout_relu16(z1[hb], kw1[hb >> 1], hb, q, scale);
-  if (a1row) {
+      for (int hb = 0; hb < 8; ++hb) z1[hb] = mfma16(w.q1[hb][s], bs, z1[hb]);
+    }
 #pragma unroll
-    for (int hb = 0; hb < 8; ++hb)
-      if ((hb >> 1) == p)
-        *reinterpret_cast<f32x4*>(a1row + 16 * hb + 4 * q) = f32x4{z1[hb][0], z1[hb][1], z1[hb][2], z1[hb][3]};
+    for (int hb = 0; hb < 8; ++hb) dropout_relu16(z1[hb], kw1[hb >> 1], hb, q, scale);
+    if (a1row) {
+#pragma unroll
+      for (int hb = 0; hb < 8; ++hb)
+        if ((hb >> 1) == p)
+          *reinterpret_cast<f32x4*>(a1row + 16 * hb + 4 * q) = f32x4{z1[hb][0], z1[hb][1], z1[hb][2], z1[hb][3]};
+    }
   }
   f32x4v z2[2];
 #pragma unroll
@@ -271,7 +316,7 @@ __device__ __forceinline__ void ft16_sum(const float (*zpart)[64][4], int j, flo
   }
 }
 
-// The batch-global QP exit of one eval with speculation: bisect to kprev + 3, publish the wave's
+// The batch-global QP exit of one eval with speculation: bisect to kprev + FIODE_KSPEC_MARGIN, publish the wave's
 // mask in granule slot slots[blockIdx] (epoch), gather all tiles; only if no iteration <= kspec
 // converged everywhere, resume to max_iter - 1 and exchange again in slots[ntiles + ..].  Called
 // by all 4 waves (identical rows); wave 0 exchanges; shK is an LDS int.  Returns K (uniform).
@@ -281,7 +326,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
                                          int& dead, int drop_block = -1,
                                          unsigned long long* prof = nullptr) {
   const int last = max_iter - 1;
-  const int kspec = min(last, kprev + 3);
+  const int kspec = min(last, kprev + FIODE_KSPEC_MARGIN);
   float lo, hi;
   const bool pr = prof && blockIdx.x == 0 && threadIdx.x == 0;      // phase timing (diagnostic builds)
   const uint64_t t0 = prof ? wall_clock64() : 0;

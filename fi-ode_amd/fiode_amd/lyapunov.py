@@ -47,7 +47,9 @@ class LyapunovLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go):
         g = ctx.saved_tensors
-        return tuple(t * go for t in g) + (None, None)
+        # the upstream scale on all nine gradients in one multi-tensor launch (was nine multiplies
+        # between the solve's forward and backward on the step stream); same float32 products
+        return tuple(torch._foreach_mul(list(g), go)) + (None, None)
 
 
 class ODETrainFn(torch.autograd.Function):
@@ -367,9 +369,16 @@ class LyapunovLearning(nn.Module):
         for m in self.init_coordinates.modules():
             if hasattr(m, "prefetch") and m is not self.dyn_fun:
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
+        # conv_streams "split": each conv map on a stream of its own (else one chain on s[0])
+        if sched.get("conv_streams") == "split":
+            if getattr(self, "_conv_streams", None) is None:
+                self._conv_streams = [s[0]] + [torch.cuda.Stream(device) for _ in range(len(convs) - 1)]
+            cst = self._conv_streams
+        else:
+            cst = [s[0]] * len(convs)
         if sched.get("order", "conv_first") == "conv_first":
-            for c in convs:
-                c.prefetch(s[0])
+            for c, st in zip(convs, cst):
+                c.prefetch(st)
         klin = list(sched.get("lin", [-1] * len(lins))) + [-1] * len(lins)
         jobs = []
         if getattr(self, "group_lin_maps", False) and not sched.get("lin"):
@@ -385,15 +394,21 @@ class LyapunovLearning(nn.Module):
                 jobs.append((-1, (lambda big=big: group_prefetch(big, s[1]))))
                 lins = [l for l in lins if l not in big]
                 klin = [-1] * len(lins)
-        jobs += [(klin[i], (lambda l=l, st=s[2 + min(i, 1)]: l.prefetch(st))) if jobs else
-                 (klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
-        jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[3])))
+        if sched.get("lin_streams") == "one":
+            # every linear map and the dynamics maps as one chain on s[1] (fewer parallel branches
+            # for the graph executor to map onto its queues)
+            jobs += [(klin[i], (lambda l=l: l.prefetch(s[1]))) for i, l in enumerate(lins)]
+            jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[1])))
+        else:
+            jobs += [(klin[i], (lambda l=l, st=s[2 + min(i, 1)]: l.prefetch(st))) if jobs else
+                     (klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
+            jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[3])))
         for k, fn in jobs:
             if k < 0:
                 fn()
         if sched.get("order", "conv_first") != "conv_first":
-            for c in convs:
-                c.prefetch(s[0])
+            for c, st in zip(convs, cst):
+                c.prefetch(st)
         later = [(k, fn) for k, fn in jobs if k >= 0]
         bb = self.init_coordinates.param_map
         target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb

@@ -125,7 +125,28 @@ def ode_on_main(m):
     m.ode_side_stream = False
 
 
-ALL = {"default": reset2, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
+def conv_first_split(m):
+    m.prefetch_schedule = {"after_input": True, "order": "conv_first", "conv_streams": "split"}
+
+
+def lin_first_split(m):
+    m.prefetch_schedule = {"after_input": True, "order": "lin_first", "conv_streams": "split"}
+
+
+def conv_first(m):
+    m.prefetch_schedule = {"after_input": True, "order": "conv_first"}
+
+
+def lin_one(m):
+    m.prefetch_schedule = {"after_input": True, "order": "lin_first", "lin_streams": "one"}
+
+
+def lin_one_conv_first(m):
+    m.prefetch_schedule = {"after_input": True, "order": "conv_first", "lin_streams": "one"}
+
+
+ALL = {"default": reset2, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+       "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "small_bwd_main", "ode_on_main"]

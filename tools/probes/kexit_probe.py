@@ -33,6 +33,11 @@ def main():
     dyn = mod.dyn_fun.dyn_cfg()
     lib = L.lib()
     hits = tot = 0
+    pred = collections.Counter()      # predictor -> correct guesses
+
+    def lowest_ge(mask, k):
+        m = mask & ~((1 << max(k, 0)) - 1)
+        return (m & -m).bit_length() - 1 if m else -1
     dk = collections.Counter()
     kc = collections.Counter()
     resumes = 0
@@ -66,11 +71,16 @@ def main():
                 f = (loc & -loc).bit_length() - 1 if loc else -1
                 hits += f == K
                 tot += 1
+                for name, k in (("local_first", 0), ("ge_kprev-1", kprev - 1), ("ge_kprev", kprev),
+                                ("ge_kprev+1", kprev + 1)):
+                    pred[name] += lowest_ge(loc, k) == K
+                pred["ge_max(f,kprev)"] += lowest_ge(loc, max(f, kprev)) == K
             dk[K - kprev] += 1
             kc[K] += 1
             kprev = K
         print(f"offset {off}: y finite {bool(torch.isfinite(y).all())}, last K {int(st[2])}", flush=True)
     print(f"tile-local first converged == global K: {hits}/{tot} = {hits / tot:.3f}")
+    print("predictor accuracy:", {k: round(v / tot, 3) for k, v in pred.items()})
     print(f"resumes {resumes}; K distribution {sorted(kc.items())}")
     print(f"K - K_prev distribution {sorted(dk.items())}")
 
