@@ -314,13 +314,14 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
 // state stays replicated.
 struct OtBwdShared {
   float gpart[2][4][64][4];
+  float gax[8][64][4];        // g_z2 blocks, one pair per wave (each wave computes its own two)
 };
 
 // The saved forward values one VJP reads (independent of the adjoint): loaded one VJP ahead, so
 // their global-memory latency overlaps the previous VJP's dependent chain.
 struct VjpIn {
   float h[C], ft[C], v[C], mu;
-  f32x4 a2[8];        // saved post-activations of layer 2, this lane's 4 hidden of each block
+  f32x4 a2[2];        // saved post-activations of layer 2, hidden blocks 2p, 2p+1 (this lane's 4 of each)
   f32x4 a1[2];        // layer 1, hidden blocks 2p, 2p+1
 };
 
@@ -332,7 +333,7 @@ __device__ __forceinline__ void load_vjp_in(const OTArgs& a, int p, int e, int b
   load_row10(a.vw + r * C, in.v);
   in.mu = a.muw[r];
 #pragma unroll
-  for (int hb = 0; hb < 8; ++hb) in.a2[hb] = *reinterpret_cast<const f32x4*>(a.a2 + r * M + 16 * hb + 4 * q);
+  for (int o = 0; o < 2; ++o) in.a2[o] = *reinterpret_cast<const f32x4*>(a.a2 + r * M + 16 * (2 * p + o) + 4 * q);
 #pragma unroll
   for (int o = 0; o < 2; ++o) in.a1[o] = *reinterpret_cast<const f32x4*>(a.a1 + r * M + 16 * (2 * p + o) + 4 * q);
 }
@@ -367,6 +368,25 @@ __device__ __forceinline__ void vjp_row_math(const OTArgs& a, const VjpIn& in, V
       rw.sig[i] = 0.f;
       rw.nominal[i] = in.ft[i];
     }
+  }
+}
+
+// g_z2 blocks 2P, 2P+1 of one VJP: Q3^T g_ft, masked by the saved a2 and the dropout scale;
+// stored to gz2 (nullable row) and to the LDS exchange.
+template <int P>
+__device__ __forceinline__ void gz2_pair(const OTArgs& a, const float (&q3t)[8][3], const float (&gft)[C],
+                                         const VjpIn& in, int q, int lane, float* gz2row, float (*gax)[64][4]) {
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    constexpr int hb0 = 2 * P;
+    f32x4v g = z4();
+#pragma unroll
+    for (int s = 0; s < 3; ++s) g = mfma16(q3t[hb0 + o][s], sel4(gft, s, q), g);
+    const f32x4 act = in.a2[o];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) g[t] = act[t] > 0.f ? g[t] * a.drop_scale : 0.f;
+    if (gz2row) *reinterpret_cast<f32x4*>(gz2row + 16 * (hb0 + o) + 4 * q) = f32x4{g[0], g[1], g[2], g[3]};
+    *reinterpret_cast<f32x4*>(&gax[hb0 + o][lane][0]) = f32x4{g[0], g[1], g[2], g[3]};
   }
 }
 
@@ -405,23 +425,23 @@ __device__ void ot_vjp(const OTArgs& a, const VjpW& wv, const float (&q3t)[8][3]
     if (a.dbg_gft) store_row10(a.dbg_gft + r * C, gft);
   }
   OT_MARK(10);
-  // g_a2^T = Q3^T g_ft^T (all 128 hidden, 8 blocks, K = 10 in 3 k-steps), masked by the saved a2
+  // g_z2^T = (Q3^T g_ft^T) masked by the saved a2 (K = 10 in 3 k-steps): wave p computes hidden
+  // blocks 2p, 2p+1 (6 MFMA), the 8 blocks meet in LDS behind one barrier (same values as every
+  // wave computing all 8)
+  {
+    switch (p) {              // wave-uniform: static register indices in each case
+      case 0: gz2_pair<0>(a, q3t, gft, in, q, lane, valid ? a.gz2 + r * M : nullptr, sh.gax); break;
+      case 1: gz2_pair<1>(a, q3t, gft, in, q, lane, valid ? a.gz2 + r * M : nullptr, sh.gax); break;
+      case 2: gz2_pair<2>(a, q3t, gft, in, q, lane, valid ? a.gz2 + r * M : nullptr, sh.gax); break;
+      default: gz2_pair<3>(a, q3t, gft, in, q, lane, valid ? a.gz2 + r * M : nullptr, sh.gax); break;
+    }
+  }
+  __syncthreads();
   f32x4v ga[8];
 #pragma unroll
-  for (int hb = 0; hb < 8; ++hb) ga[hb] = z4();
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const float bs = sel4(gft, s, q);
-#pragma unroll
-    for (int hb = 0; hb < 8; ++hb) ga[hb] = mfma16(q3t[hb][s], bs, ga[hb]);
-  }
-#pragma unroll
   for (int hb = 0; hb < 8; ++hb) {
-    const f32x4 act = in.a2[hb];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) ga[hb][t] = act[t] > 0.f ? ga[hb][t] * a.drop_scale : 0.f;
-    if (valid && (hb >> 1) == p)
-      *reinterpret_cast<f32x4*>(a.gz2 + r * M + 16 * hb + 4 * q) = f32x4{ga[hb][0], ga[hb][1], ga[hb][2], ga[hb][3]};
+    const f32x4 v = *reinterpret_cast<const f32x4*>(&sh.gax[hb][lane][0]);
+    ga[hb] = f32x4v{v[0], v[1], v[2], v[3]};
   }
   OT_MARK(11);
   // hidden blocks 2p, 2p+1 of g_a1^T = Q2^T g_z2^T (two independent accumulators), with the next

@@ -30,5 +30,8 @@ for B, sn in ((128, False), (300, True), (37, False)):
     y, st, ws = ops.odetrain_forward(x, h0, w, ops.DynCfg(scale_nominal=sn), cfg)
     sv = ops.odetrain_saved(ws, cfg)
     out.update({f"y{B}": y.cpu(), f"mu{B}": sv["mu"].cpu(), f"v{B}": sv["v"].cpu(), f"stats{B}": st.cpu()})
+    gy = torch.from_numpy(rng.normal(size=(B, 10)).astype(np.float32)).to(dev)
+    grads, _ = ops.odetrain_backward(gy, x, w, ops.DynCfg(scale_nominal=sn), cfg, ws)
+    out.update({f"g{k}{B}": v.cpu() for k, v in grads.items()})
 torch.save(out, sys.argv[1])
 print("saved", sys.argv[1])
