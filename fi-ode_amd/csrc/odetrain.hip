@@ -105,7 +105,7 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 #endif
 struct OtShared {
   float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
-  float mu_rec[4][TR][33];    // [wave][row][bisection iteration] (padded)
+  float mu_rec[4][64][33];    // [wave][lane][bisection iteration] (padded): every lane its own
   float z1x[8][64][4];        // layer-1 blocks, one pair per wave (mlp16_part)
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
@@ -140,8 +140,8 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
     lower[i] = -a.d.alpha_1 * (expf(a.d.sigma_1 * h[i]) - 1.0f);
     asm volatile("" ::"v"(lower[i]));          // keep it here (IR passes would sink it to its use)
   }
-  mlp16_part(w, uacc, h, kw1, kw2p, a.drop_scale, p, q, valid ? a.a1 + r * M : nullptr,
-             valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0], OT_SHARE_L1 ? sh.z1x : nullptr);
+  mlp16_part<OT_SHARE_L1 != 0>(w, uacc, h, kw1, kw2p, a.drop_scale, p, q, valid ? a.a1 + r * M : nullptr,
+                               valid ? a.a2 + r * M : nullptr, &sh.zpart[p][lane][0], sh.z1x);
 #pragma unroll
   for (int i = 0; i < (OT_SHARE_L1 ? 78 : 96); ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // one MFMA
@@ -165,7 +165,7 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
     }
   }
   OT_MARK(5);
-  float* rec = &sh.mu_rec[p][j][0];
+  float* rec = &sh.mu_rec[p][lane][0];
   qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
             a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
             a.drop_block,
@@ -177,7 +177,7 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
   );
   OT_MARK(3);
   const int K = sh.K;
-  const float mu = sh.mu_rec[p][j][K];
+  const float mu = sh.mu_rec[p][lane][K];
 #pragma unroll
   for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);
   if (p == 0 && valid && q == 0) {

@@ -161,14 +161,19 @@ __device__ __forceinline__ float qp_eps(const float (&lower)[C], const float (&n
 // iteration.  Measured on gfx950 (tools/probes/bisect_probe.hip, cycles per 20 iterations of a
 // 4-wave workgroup): this 4.2k, the 2-per-round permlane variant 5.4k, the 4-level workgroup tree
 // 6.0k -- at one wave per SIMD the exchange and path selection of a speculative variant cost more
-// than the eps evaluations they save.  Convergence: per-lane open bits, OR-reduced once per call.
+// than the eps evaluations they save.  Per iteration the dependent chain is mu, 5 packed
+// subtracts, 10 max, the 9 ordered adds and the bracket update; everything else is kept off it:
+// mu = fma(hi - lo, 0.5, lo) is (hi - lo) / 2 + lo exactly (the halving is exact for any width
+// above 2^-125), the per-lane open bits are OR-reduced over the wave once per call (a ballot per
+// iteration measured slower: its scalar test waits on the compare), and mu_rec (nullable) is
+// written by every lane (rec: the caller's per-lane slot) with no exec-mask branch.
 __device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const float (&nom)[C], int from, int to,
                                                   float tol, float& lo, float& hi, float* mu_rec, bool rec,
                                                   bool valid) {
   if (from > to) return 0u;
   uint32_t open = 0;
   for (int it = from; it <= to; ++it) {
-    const float mu = (hi - lo) / 2.0f + lo;
+    const float mu = __fmaf_rn(hi - lo, 0.5f, lo);
     const float eps = qp_eps(lower, nom, mu);
     if (rec) mu_rec[it] = mu;
     open |= ((valid && !(fabsf(eps) < tol)) ? 1u : 0u) << it;
@@ -179,7 +184,6 @@ __device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const
   const uint32_t span = (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << from;
   return ~wave_or16(open) & span;
 }
-
 
 
 // The weights one wave (hidden part p) reads in the MLP of a tile, held in registers for the whole
@@ -235,15 +239,16 @@ __device__ __forceinline__ void l1_pair(const T16W& w, const f32x4v (&uacc)[8], 
 // The MLP of one tile for hidden part p (of 4): layer 1 in full (24 MFMA), layer-2 output blocks
 // 2p, 2p+1 (64 MFMA), their layer-3 partial (8 MFMA; bias on part 0) -> zpart_lane[4] (LDS).
 // a1row / a2row (nullable): the row's saved post-activations (part p stores its blocks).
-// z1x (nullable, LDS [8][64][4], all 4 waves call with the same choice): layer 1 split over the
+// kShareL1 (z1x: LDS [8][64][4], all 4 waves call with the same choice): layer 1 split over the
 // waves -- wave p computes blocks 2p, 2p+1 (6 MFMA instead of 24), they meet in LDS behind one
 // workgroup barrier and every wave reads the 8 blocks back; bit-identical to the replicated layer 1.
+template <bool kShareL1 = false>
 __device__ __forceinline__ void mlp16_part(const T16W& w, const f32x4v (&uacc)[8], const float (&h)[C],
                                            const uint32_t (&kw1)[4], uint32_t kw2p, float scale, int p, int q,
                                            float* a1row, float* a2row, float* zpart_lane,
                                            float (*z1x)[64][4] = nullptr) {
   f32x4v z1[8];
-  if (z1x) {
+  if constexpr (kShareL1) {
     const int lane = threadIdx.x & 63;
     switch (p) {              // wave-uniform: static register indices in each case
       case 0: l1_pair<0>(w, uacc, h, kw1, scale, q, lane, a1row, z1x); break;
@@ -331,7 +336,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   const bool pr = prof && blockIdx.x == 0 && threadIdx.x == 0;      // phase timing (diagnostic builds)
   const uint64_t t0 = prof ? wall_clock64() : 0;
   qp_bracket(lower, nominal, lo, hi);
-  uint32_t conv = qp_bisect_seq(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, q == 0, valid);
+  uint32_t conv = qp_bisect_seq(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, true, valid);
   const uint64_t t1 = prof ? wall_clock64() : 0;
   if (pr) atomicAdd(prof + 6, (unsigned long long)(t1 - t0));
   const int ntiles = gridDim.x;
@@ -350,7 +355,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
     if (shK < 0) atomicAdd(prof + 8, 1ull);
   }
   if (shK < 0) {                        // block-uniform: every tile saw the same masks
-    conv |= qp_bisect_seq(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, q == 0, valid);
+    conv |= qp_bisect_seq(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, true, valid);
     if (p == 0) {
       if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, epoch, conv);
       const uint32_t all = gather_masks(slots + ntiles, ntiles, epoch, status, lane, dead);
