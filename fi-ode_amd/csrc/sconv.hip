@@ -14,20 +14,23 @@
 //   k_sconv_irfft2   y = irfft2(Y) (torch's c2c-then-c2r order and 1/n^2 scaling), optional + bias
 //                    and GroupSort (pairs c, c + C/2; codes saved for the backward), or the
 //                    inverse space-to-channel scatter (the input gradient of a stride-2 conv).
-// n in {8, 16, 32}, so each transform is a direct DFT per axis (n^2 (n/2+1) x 2 complex MACs per
-// image, ~17 K at n = 32), one length-n DFT per thread with inputs and twiddles in registers, on
-// an LDS image of BT images of one channel: no butterflies, no bit reversal, coalesced BT-wide
-// loads and stores along B.
+// n in {8, 16, 32}: each 1-D transform is one in-register radix-2 FFT per thread (fft.h; ~0.6 K
+// VALU ops at n = 32 where the direct DFT of the first version took ~4 K FMAs), on an LDS image of
+// BT images of one channel, with coalesced BT-wide loads and stores along B.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "common.h"
+#include "fft.h"
 #include "fiode.h"
 
 namespace {
 
 typedef float2 c32;
-constexpr int NT = 1024;
+// threads per workgroup: 1024, or 512 for n = 32 (a length-32 FFT keeps 64 values + temporaries
+// live: 256 registers at 2 waves per SIMD instead of 128 at 4)
+template <int N>
+constexpr int nthreads() { return N == 32 ? 512 : 1024; }
 constexpr int BT_F = 16;     // images per forward-transform workgroup
 constexpr int BT_I = 8;      // images per inverse-transform workgroup
 
@@ -53,18 +56,6 @@ struct SArgs {
   uint8_t* code_out;             // [n][n][C/2][B]
 };
 
-// e^{sign 2 pi i m / N}, m < N, in registers (every index below is a compile-time constant once the
-// transform loops are unrolled, so the table never touches LDS)
-template <int N>
-__device__ __forceinline__ void twiddles(c32 (&t)[N], float sign) {
-#pragma unroll
-  for (int m = 0; m < N; ++m) {
-    float sn, cs;
-    sincospif(2.0f * (float)m / (float)N, &sn, &cs);
-    t[m] = make_float2(cs, sign * sn);
-  }
-}
-
 __device__ __forceinline__ int64_t act_index(const SArgs& a, int h, int w, int c, int b) {
   return (((int64_t)h * a.n + w) * a.C + c) * a.B + b;
 }
@@ -86,7 +77,8 @@ struct Geo {
 
 // ---- X[f][c][b0..b0+BT) = rfft2 of channel c ------------------------------------------------------
 template <int N, int BT>
-__global__ void __launch_bounds__(NT) k_sconv_rfft2(SArgs a) {
+__global__ void __launch_bounds__(nthreads<N>()) k_sconv_rfft2(SArgs a) {
+  constexpr int NT = nthreads<N>();
   typedef Geo<N> g;
   __shared__ float img[BT * g::IS];
   __shared__ c32 Z[BT * g::ZS];
@@ -125,53 +117,31 @@ __global__ void __launch_bounds__(NT) k_sconv_rfft2(SArgs a) {
     }
   }
   __syncthreads();
-  // The two 1-D transforms as one length-N DFT per thread in registers (rows, then columns): N^2
-  // complex MACs of pure VALU per transform with the inputs and twiddles in registers -- a
-  // tap-by-tap LDS loop here was LDS-latency bound at one wave per SIMD (~90 cycles per MAC).
-  c32 tw[N];
-  twiddles<N>(tw, -1.0f);
-  // r2c along w: one (image, h) row per thread; input-outer / output-inner loop order so the H
-  // accumulators form independent FMA chains (one wave per SIMD has no other latency hiding)
+  // The two 1-D transforms as one length-N FFT per thread in registers (rows, then columns;
+  // fft.h): a direct DFT here (N^2 complex MACs per transform) left the workgroups VALU-bound.
+  // r2c along w: one (image, h) row per thread (imaginary part 0, the N/2 + 1 kept outputs)
   for (int row = tid; row < BT * N; row += NT) {
     const int bt = row % BT, h = row / BT;
     const float* src = img + bt * g::IS + h * g::RS;
-    c32 acc[H];
+    c32 x[N];
 #pragma unroll
-    for (int kb = 0; kb < H; ++kb) acc[kb] = make_float2(0.f, 0.f);
+    for (int w = 0; w < N; ++w) x[w] = make_float2(src[w], 0.f);
+    fiode_fft::fft_reg<N, false>(x);
 #pragma unroll
-    for (int w = 0; w < N; ++w) {
-      const float v = src[w];
-#pragma unroll
-      for (int kb = 0; kb < H; ++kb) {
-        const c32 e = tw[(kb * w) % N];
-        acc[kb].x = fmaf(v, e.x, acc[kb].x);
-        acc[kb].y = fmaf(v, e.y, acc[kb].y);
-      }
-    }
-#pragma unroll
-    for (int kb = 0; kb < H; ++kb) Z[bt * g::ZS + h * H + kb] = acc[kb];
+    for (int kb = 0; kb < H; ++kb) Z[bt * g::ZS + h * H + kb] = x[kb];
   }
   __syncthreads();
   // c2c along h: one (image, kb) column per thread, written as X[f][c][b]
   for (int col = tid; col < BT * H; col += NT) {
     const int bt = col % BT, kb = col / BT;
-    c32 acc[N];
+    c32 x[N];
 #pragma unroll
-    for (int ka = 0; ka < N; ++ka) acc[ka] = make_float2(0.f, 0.f);
-#pragma unroll
-    for (int h = 0; h < N; ++h) {
-      const c32 v = Z[bt * g::ZS + h * H + kb];
-#pragma unroll
-      for (int ka = 0; ka < N; ++ka) {
-        const c32 e = tw[(ka * h) % N];
-        acc[ka].x = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[ka].x));
-        acc[ka].y = fmaf(v.x, e.y, fmaf(v.y, e.x, acc[ka].y));
-      }
-    }
+    for (int h = 0; h < N; ++h) x[h] = Z[bt * g::ZS + h * H + kb];
+    fiode_fft::fft_reg<N, false>(x);
     const int b = b0 + bt;
     if (b < a.B) {
 #pragma unroll
-      for (int ka = 0; ka < N; ++ka) a.X[((int64_t)(ka * H + kb) * a.C + c) * a.B + b] = acc[ka];
+      for (int ka = 0; ka < N; ++ka) a.X[((int64_t)(ka * H + kb) * a.C + c) * a.B + b] = x[ka];
     }
   }
 }
@@ -179,6 +149,7 @@ __global__ void __launch_bounds__(NT) k_sconv_rfft2(SArgs a) {
 // irfft2 of one channel of BT_I images into out (LDS, real image stride Geo<N>::IS)
 template <int N>
 __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c32* Ys, c32* Zs, float* out) {
+  constexpr int NT = nthreads<N>();
   typedef Geo<N> g;
   constexpr int H = g::H;
   const int tid = threadIdx.x;
@@ -190,49 +161,36 @@ __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c3
     Ys[bt * g::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
   }
   __syncthreads();
-  c32 tw[N];
-  twiddles<N>(tw, 1.0f);
-  // inverse c2c along ka: one (image, kb) column per thread (input-outer, independent accumulators)
+  // inverse c2c along ka: one (image, kb) column per thread (in-register FFT, fft.h)
   for (int col = tid; col < BT_I * H; col += NT) {
     const int bt = col % BT_I, kb = col / BT_I;
-    c32 acc[N];
+    c32 x[N];
 #pragma unroll
-    for (int h = 0; h < N; ++h) acc[h] = make_float2(0.f, 0.f);
+    for (int ka = 0; ka < N; ++ka) x[ka] = Ys[bt * g::ZS + ka * H + kb];
+    fiode_fft::fft_reg<N, true>(x);
 #pragma unroll
-    for (int ka = 0; ka < N; ++ka) {
-      const c32 v = Ys[bt * g::ZS + ka * H + kb];
-#pragma unroll
-      for (int h = 0; h < N; ++h) {
-        const c32 e = tw[(ka * h) % N];
-        acc[h].x = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[h].x));
-        acc[h].y = fmaf(v.x, e.y, fmaf(v.y, e.x, acc[h].y));
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < N; ++h) Zs[bt * g::ZS + h * H + kb] = acc[h];
+    for (int h = 0; h < N; ++h) Zs[bt * g::ZS + h * H + kb] = x[h];
   }
   __syncthreads();
-  // c2r along kb: one (image, h) row per thread: Re Z0 + Re(Z_{n/2} (-1)^w) + 2 sum_mid Re(Z_kb e^{+i..})
+  // c2r along kb: one (image, h) row per thread: the Hermitian completion X[N - k] = conj X[k]
+  // (imaginary parts of X[0], X[N/2] ignored, as torch's irfft does), inverse FFT, real part, 1/n^2
   constexpr float inv = 1.0f / (float)(N * N);
   constexpr int nh = N / 2;
   for (int row = tid; row < BT_I * N; row += NT) {
     const int bt = row % BT_I, h = row / BT_I;
     const c32* src = Zs + bt * g::ZS + h * H;
-    float acc[N];
-    const float z0 = src[0].x, zn = src[nh].x;
-#pragma unroll
-    for (int w = 0; w < N; ++w) acc[w] = 0.f;
+    c32 x[N];
+    x[0] = make_float2(src[0].x, 0.f);
+    x[nh] = make_float2(src[nh].x, 0.f);
 #pragma unroll
     for (int kb = 1; kb < nh; ++kb) {
       const c32 v = src[kb];
-#pragma unroll
-      for (int w = 0; w < N; ++w) {
-        const c32 e = tw[(kb * w) % N];
-        acc[w] = fmaf(v.x, e.x, fmaf(-v.y, e.y, acc[w]));
-      }
+      x[kb] = v;
+      x[N - kb] = make_float2(v.x, -v.y);
     }
+    fiode_fft::fft_reg<N, true>(x);
 #pragma unroll
-    for (int w = 0; w < N; ++w) out[bt * g::IS + h * g::RS + w] = (z0 + ((w & 1) ? -zn : zn) + 2.0f * acc[w]) * inv;
+    for (int w = 0; w < N; ++w) out[bt * g::IS + h * g::RS + w] = x[w].x * inv;
   }
   __syncthreads();
 }
@@ -240,7 +198,8 @@ __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c3
 // ---- y = irfft2(Y) (+ bias, GroupSort) or the space-to-channel scatter ---------------------------
 // gs: grid.x = C/2 channel pairs; else grid.x = C channels.
 template <int N>
-__global__ void __launch_bounds__(NT) k_sconv_irfft2(SArgs a) {
+__global__ void __launch_bounds__(nthreads<N>()) k_sconv_irfft2(SArgs a) {
+  constexpr int NT = nthreads<N>();
   typedef Geo<N> g;
   __shared__ c32 Ys[BT_I * g::ZS];
   __shared__ c32 Zs[BT_I * g::ZS];
@@ -308,14 +267,14 @@ extern "C" int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, co
   const int bt = small ? 4 : BT_F;
   const dim3 grid(a.C, (a.B + bt - 1) / bt);
   if (a.n == 8) {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(NT), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8>()), 0, st, a);
   } else if (a.n == 16) {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(NT), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(nthreads<16>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(nthreads<16>()), 0, st, a);
   } else {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<32, BT_F>), grid, dim3(NT), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(nthreads<32>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<32, BT_F>), grid, dim3(nthreads<32>()), 0, st, a);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
@@ -335,9 +294,9 @@ extern "C" int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, c
   const int gx = a.gs ? a.C / 2 : a.C;
   const dim3 grid(gx, (a.B + BT_I - 1) / BT_I);
   hipStream_t st = (hipStream_t)stream;
-  if (a.n == 8) hipLaunchKernelGGL(k_sconv_irfft2<8>, grid, dim3(NT), 0, st, a);
-  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_irfft2<16>, grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL(k_sconv_irfft2<32>, grid, dim3(NT), 0, st, a);
+  if (a.n == 8) hipLaunchKernelGGL(k_sconv_irfft2<8>, grid, dim3(nthreads<8>()), 0, st, a);
+  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_irfft2<16>, grid, dim3(nthreads<16>()), 0, st, a);
+  else hipLaunchKernelGGL(k_sconv_irfft2<32>, grid, dim3(nthreads<32>()), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
