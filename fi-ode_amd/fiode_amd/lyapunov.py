@@ -65,13 +65,27 @@ class ODETrainFn(torch.autograd.Function):
                                             masks=plan.get("masks"), offset_dev=plan.get("offset_dev"))
         plan["stats"] = stats
         ctx.plan, ctx.w, ctx.xf, ctx.ws = plan, w, xf, ws
+        from . import cayley as _cy
+        ctx.step_stream = _cy.STEP_STREAM
         return y
 
     @staticmethod
     def backward(ctx, g_y):
-        grads, _ = ops.odetrain_backward(g_y.contiguous(), ctx.xf, ctx.w, ctx.plan["dyn"], ctx.plan["cfg"], ctx.ws)
+        # The forward ran on a side stream beside the fan-out kernels; the backward has nothing to
+        # overlap with (the backbone backward needs its dL/dx_feat), so it runs on the step stream
+        # that produces g_y and consumes the gradients (ODE_BWD_ON_MAIN: no cross-queue hops).
+        from . import cayley as _cy
+
+        def run():
+            grads, _ = ops.odetrain_backward(g_y.contiguous(), ctx.xf, ctx.w, ctx.plan["dyn"], ctx.plan["cfg"],
+                                             ctx.ws)
+            return tuple(grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3"))
+        out = _cy._run_on_step_stream(ODE_BWD_ON_MAIN, ctx.step_stream, run)
         ctx.ws = None
-        return tuple(grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")) + (None, None)
+        return tuple(out) + (None, None)
+
+
+ODE_BWD_ON_MAIN = True
 
 
 class ODENllFn(torch.autograd.Function):

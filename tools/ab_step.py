@@ -145,7 +145,17 @@ def lin_one_conv_first(m):
     m.prefetch_schedule = {"after_input": True, "order": "conv_first", "lin_streams": "one"}
 
 
-ALL = {"default": reset2, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+def ode_bwd_side(m):
+    from fiode_amd import lyapunov
+    lyapunov.ODE_BWD_ON_MAIN = False
+
+
+def ode_bwd_main(m):
+    from fiode_amd import lyapunov
+    lyapunov.ODE_BWD_ON_MAIN = True
+
+
+ALL = {"default": reset2, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
@@ -155,6 +165,7 @@ steps = {}
 for k, f in VARIANTS.items():
     steps[k] = make(f)
     reset2(None)                    # flags only matter at capture time (inside make)
+    ode_bwd_main(None)
 times = {k: [] for k in VARIANTS}
 for r in range(rounds):
     for k, gs in steps.items():
