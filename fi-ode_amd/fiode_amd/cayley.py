@@ -468,11 +468,16 @@ class CayleyLinear(nn.Linear):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._pre is not None and self.training:
-            self._Q = _take(self._pre)
+            Q = _take(self._pre)
             self._pre = None
         elif self.training or self._Q is None:
-            self._Q = self.effective_weight()
-        return F.linear(x, self._Q if self.training else self._Q.detach(), self.bias)
+            Q = self.effective_weight()
+        else:
+            Q = self._Q
+        # kept detached: a stored Q with its graph would keep the step's autograd nodes (and the
+        # parameters' AccumulateGrad nodes) alive into the next step
+        self._Q = Q.detach()
+        return F.linear(x, Q if self.training else self._Q, self.bias)
 
 
 def group_prefetch(lins, stream: torch.cuda.Stream) -> None:
