@@ -161,18 +161,29 @@ __device__ __forceinline__ void tile_load(float (*dst)[LDT], const float* __rest
   }
 }
 
+// Look-ahead pivot: the workgroup of tile (k0 + PB, k0 + PB) -- the next panel's pivot block,
+// which no other tile of this launch reads -- inverts its freshly updated tile in LDS right away
+// (gjb.h, 4 waves) and writes P_next, so the next panel needs no pivot launch of its own (the chain
+// of a 512 inverse: pivot + 8 updates instead of 8 pivots + 8 updates).  The values are those the
+// separate pivot launch would load, so the inverse is bit-identical.
+typedef fiode_gjb::GJB<PB, 4> UpdGJ;
+static_assert(sizeof(UpdGJ::Smem) <= 3 * PB * LDT * sizeof(float), "pivot scratch fits the update's LDS");
+
 __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
                                                       const float* __restrict__ P, float* __restrict__ Y,
-                                                      float* __restrict__ final_out, int n, int64_t wstride) {
-  __shared__ __attribute__((aligned(16))) float sA[PB][LDT];    // P, or X_iK (row-major A operands)
-  __shared__ __attribute__((aligned(16))) float sX[PB][LDT];    // X_iK for the second product
-  __shared__ __attribute__((aligned(16))) float sB[PB][LDT];    // column-major B: X_Kj^T or P^T, then R^T
+                                                      float* __restrict__ final_out, int n, int64_t wstride,
+                                                      float* __restrict__ P_next) {
+  __shared__ __attribute__((aligned(16))) float lds[3][PB][LDT];
+  float (*sA)[LDT] = lds[0];    // P, or X_iK (row-major A operands)
+  float (*sX)[LDT] = lds[1];    // X_iK for the second product
+  float (*sB)[LDT] = lds[2];    // column-major B: X_Kj^T or P^T, then R^T
   const int ib = blockIdx.x * PB, jb = blockIdx.y * PB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
   const int64_t m = blockIdx.z;
   X += m * wstride;
   P += m * wstride;
   Y += m * wstride;
+  if (P_next) P_next += m * wstride;
   if (final_out) final_out += m * (int64_t)n * n;
   const bool piv_r = ib == k0, piv_c = jb == k0;
   f4v acc[4];
@@ -218,6 +229,17 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
         Y[(int64_t)gi * np + gj] = acc[bj][r];
       }
     }
+  if (P_next && ib == k0 + PB && jb == k0 + PB) {
+    UpdGJ::Smem& sm = *reinterpret_cast<UpdGJ::Smem*>(&lds[0][0][0]);
+    __syncthreads();                          // every wave is done with the product operands
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sm.cm[16 * w + 4 * q + r][16 * bj + i] = acc[bj][r];
+    __syncthreads();
+    UpdGJ::invert(sm);
+    UpdGJ::store(sm, P_next, PB, PB);
+  }
 }
 
 }  // namespace
@@ -239,7 +261,7 @@ extern "C" int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch,
 extern "C" size_t fiode_block_inverse_workspace_bytes(int32_t n) {
   if (n < 1) return 0;
   const size_t np = (size_t)((n + PB - 1) / PB) * PB;
-  return (2 * np * np + (size_t)PB * PB) * sizeof(float);
+  return (2 * np * np + 2 * (size_t)PB * PB) * sizeof(float);   // ping-pong matrices + two pivot inverses
 }
 
 extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
@@ -252,16 +274,17 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
   const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
   float* A = (float*)workspace;
   float* B = A + (size_t)np * np;
-  float* P = B + (size_t)np * np;
+  float* Pb[2] = {B + (size_t)np * np, B + (size_t)np * np + (size_t)PB * PB};
   hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256), (unsigned)batch), dim3(256), 0, st,
                      n, np, in, A, wstride);
+  // the first pivot block on its own; every later one is inverted by the previous update (look-ahead)
+  hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, 0, A,
+                     Pb[0], wstride);
   for (int kb = 0; kb < nb; ++kb) {
     const int k0 = kb * PB;
-    hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, k0, A,
-                       P, wstride);
     const bool last = kb == nb - 1;
-    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, P, B,
-                       last ? out : nullptr, n, wstride);
+    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, Pb[kb & 1], B,
+                       last ? out : nullptr, n, wstride, last ? nullptr : Pb[(kb + 1) & 1]);
     float* t = A;
     A = B;
     B = t;

@@ -277,14 +277,15 @@ FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64
 /* Error text for a return code. */
 /* Inverse of one real n x n matrix with positive-definite symmetric part (the Cayley systems of the
  * 512 x 512 backbone CayleyLinears and the 128 x 128 dynamics map): block Gauss-Jordan over
- * 64-wide panels (2 launches per panel), no pivot search, no host sync.  in may equal out. */
+ * 64-wide panels (one update launch per panel; the next pivot block is inverted inside it), no
+ * pivot search, no host sync.  in may equal out. */
 #define FIODE_BLOCK_INV_MAX_N 4096
 FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                   size_t workspace_bytes);
 /* The same for a batch of n x n matrices (in / out [batch][n][n] contiguous, workspace
  * batch * fiode_block_inverse_workspace_bytes(n)): one launch sequence for all of them, so the
- * Cayley systems of several layers share the 2 * n/64 dependent launches. */
+ * Cayley systems of several layers share the n/64 + 1 dependent launches. */
 FIODE_API int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
                                           void* workspace, size_t workspace_bytes);
 

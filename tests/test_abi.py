@@ -101,8 +101,8 @@ def test_spectral_cayley_host_checks():
 def test_block_inverse_host_checks():
     from fiode_amd import _lib
     lib = _lib.lib()
-    assert lib.fiode_block_inverse_workspace_bytes(512) == (2 * 512 * 512 + 64 * 64) * 4
-    assert lib.fiode_block_inverse_workspace_bytes(65) == (2 * 128 * 128 + 64 * 64) * 4
+    assert lib.fiode_block_inverse_workspace_bytes(512) == (2 * 512 * 512 + 2 * 64 * 64) * 4
+    assert lib.fiode_block_inverse_workspace_bytes(65) == (2 * 128 * 128 + 2 * 64 * 64) * 4
     assert lib.fiode_block_inverse(None, 0, None, None, None, 0) == 1
     dummy = ct.c_void_p(1)
     assert lib.fiode_block_inverse(None, 512, dummy, dummy, dummy, 100) == 3

@@ -7,8 +7,11 @@ export TMPDIR=/tmp
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
 FIODE_LIB=$PWD/tools/libfiode_ref.so timeout -k 10 120 python tools/ab_odetrain.py $O/ref.pt > $O/ref.log 2>&1 || { echo ref failed; exit 1; }
+FIODE_LIB=$PWD/tools/libfiode_ref.so timeout -k 10 60 python tools/ab_inverse.py $O/ref_inv.pt > $O/ref_inv.log 2>&1 || { echo ref inv failed; exit 1; }
 for L in "$@"; do
   n=$(basename $L .so)
+  FIODE_LIB=$PWD/$L timeout -k 10 60 python tools/ab_inverse.py $O/${n}_inv.pt > $O/${n}_inv.log 2>&1 || { echo $n inv failed; tail $O/${n}_inv.log; exit 1; }
+  echo "== $n inverse"; python tools/ab_inverse.py --cmp $O/ref_inv.pt $O/${n}_inv.pt
   FIODE_LIB=$PWD/$L timeout -k 10 120 python tools/ab_odetrain.py $O/$n.pt > $O/$n.log 2>&1 || { echo $n failed; tail $O/$n.log; exit 1; }
   echo "== $n"; python tools/ab_odetrain.py --cmp $O/ref.pt $O/$n.pt | grep -c identical
 done
