@@ -94,6 +94,25 @@ class GradAllReducer:
     def zero_grad(self):
         self.flat.zero_()
 
+    def gather(self):
+        """Move the gradients autograd just produced (fresh tensors: the backward ran with p.grad =
+        None, so AccumulateGrad stole its results instead of adding them into the bucket one kernel
+        per parameter) into the bucket with ONE multi-tensor copy, and re-point p.grad at the bucket
+        views.  A parameter that received no gradient gets zeros."""
+        views, o = [], 0
+        for p in self.params:
+            n = p.numel()
+            views.append(self.flat[o:o + n].view_as(p))
+            o += n
+        have = [(v, p.grad) for v, p in zip(views, self.params) if p.grad is not None]
+        if have:
+            torch._foreach_copy_([v for v, _ in have], [g for _, g in have])
+        for v, p in zip(views, self.params):
+            if p.grad is None:
+                v.zero_()
+            p.grad = v
+        return self.flat
+
     def allreduce(self, world: Optional[int] = None):
         world = dist.get_world_size(self.group) if world is None else world
         if world > 1:

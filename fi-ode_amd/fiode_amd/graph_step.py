@@ -42,16 +42,12 @@ class GraphTrainStep:
         if module.rng_counter is None:
             module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.params = [p for p in module.parameters() if p.requires_grad]
-        # N ranks: persistent grads (views into the reducer's flat bucket), zeroed and accumulated
-        # in place.  One rank: grads are set to None before the backward, so autograd hands its
-        # result tensors over (no zero fills, no accumulate adds); inside the graph they come from
-        # the graph's private pool at fixed addresses.
-        self.persistent = world > 1
-        if self.persistent:
-            for p in self.params:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-        self._grad_ptrs = [p.grad.data_ptr() for p in self.params] if self.persistent else None
+        # Grads are set to None before every backward, so autograd hands its result tensors over
+        # (no zero fills, no per-parameter accumulate adds); inside the graph they come from the
+        # graph's private pool at fixed addresses.  N ranks: one multi-tensor copy then moves them
+        # into the reducer's flat bucket (GradAllReducer.gather) and p.grad points at the bucket
+        # views, which the RCCL all-reduce and the optimizer graph use.
+        self.persistent = False
 
         # Warm-up iterations (lazy optimizer state, library handles, workspaces) run real updates on
         # the constructor's batch; the reference's Lightning loop makes no such updates, so the
@@ -81,8 +77,11 @@ class GraphTrainStep:
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt):
                 self.opt.step()
-        if self.persistent and [p.grad.data_ptr() for p in self.params] != self._grad_ptrs:
-            raise RuntimeError("autograd re-allocated .grad during capture; cannot replay into the bucket")
+        if self.reducer is not None and world > 1:
+            views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
+                     + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
+            if not all(views):
+                raise RuntimeError("p.grad does not point into the reducer's bucket after capture")
         self.scalars = module.last_plan["scalars"]
 
     def _snapshot(self):
@@ -120,17 +119,12 @@ class GraphTrainStep:
 
     def _fwd_bwd(self):
         m = self.module
-        if self.persistent:
-            if self.reducer is not None:
-                self.reducer.zero_grad()          # one fill of the flat bucket
-            else:
-                for p in self.params:
-                    p.grad.zero_()
-        else:
-            for p in self.params:
-                p.grad = None
+        for p in self.params:
+            p.grad = None
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         loss.backward()
+        if self.reducer is not None and self.world > 1:
+            self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)
         return loss
 
