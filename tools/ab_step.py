@@ -155,7 +155,15 @@ def ode_bwd_main(m):
     lyapunov.ODE_BWD_ON_MAIN = True
 
 
-ALL = {"default": reset2, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+def blas_rocblas(m):
+    torch.backends.cuda.preferred_blas_library("cublas")       # rocBLAS on ROCm
+
+
+def blas_lt(m):
+    torch.backends.cuda.preferred_blas_library("cublaslt")     # hipBLASLt on ROCm
+
+
+ALL = {"default": reset2, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
@@ -166,6 +174,7 @@ for k, f in VARIANTS.items():
     steps[k] = make(f)
     reset2(None)                    # flags only matter at capture time (inside make)
     ode_bwd_main(None)
+    blas_lt(None)
 times = {k: [] for k in VARIANTS}
 for r in range(rounds):
     for k, gs in steps.items():
