@@ -138,6 +138,79 @@ class ODELossMixFn(torch.autograd.Function):
         return go * (1.0 - ctx.p), gunit * go, None, None
 
 
+class LyapODELossFn(torch.autograd.Function):
+    """The configs[1] training loss as ONE autograd node (pl_modules.py:444-500): the fused
+    Lyapunov step, the train_ode RK4 solve (launched first on ``ode_stream`` when given, so it
+    overlaps the fan-out kernels), the nll term and the mix  loss * (1 - p) + nll(log y_hat) * p.
+    Backward: the solve's backward with dL/dy_hat = go * p * d nll / d y_hat (the mix kernel's unit
+    gradient), then its nine gradients plus the fused step's saved ones scaled by go * (1 - p), in
+    one multi-tensor add.  (As three nodes, autograd inserted two scale kernels, a zero fill and
+    one add kernel per shared input -- nine -- on the step's critical path.)  x_ode: the solve's
+    features when they are not x_feat (ode_reuse_features False), else None."""
+
+    @staticmethod
+    def forward(ctx, x_feat, x_ode, Q1, b1, Qx, bx, Q2, b2, Q3, b3, h0, y, plan: dict, oplan: dict, p: float,
+                ode_stream):
+        from .cayley import _prefetch, _take
+        w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
+        w = {k: v.detach().contiguous() for k, v in w.items()}
+        xf = x_feat.detach().float().contiguous()
+        xo = xf if x_ode is None else x_ode.detach().float().contiguous()
+
+        def solve():
+            return ops.odetrain_forward(xo, h0.detach().float().contiguous(), w, oplan["dyn"], oplan["cfg"],
+                                        masks=oplan.get("masks"), offset_dev=oplan.get("offset_dev"))
+        pre = _prefetch(ode_stream, solve) if ode_stream is not None else None
+        res = None if pre is not None else solve()
+        sc, grads, dbg = ops.lyap_step(
+            xf, y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"],
+            sampler=plan["sampler"], dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"],
+            offset=plan["offset"], h=plan.get("h"), masks=plan.get("masks"), debug=plan.get("debug", False),
+            out=plan.get("out"), offset_dev=plan.get("offset_dev"))
+        plan["scalars"] = sc
+        plan["debug_out"] = dbg
+        if pre is not None:
+            main = torch.cuda.current_stream(xf.device)
+            main.wait_event(pre[1])
+            for t in pre[0]:
+                t.record_stream(main)
+            res = pre[0]
+        y_hat, stats, ws = res
+        oplan["stats"] = stats
+        B = y_hat.shape[0]
+        total = torch.empty((), dtype=torch.float32, device=y_hat.device)
+        loss_ode = torch.empty((), dtype=torch.float32, device=y_hat.device)
+        gunit = torch.empty_like(y_hat)
+        L.check(L.lib().fiode_ode_loss_mix(ops._stream(y_hat.device), B, y_hat.data_ptr(), y.contiguous().data_ptr(),
+                                           sc.data_ptr(), float(p), loss_ode.data_ptr(), total.data_ptr(),
+                                           gunit.data_ptr()), "fiode_ode_loss_mix")
+        plan["loss_ode"] = loss_ode
+        plan["y_hat"] = y_hat
+        ctx.lyap = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+        ctx.ode = (gunit, xo, w, oplan, ws)
+        ctx.p = float(p)
+        ctx.split = x_ode is not None
+        return total
+
+    @staticmethod
+    def backward(ctx, go):
+        gunit, xo, w, oplan, ws = ctx.ode
+        ctx.ode = None
+        g_y = gunit * go
+        gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
+        keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+        ode = [gr[k] for k in keys]
+        lyap = torch._foreach_mul(ctx.lyap, go * (1.0 - ctx.p))
+        ctx.lyap = None
+        if ctx.split:     # the solve's features are another tensor: its gradient goes there
+            torch._foreach_add_(ode[1:], lyap[1:])
+            gx, gxo = lyap[0], ode[0]
+        else:
+            torch._foreach_add_(ode, lyap)
+            gx, gxo = ode[0], None
+        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None)
+
+
 class DecisionBoundary(nn.Module):
     """lya_cands.py:72-94 (kept for the validation/ODE path; the training step fuses it)."""
 
@@ -226,6 +299,9 @@ class LyapunovLearning(nn.Module):
         # train_ode branch: reuse the step's backbone features (True) or re-run the backbone as the
         # reference's self.model(x) does (False); DESIGN.md section 5 (common-subexpression reuse)
         self.ode_reuse_features = True
+        # the configs[1] loss as one autograd node (LyapODELossFn); False: three nodes (the Lyapunov
+        # step, the solve, the mix) as in round 1
+        self.fused_ode_loss = True
         self._side_streams = None
         self.logged: Dict[str, float] = {}
         self._out = None
@@ -452,6 +528,9 @@ class LyapunovLearning(nn.Module):
         plan = self.step_plan(y, h=h, masks=masks, debug=debug, static_state=static_state)
         w = self.dyn_fun.effective_weights()
         ode_on = self.train_ode and self.current_epoch > self.train_ode_epoch
+        if (ode_on and self.fused_ode_loss and static_state.is_cuda and self.simplex and y.dtype == torch.int64
+                and not self.lyap_after_ode):
+            return self._lyap_ode_loss(x, static_state, w, y, plan)
         if ode_on:        # launched first: on ROCm it runs on a side stream beside the fan-out kernels
             feat_ode = static_state
             if not self.ode_reuse_features:
@@ -525,6 +604,32 @@ class LyapunovLearning(nn.Module):
                 self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
             return _prefetch(self._ode_stream, lambda: ODETrainFn.apply(*args))
         return ODETrainFn.apply(*args)
+
+    def _lyap_ode_loss(self, x, static_state, w, y, plan):
+        """The fused configs[1] loss (LyapODELossFn): one autograd node for the Lyapunov step, the
+        train_ode solve and the mix (pl_modules.py:444-500)."""
+        x_ode = None
+        if not self.ode_reuse_features:
+            # reference order: self.model(x, ...) re-runs the backbone (pl_modules.py:491)
+            x_ode, _ = self.init_coordinates(x, self.dyn_fun)
+        h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
+        oplan = self.ode_plan(static_state.shape[0])
+        self.last_ode_plan = oplan
+        stream = None
+        if self.parallel_cayley and getattr(self, "ode_side_stream", True):
+            if getattr(self, "_ode_stream", None) is None:
+                self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
+            stream = self._ode_stream
+        p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
+        total = LyapODELossFn.apply(static_state, x_ode, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
+                                    w["b3"], h0, y, plan, oplan, p, stream)
+        sc = plan["scalars"]
+        self.log("kappa", plan["kappa"])
+        self.log("effective_batch_size", sc[1])
+        self.log("mean_active_constraints", sc[2])
+        self.log("loss_ode", plan["loss_ode"])
+        self.last_plan = plan
+        return total
 
     def _ode_loss(self, loss, y_hat, y):
         """pl_modules.py:494-500: loss * (1 - p) + nll(log y_hat) * p."""
