@@ -167,7 +167,7 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
