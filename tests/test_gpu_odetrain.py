@@ -122,6 +122,34 @@ def test_module_train_ode_loss_mix():
     assert int(s[0]) == 40 and int(s[1]) == 10
 
 
+@pytest.mark.parametrize("reuse", [True, False])
+def test_fused_loss_node_equals_three_nodes(reuse):
+    """LyapODELossFn (the configs[1] loss as one autograd node) = the three-node graph
+    (LyapunovLossFn + ODETrainFn + ODELossMixFn): same loss and the same gradients bit for bit --
+    the node sums ode + lyap * ((1 - p) go) exactly as autograd's accumulation does, with the same
+    Philox draws (same seed / offset) and the solve on its side stream in both."""
+    import bench
+    dev = _dev()
+    x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
+    out = {}
+    for fused in (True, False):
+        mod = bench.build_module(dev, seed=0, train_ode=True)
+        mod.parallel_cayley = False
+        mod.ode_reuse_features = reuse
+        mod.fused_ode_loss = fused
+        mod._rng_offset = 0
+        loss = mod.compute_loss(x, yb, 32, "relu")
+        loss.backward()
+        torch.cuda.synchronize()
+        out[fused] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
+                      {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
+    (la, oa, ga), (lb, ob, gb) = out[True], out[False]
+    assert torch.equal(la, lb) and oa == ob
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+
+
 @pytest.mark.parametrize("B", [1, 128, 300])
 def test_ode_nll_matches_torch(B):
     """ODENllFn (fiode_ode_nll) = F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497), forward
