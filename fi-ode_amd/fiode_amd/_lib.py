@@ -80,6 +80,12 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
+class AdamConfig(ct.Structure):
+    _fields_ = [("n_tensors", ct.c_int32), ("decoupled", ct.c_int32), ("maximize", ct.c_int32), ("pad_", ct.c_int32),
+                ("lr", ct.c_double), ("beta1", ct.c_double), ("beta2", ct.c_double), ("eps", ct.c_double),
+                ("weight_decay", ct.c_double), ("step", ct.c_double)]
+
+
 class SconvConfig(ct.Structure):
     _fields_ = [("n", ct.c_int32), ("C", ct.c_int32), ("B", ct.c_int32), ("downsample", ct.c_int32)]
 
@@ -155,6 +161,7 @@ def _load():
                                                      ct.c_size_t]),
         "fiode_spectral_cayley_backward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp, _vp,
                                                       _vp, ct.c_size_t]),
+        "fiode_adam_step": (ct.c_int, [_vp, ct.POINTER(AdamConfig), _vp, _vp, _vp, _vp, _vp, _vp]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

@@ -25,6 +25,7 @@ from . import ops
 from .dynamics import OrthoClassDynProjectSimplexLips
 from .models import IVP, DefaultOutputFun
 from .odeint import make_solver_params
+from .optim import FiodeAdam, FiodeAdamW
 from .sampling import CompositeSampler, CompositeSamplerScheduler, TrajectorySampler
 
 
@@ -360,18 +361,20 @@ class LyapunovLearning(nn.Module):
     def configure_optimizers(self, capturable: bool = False, fused: Optional[bool] = None):
         """pl_modules.py:97-147 (Adam/AdamW/SGD; cosine or step schedule; warm-up Adam).
         ``capturable``: Adam/AdamW keep their step counts on the device so the optimizer step
-        can be captured in a hipGraph (fiode_amd.graph_step).  ``fused``: Adam/AdamW as torch's
-        fused multi-tensor kernel (default on ROCm device parameters)."""
+        can be captured in a hipGraph (fiode_amd.graph_step).  ``fused`` (default on ROCm device
+        parameters): Adam/AdamW as fiode_amd.optim.FiodeAdam / FiodeAdamW -- torch's classes (same
+        state and state_dict) whose step is one HIP launch over all parameters (adam.hip)."""
         params = list(self.parameters())
         if fused is None:
             fused = bool(params) and params[0].is_cuda
         fk = {"fused": True, "capturable": capturable} if fused else {"capturable": capturable}
+        adam, adamw = (FiodeAdam, FiodeAdamW) if fused else (torch.optim.Adam, torch.optim.AdamW)
         if self.current_epoch < self.warmup:
-            return [torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas, **fk)]
+            return [adam(params, lr=1e-3, weight_decay=5e-4, amsgrad=False, betas=self.betas, **fk)]
         if self.opt_name == "Adam":
-            opt = torch.optim.Adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
+            opt = adam(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
         elif self.opt_name == "AdamW":
-            opt = torch.optim.AdamW(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
+            opt = adamw(params, lr=self.lr, weight_decay=self.weight_decay, betas=self.betas, **fk)
         elif self.opt_name == "SGD":
             # fix_backbone: SGD over the dynamics' parameters only (pl_modules.py:110-114)
             sgd_params = list(self.model.dyn_fun.parameters()) if self.fix_backbone else params

@@ -361,6 +361,26 @@ FIODE_API int fiode_spectral_cayley_backward(void* stream, const fiode_spectral_
                                              float* grad_weight, float* grad_alpha, void* workspace,
                                              size_t workspace_bytes);
 
+/* ---- optimizer step (pl_modules.py:97-147 configure_optimizers -> torch.optim.Adam / AdamW;
+ * fiode_amd/optim.py FiodeAdam): one launch updates every parameter tensor (adam.hip).  The host
+ * arrays hold n_tensors device pointers each; tensors are contiguous float32 of numel[i] elements.
+ * step: host array of device pointers to each tensor's step count after this step's increment
+ * (capturable Adam; an entry or the array may be NULL: cfg->step is used). */
+#define FIODE_ADAM_MAX_TENSORS 64
+typedef struct fiode_adam_config {
+  int32_t n_tensors;
+  int32_t decoupled;     /* AdamW: p -= lr wd p before the moments (else g += wd p)             */
+  int32_t maximize;
+  int32_t pad_;
+  /* hyper-parameters as the host holds them (Python floats): 1 - beta, the bias corrections and
+   * lr / (1 - beta1^t) are formed in double, then rounded to the fp32 the update runs in */
+  double lr, beta1, beta2, eps, weight_decay;
+  double step;
+} fiode_adam_config;
+FIODE_API int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float* const* params,
+                              const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                              const int64_t* numel, const float* const* step);
+
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);
 

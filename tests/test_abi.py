@@ -118,3 +118,38 @@ def test_small_cayley_host_checks():
     assert lib.fiode_small_cayley_forward(None, 1, 10, 20, None, None, None, None, None) == 1   # NULL pointers
     assert lib.fiode_small_cayley_forward(None, 0, 10, 20, None, None, None, None, None) == 0
     assert lib.fiode_small_cayley_backward(None, 1, 16, 513, None, None, None, None, None, None, None) == 1
+
+
+def test_adam_step_host_checks():
+    """fiode_adam_step validates the tensor table before launching: n_tensors <= 64, numel >= 0,
+    no NULL pointer for a non-empty tensor; zero tensors is a no-op."""
+    from fiode_amd import _lib as L
+    lib = L.lib()
+    cfg = L.AdamConfig(2, 0, 0, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0)
+    arr = ct.c_void_p * 2
+    one = arr(1, 2)
+    assert lib.fiode_adam_step(None, ct.byref(cfg), one, one, one, one, (ct.c_int64 * 2)(5, -1), None) == 1
+    assert lib.fiode_adam_step(None, ct.byref(cfg), arr(1, None), one, one, one, (ct.c_int64 * 2)(5, 3), None) == 1
+    cfg.n_tensors = 65
+    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None) == 1
+    cfg.n_tensors = 0
+    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None) == 0
+
+
+def test_fiode_adam_cpu_params_use_torch_step():
+    """FiodeAdam on CPU parameters is torch.optim.Adam exactly (the kernel covers ROCm tensors)."""
+    import torch
+    from fiode_amd.optim import FiodeAdam
+    g = torch.Generator().manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(7, generator=g))
+    q = torch.nn.Parameter(p.detach().clone())
+    o1 = FiodeAdam([p], lr=1e-2, weight_decay=1e-3)
+    o2 = torch.optim.Adam([q], lr=1e-2, weight_decay=1e-3)
+    for _ in range(3):
+        gr = torch.randn(7, generator=g)
+        p.grad, q.grad = gr.clone(), gr.clone()
+        o1.step()
+        o2.step()
+    assert torch.equal(p, q)
+    assert isinstance(o1, torch.optim.Adam)
+    assert o1.state_dict()["state"][0]["step"].item() == 3

@@ -24,6 +24,10 @@ def make(setup):
     mod = bench.build_module(dev, train_ode=True)
     setup(mod)
     opt = mod.configure_optimizers(capturable=True)[0][0]
+    if getattr(mod, "_torch_adam", False):
+        g0 = opt.param_groups[0]
+        opt = torch.optim.Adam(mod.parameters(), lr=g0["lr"], betas=g0["betas"], weight_decay=g0["weight_decay"],
+                               fused=True, capturable=True)
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
@@ -163,11 +167,15 @@ def blas_lt(m):
     torch.backends.cuda.preferred_blas_library("cublaslt")     # hipBLASLt on ROCm
 
 
+def torch_adam(m):
+    m._torch_adam = True
+
+
 def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "torch_adam": torch_adam, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
