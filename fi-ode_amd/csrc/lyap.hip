@@ -739,7 +739,7 @@ __global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
     for (int b = 0; b < a.B; ++b) s += a.g_u[(size_t)b * M + i];
     a.grads.bx[i] = s;
     a.grads.b1[i] = s;
-  } else if (e < M * FIODE_X + M + a.B * FIODE_X) {
+  } else if (a.grads.x_feat && e < M * FIODE_X + M + a.B * FIODE_X) {
     const int q = e - M * FIODE_X - M, b = q / FIODE_X, c = q - b * FIODE_X;
     float s = 0.f;
 #pragma unroll 16

@@ -715,29 +715,83 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   return FIODE_OK;
 }
 
-extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
-                                       const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
-                                       fiode_lyap_grads* grads, float* dbg_gft, void* workspace,
-                                       size_t workspace_bytes) {
+namespace {
+// dL/dx_feat of the solve straight from the per-row layer-1 gradients k_ot_bwd leaves in the
+// workspace: g_u[b][m] = sum_e gz1[b E + e][m] (e ascending), gx[b][x] = sum_m g_u[b][m] Qx[m][x]
+// (m ascending, fused multiply-adds as k_lyap_static_grads), then optionally + add[b][x] * scale[0]
+// (the other loss term's x_feat gradient and its upstream scale: the combined gradient in one
+// launch).  One workgroup per image, one thread per hidden unit.
+__global__ __launch_bounds__(M) void k_ot_gx(int E, const float* __restrict__ gz1, const float* __restrict__ Qx,
+                                             const float* __restrict__ add, const float* __restrict__ scale,
+                                             float* __restrict__ gx) {
+  __shared__ float gu[M];
+  const int b = blockIdx.x, m = threadIdx.x;
+  const float* p = gz1 + (size_t)b * E * M + m;
+  float s = 0.f;
+#pragma unroll 8
+  for (int e = 0; e < E; ++e) s += p[(size_t)e * M];
+  gu[m] = s;
+  __syncthreads();
+  if (m < FIODE_X) {
+    float d = 0.f;
+#pragma unroll 16
+    for (int i = 0; i < M; ++i) d = __fmaf_rn(gu[i], Qx[i * FIODE_X + m], d);
+    if (add) d = d + add[(size_t)b * FIODE_X + m] * scale[0];
+    gx[(size_t)b * FIODE_X + m] = d;
+  }
+}
+}  // namespace
+
+extern "C" int fiode_odetrain_backward_x(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
+                                         const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
+                                         float* gx, const float* gx_add, const float* gx_add_scale, float* dbg_gft,
+                                         void* workspace, size_t workspace_bytes) {
   OTArgs a{};
   int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
-  if (!g_y || !grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 ||
-      !grads->Q3 || !grads->b3 || !grads->x_feat)
-    return FIODE_EINVAL;
+  if (!g_y || !gx || (gx_add && !gx_add_scale)) return FIODE_EINVAL;
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t lds = sizeof(OtBwdShared);     // weight operands in registers (VjpW)
   if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
   else hipLaunchKernelGGL(k_ot_bwd<false>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_ot_gx, dim3(a.B), dim3(M), 0, st, a.E, (const float*)a.gz1, w->Qx, gx_add, gx_add_scale, gx);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
+
+extern "C" int fiode_odetrain_backward_weights(void* stream, const fiode_odetrain_config* cfg,
+                                               const fiode_dyn_config* dyn, const fiode_dyn_weights* w,
+                                               const float* x_feat, fiode_lyap_grads* grads, void* workspace,
+                                               size_t workspace_bytes) {
+  OTArgs a{};
+  int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
+  if (rc) return rc;
+  if (!grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
+      !grads->b3)
+    return FIODE_EINVAL;
   const OtLayout L = ot_layout(a.B, a.E);
   fiode_internal::WgradIO io{};
   io.B = a.B; io.S = a.E; io.x_feat = x_feat; io.Qx = w->Qx; io.h = a.hs; io.a1 = a.a1; io.a2 = a.a2;
   io.gz2 = a.gz2; io.gz1 = a.gz1; io.gft = a.gft;
   io.workspace = static_cast<char*>(workspace) + L.wg;
   io.grads = *grads;
-  return fiode_internal::launch_wgrad(st, io);
+  io.grads.x_feat = nullptr;                  // dL/dx_feat: fiode_odetrain_backward_x
+  return fiode_internal::launch_wgrad(static_cast<hipStream_t>(stream), io);
+}
+
+extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
+                                       const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
+                                       fiode_lyap_grads* grads, float* dbg_gft, void* workspace,
+                                       size_t workspace_bytes) {
+  if (!grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
+      !grads->b3 || !grads->x_feat)
+    return FIODE_EINVAL;
+  int rc = fiode_odetrain_backward_x(stream, cfg, dyn, w, x_feat, g_y, grads->x_feat, nullptr, nullptr, dbg_gft,
+                                 workspace, workspace_bytes);
+  if (rc) return rc;
+  return fiode_odetrain_backward_weights(stream, cfg, dyn, w, x_feat, grads, workspace, workspace_bytes);
 }
 
 // ---- the train_ode loss term: F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497) --------

@@ -134,6 +134,12 @@ def _load():
         "fiode_odetrain_backward": (ct.c_int, [_vp, ct.POINTER(OdeTrainConfig), ct.POINTER(DynConfig),
                                                ct.POINTER(DynWeights), _vp, _vp, ct.POINTER(LyapGrads), _vp, _vp,
                                                ct.c_size_t]),
+        "fiode_odetrain_backward_x": (ct.c_int, [_vp, ct.POINTER(OdeTrainConfig), ct.POINTER(DynConfig),
+                                                 ct.POINTER(DynWeights), _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                 ct.c_size_t]),
+        "fiode_odetrain_backward_weights": (ct.c_int, [_vp, ct.POINTER(OdeTrainConfig), ct.POINTER(DynConfig),
+                                                       ct.POINTER(DynWeights), _vp, ct.POINTER(LyapGrads), _vp,
+                                                       ct.c_size_t]),
         "fiode_groupsort_forward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp]),
         "fiode_groupsort_backward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp, _vp]),
         "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,

@@ -151,7 +151,7 @@ class LyapODELossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_feat, x_ode, Q1, b1, Qx, bx, Q2, b2, Q3, b3, h0, y, plan: dict, oplan: dict, p: float,
-                ode_stream):
+                ode_stream, wtok=None, holder=None):
         from .cayley import _prefetch, _take
         w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
         w = {k: v.detach().contiguous() for k, v in w.items()}
@@ -191,6 +191,7 @@ class LyapODELossFn(torch.autograd.Function):
         ctx.ode = (gunit, xo, w, oplan, ws)
         ctx.p = float(p)
         ctx.split = x_ode is not None
+        ctx.holder = holder
         return total
 
     @staticmethod
@@ -198,6 +199,21 @@ class LyapODELossFn(torch.autograd.Function):
         gunit, xo, w, oplan, ws = ctx.ode
         ctx.ode = None
         g_y = gunit * go
+        if ctx.holder is not None:
+            # weight gradients in _ODEWeightGradFn (its own node, on its own stream): here only the
+            # adjoint sweep and dL/dx_feat, so the backbone's backward starts right after them
+            s = go * (1.0 - ctx.p)
+            lyap_x = ctx.lyap[0]
+            if ctx.split:
+                gxo = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
+                gx = lyap_x * s
+            else:
+                gx = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws, gx_add=lyap_x,
+                                             gx_add_scale=s)
+                gxo = None
+            ctx.holder.update(ode=(xo, w, oplan, ws), lyap_w=ctx.lyap[1:], scale=s)
+            ctx.lyap = ctx.holder = None
+            return (gx, gxo) + (None,) * 14 + (go, None)
         gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
         keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         ode = [gr[k] for k in keys]
@@ -209,7 +225,33 @@ class LyapODELossFn(torch.autograd.Function):
         else:
             torch._foreach_add_(ode, lyap)
             gx, gxo = ode[0], None
-        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None)
+        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None, None, None)
+
+
+class _ODEWeightGradFn(torch.autograd.Function):
+    """The weight-gradient half of LyapODELossFn's backward as a node of its own: forward returns a
+    token LyapODELossFn consumes; backward (run on the stream the forward ran on -- a side stream,
+    see LyapunovLearning._lyap_ode_loss) sums the solve's weight gradients
+    (fiode_odetrain_backward_weights) and adds the fused step's, scaled by go * (1 - p): the same
+    float32 operations as the one-node backward, off the path to the backbone's backward."""
+
+    @staticmethod
+    def forward(ctx, Q1, b1, Qx, bx, Q2, b2, Q3, b3, holder: dict):
+        ctx.holder = holder
+        return Q1.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _g):
+        h, ctx.holder = ctx.holder, None
+        xo, w, oplan, ws = h.pop("ode")
+        lyap_w, s = h.pop("lyap_w"), h.pop("scale")
+        gr = ops.odetrain_backward_weights(xo, w, oplan["dyn"], oplan["cfg"], ws)
+        ode = [gr[k] for k in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+        torch._foreach_add_(ode, torch._foreach_mul(lyap_w, s))
+        st = torch.cuda.current_stream(xo.device)
+        for t in (xo, ws, s, *lyap_w, *w.values()):     # produced on other streams, freed after this
+            t.record_stream(st)
+        return tuple(ode) + (None,)
 
 
 class DecisionBoundary(nn.Module):
@@ -303,6 +345,10 @@ class LyapunovLearning(nn.Module):
         # the configs[1] loss as one autograd node (LyapODELossFn); False: three nodes (the Lyapunov
         # step, the solve, the mix) as in round 1
         self.fused_ode_loss = True
+        # the fused loss node's weight gradients as a separate node (_ODEWeightGradFn) on a side
+        # stream ("own") or the solve's stream ("ode"), off the path from the solve's backward to
+        # the backbone's: no measurable gain (scheduling probes), off
+        self.split_ode_wgrad = False
         self._side_streams = None
         self.logged: Dict[str, float] = {}
         self._out = None
@@ -624,8 +670,25 @@ class LyapunovLearning(nn.Module):
                 self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
             stream = self._ode_stream
         p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
+        wtok = holder = None
+        if self.split_ode_wgrad and static_state.is_cuda and torch.is_grad_enabled():
+            # the weight-gradient node forks onto its own stream (joined here: a captured graph
+            # sees a fork / join), so its backward runs beside the backbone's
+            if self.split_ode_wgrad == "ode" and stream is not None:
+                ws_stream = stream
+            else:
+                if getattr(self, "_wgrad_stream", None) is None:
+                    self._wgrad_stream = torch.cuda.Stream(static_state.device)
+                ws_stream = self._wgrad_stream
+            main = torch.cuda.current_stream(static_state.device)
+            ws_stream.wait_stream(main)
+            holder = {}
+            with torch.cuda.stream(ws_stream):
+                wtok = _ODEWeightGradFn.apply(w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"], w["b3"],
+                                              holder)
+            main.wait_stream(ws_stream)
         total = LyapODELossFn.apply(static_state, x_ode, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
-                                    w["b3"], h0, y, plan, oplan, p, stream)
+                                    w["b3"], h0, y, plan, oplan, p, stream, wtok, holder)
         sc = plan["scalars"]
         self.log("kappa", plan["kappa"])
         self.log("effective_batch_size", sc[1])

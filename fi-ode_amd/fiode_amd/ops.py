@@ -349,6 +349,47 @@ def odetrain_backward(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str
     return grads, dbg
 
 
+def odetrain_backward_x(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
+                        cfg: L.OdeTrainConfig, ws: torch.Tensor, gx_add: Optional[torch.Tensor] = None,
+                        gx_add_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fiode_odetrain_backward_x: the adjoint sweep and dL/dx_feat [B, X] (+ gx_add * gx_add_scale,
+    a device scalar).  ``odetrain_backward_weights`` on the same workspace completes the gradients."""
+    dev = g_y.device
+    B = int(cfg.batch)
+    g_y = _need(g_y.float(), "g_y", (B, C), torch.float32, dev)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    if gx_add is not None:
+        gx_add = _need(gx_add, "gx_add", (B, X), torch.float32, dev)
+        gx_add_scale = _need(gx_add_scale.reshape(1), "gx_add_scale", (1,), torch.float32, dev)
+    ws_w, cw = _weights_c(weights, dev)
+    gx = torch.empty((B, X), dtype=torch.float32, device=dev)
+    dc = dyn.to_c()
+    rc = L.lib().fiode_odetrain_backward_x(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(),
+                                           g_y.data_ptr(), gx.data_ptr(), _ptr(gx_add),
+                                           _ptr(gx_add_scale if gx_add is not None else None), None, ws.data_ptr(),
+                                           ws.numel())
+    L.check(rc, "fiode_odetrain_backward_x")
+    del ws_w
+    return gx
+
+
+def odetrain_backward_weights(x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
+                              cfg: L.OdeTrainConfig, ws: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """fiode_odetrain_backward_weights: the eight weight gradients (after odetrain_backward_x)."""
+    dev = x_feat.device
+    B = int(cfg.batch)
+    x_feat = _need(x_feat, "x_feat", (B, X), torch.float32, dev)
+    ws_w, cw = _weights_c(weights, dev)
+    grads = {k: torch.empty(WEIGHT_SHAPES[k], dtype=torch.float32, device=dev) for k in WEIGHT_KEYS}
+    cg = L.LyapGrads(*([grads[k].data_ptr() for k in WEIGHT_KEYS] + [None]))
+    dc = dyn.to_c()
+    rc = L.lib().fiode_odetrain_backward_weights(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw),
+                                                 x_feat.data_ptr(), ct.byref(cg), ws.data_ptr(), ws.numel())
+    L.check(rc, "fiode_odetrain_backward_weights")
+    del ws_w
+    return grads
+
+
 def certify_grid(T: int = 40, n: int = C, device="cuda") -> torch.Tensor:
     """grid_label_0 of sample_decision_boundary(n, T) as uint8 counts [G][n] (eta = v/T)."""
     lib = L.lib()

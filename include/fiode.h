@@ -228,6 +228,20 @@ FIODE_API int fiode_odetrain_backward(void* stream, const fiode_odetrain_config*
                                       const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
                                       fiode_lyap_grads* grads, float* dbg_gft, void* workspace,
                                       size_t workspace_bytes);
+/* fiode_odetrain_backward in two parts, so the backbone's backward (which needs only dL/dx_feat)
+ * can start before the weight gradients are summed (these may then run on another stream):
+ *   _x:       the adjoint sweep (k_ot_bwd) and gx [B][X] = dL/dx_feat, plus gx_add [B][X] times
+ *             gx_add_scale[0] (device scalar) when gx_add is given;
+ *   _weights: the weight gradients (grads->x_feat ignored); after _x on the same workspace.
+ * fiode_odetrain_backward = _x then _weights (same results). */
+FIODE_API int fiode_odetrain_backward_x(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
+                                        const fiode_dyn_weights* w, const float* x_feat, const float* g_y, float* gx,
+                                        const float* gx_add, const float* gx_add_scale, float* dbg_gft,
+                                        void* workspace, size_t workspace_bytes);
+FIODE_API int fiode_odetrain_backward_weights(void* stream, const fiode_odetrain_config* cfg,
+                                              const fiode_dyn_config* dyn, const fiode_dyn_weights* w,
+                                              const float* x_feat, fiode_lyap_grads* grads, void* workspace,
+                                              size_t workspace_bytes);
 
 /* ---- Certification grid (robustness/eval_utils.py:31-89, certify_lipschitz.py:37-143) ------ */
 typedef struct fiode_certify_config {

@@ -153,3 +153,24 @@ def test_fiode_adam_cpu_params_use_torch_step():
     assert torch.equal(p, q)
     assert isinstance(o1, torch.optim.Adam)
     assert o1.state_dict()["state"][0]["step"].item() == 3
+
+
+def test_odetrain_backward_parts_host_checks():
+    """fiode_odetrain_backward_x / _weights refuse missing arguments before any launch (gx_add
+    without its scale; a NULL gradient output)."""
+    from fiode_amd import _lib as L
+    lib = L.lib()
+    assert lib.fiode_odetrain_backward_x(None, None, None, None, None, None, None, None, None, None, None, 0) == 1
+    assert lib.fiode_odetrain_backward_weights(None, None, None, None, None, None, None, 0) == 1
+    cfg = L.OdeTrainConfig(8, 0, 0, 0, 0.0, 1.0, 0.25)
+    dyn = L.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 30, 1e-4)
+    d = ct.c_void_p(1)
+    w = L.DynWeights(*([d] * 8))
+    big = 1 << 40
+    # gx_add given, scale missing
+    assert lib.fiode_odetrain_backward_x(None, ct.byref(cfg), ct.byref(dyn), ct.byref(w), d, d, d, d, None, None, d,
+                                         big) == 1
+    g = L.LyapGrads(*([d] * 8 + [None]))
+    g.Q2 = None
+    assert lib.fiode_odetrain_backward_weights(None, ct.byref(cfg), ct.byref(dyn), ct.byref(w), d, ct.byref(g), d,
+                                               big) == 1

@@ -127,27 +127,33 @@ def test_fused_loss_node_equals_three_nodes(reuse):
     """LyapODELossFn (the configs[1] loss as one autograd node) = the three-node graph
     (LyapunovLossFn + ODETrainFn + ODELossMixFn): same loss and the same gradients bit for bit --
     the node sums ode + lyap * ((1 - p) go) exactly as autograd's accumulation does, with the same
-    Philox draws (same seed / offset) and the solve on its side stream in both."""
+    Philox draws (same seed / offset) and the solve on its side stream in both.  Also with the
+    node's weight gradients split off into their own node on another stream."""
     import bench
     dev = _dev()
     x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
     yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
     out = {}
-    for fused in (True, False):
+    for variant in ("fused", "split", "three"):
         mod = bench.build_module(dev, seed=0, train_ode=True)
         mod.parallel_cayley = False
         mod.ode_reuse_features = reuse
-        mod.fused_ode_loss = fused
+        mod.fused_ode_loss = variant != "three"
+        # "split": the node's weight gradients as a second node on its own stream (_ODEWeightGradFn,
+        # fiode_odetrain_backward_x / _weights)
+        mod.split_ode_wgrad = "own" if variant == "split" else False
         mod._rng_offset = 0
         loss = mod.compute_loss(x, yb, 32, "relu")
         loss.backward()
         torch.cuda.synchronize()
-        out[fused] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
-                      {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
-    (la, oa, ga), (lb, ob, gb) = out[True], out[False]
-    assert torch.equal(la, lb) and oa == ob
-    for n in ga:
-        assert torch.equal(ga[n], gb[n]), n
+        out[variant] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
+                        {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
+    lb, ob, gb = out["three"]
+    for variant in ("fused", "split"):
+        la, oa, ga = out[variant]
+        assert torch.equal(la, lb) and oa == ob, variant
+        for n in ga:
+            assert torch.equal(ga[n], gb[n]), (variant, n)
 
 
 @pytest.mark.parametrize("B", [1, 128, 300])
@@ -273,13 +279,18 @@ def test_feature_reuse_equals_reference_order():
                                               if p.requires_grad})
     (la, ga), (lb, gb) = out[True], out[False]
     assert torch.equal(la, lb)
+    errs = {}
     for n in ga:
         if n.startswith("model.dyn_fun."):
             assert torch.equal(ga[n], gb[n]), n
         else:
             scale = float(gb[n].abs().max()) + 1e-12
-            err = float((ga[n] - gb[n]).abs().max()) / scale
-            assert err <= 1e-4, (n, err)
+            errs[n] = float((ga[n] - gb[n]).abs().max()) / scale
+    print("backbone gradient max relative differences:", sorted(errs.items(), key=lambda kv: -kv[1])[:4])
+    # a CayleyLinear's alpha gradient is one scalar, <dL/dX, W> / ||W|| over all cout x cin
+    # entries with terms of both signs: its relative rounding spread is a few times a tensor's
+    for n, e in errs.items():
+        assert e <= (3e-4 if n.endswith(".alpha") else 1e-4), (n, e)
 
 
 @pytest.mark.parametrize("scale_nominal,mode", [(False, "philox"), (True, "given")])

@@ -167,6 +167,18 @@ def blas_lt(m):
     torch.backends.cuda.preferred_blas_library("cublaslt")     # hipBLASLt on ROCm
 
 
+def no_split(m):
+    m.split_ode_wgrad = False
+
+
+def split_own(m):
+    m.split_ode_wgrad = "own"
+
+
+def split_ode(m):
+    m.split_ode_wgrad = "ode"
+
+
 def torch_adam(m):
     m._torch_adam = True
 
@@ -175,7 +187,7 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "torch_adam": torch_adam, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
