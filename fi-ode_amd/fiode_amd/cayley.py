@@ -560,6 +560,34 @@ class _SpectralCayleyFn(torch.autograd.Function):
         return gw, ga.reshape(alpha.shape), None
 
 
+class _SpectralCayleyStoredFn(torch.autograd.Function):
+    """The Q of a CayleyConv whose map was computed AHEAD, into fixed buffers (CayleyConv
+    pipeline_on / refresh_map: at the end of the previous training step, right after this layer's
+    parameters were updated): forward hands out the stored Q (no kernel); backward is
+    _SpectralCayleyFn's, from the stored inverse and workspace, then ``store["on_grads"]`` (if set)
+    gets (dL/dweight, dL/dalpha) -- GraphTrainStep updates the layer's parameters there and
+    computes its next map while the rest of the backward runs."""
+
+    @staticmethod
+    def forward(ctx, weight, alpha, n: int, store: dict):
+        ctx.save_for_backward(weight, alpha)
+        ctx.store, ctx.n = store, n
+        return store["Q"].detach()
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from . import ops
+        weight, alpha = ctx.saved_tensors
+        st = ctx.store
+        gw, ga = ops.spectral_cayley_backward(gQ.contiguous(), weight.detach(), alpha.detach(), ctx.n, st["inv"],
+                                              st["ws"])
+        ga = ga.reshape(alpha.shape)
+        hook = st.get("on_grads")
+        if hook is not None:
+            hook(gw, ga)
+        return gw, ga, None, None
+
+
 class _SpectralConvFn(torch.autograd.Function):
     """y = [GroupSort](irfft2(Q[f] @ rfft2(x)[f]) + bias) on spatial-major activations, the
     transforms as HIP kernels that read / write the GEMM layout [f][C][B] (sconv.hip), the
@@ -625,6 +653,7 @@ class CayleyConv(nn.Conv2d):
         self._shift = {}
         self._n = None
         self._pre = None
+        self._store = None              # map computed ahead (pipeline_on), else None
 
     def _load_from_state_dict(self, *args, **kw):
         super()._load_from_state_dict(*args, **kw)
@@ -667,14 +696,52 @@ class CayleyConv(nn.Conv2d):
             self._alpha_init = True
         return cayley_scaled(wf, self.alpha)
 
+    # ---- maps computed ahead (GraphTrainStep): the next step's Q right after this step's update --
+    def pipeline_on(self) -> bool:
+        """Keep this layer's map in fixed buffers, computed ahead by refresh_map (now, from the
+        current parameters).  Only for the fused map after one training forward (input size known);
+        returns whether the layer is pipelined."""
+        if not (self.fused and self._alpha_init and self._n is not None and self.weight.is_cuda
+                and self._fused_ok(self._n)):
+            return False
+        from . import ops
+        Q, inv, ws = ops.spectral_cayley_forward(self.weight.detach(), self.alpha.detach(), self._n)
+        self._store = {"Q": Q, "inv": inv, "ws": ws, "n": self._n,
+                       "stream": torch.cuda.Stream(self.weight.device)}
+        return True
+
+    def pipeline_off(self) -> None:
+        self._store = None
+
+    def refresh_map(self) -> None:
+        """Recompute the stored map from the current parameters (same kernels as the step-start
+        map, so the same Q bit for bit), on the current stream."""
+        from . import ops
+        st = self._store
+        ops.spectral_cayley_forward(self.weight.detach(), self.alpha.detach(), st["n"],
+                                    out=(st["Q"], st["inv"], st["ws"]))
+
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's spectral Cayley maps on a side stream (needs one forward first, to
         know the input size and initialise alpha)."""
+        if self._store is not None:
+            return
         if self._n is not None and self._alpha_init:
             n = self._n
             self._pre = _prefetch(stream, lambda: self.spectral_weight(n, self.weight.device))
 
     def _take_spectral(self, n: int, device) -> torch.Tensor:
+        st = self._store
+        if st is not None and self.training and st["n"] == n and torch.is_grad_enabled():
+            # the node's backward (map backward + the store's hook) runs on the layer's own stream
+            side = st["stream"]
+            main = torch.cuda.current_stream(device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                Q = _SpectralCayleyStoredFn.apply(self.weight, self.alpha, n, st)
+            main.wait_stream(side)
+            self._pre = None
+            return Q
         if self._pre is not None and self.training and self._n == n:
             Q = _take(self._pre)
         else:

@@ -9,7 +9,9 @@ the Cayley inverses are all device-side), so it is captured once and replayed:
   -> backward, accumulating into the persistent ``p.grad`` tensors (with a GradAllReducer these
   are views into its flat bucket) -> advance the device Philox counter, so every replay draws
   fresh samples and dropout masks;
-* ``opt`` graph: the Adam step (``capturable=True``: step counts on the device).
+* ``opt`` graph: the Adam step (``capturable=True``: step counts on the device);
+* maps_ahead: the conv layers' Cayley maps of the NEXT step are computed inside this one (see
+  ``_maps_ahead_on``).
 For one rank both are captured into a single graph; for N ranks the RCCL gradient all-reduce
 and the metric reduce run eagerly between the two replays.
 
@@ -27,7 +29,7 @@ import torch
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
-                 warmup: int = 3, act: str = "relu", check_every: int = 200):
+                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
@@ -67,22 +69,67 @@ class GraphTrainStep:
         torch.cuda.synchronize(dev)
 
         self.single = world == 1
+        self.piped, self.early = [], False
+        if maps_ahead:
+            self._maps_ahead_on()
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
             self.loss = self._fwd_bwd()
             if self.single:
                 self.opt.step()
+                self._refresh_late()
         self.g_opt = None
         if not self.single:
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt):
                 self.opt.step()
+                self._refresh_late()
         if self.reducer is not None and world > 1:
             views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
                      + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
             if not all(views):
                 raise RuntimeError("p.grad does not point into the reducer's bucket after capture")
         self.scalars = module.last_plan["scalars"]
+
+    # ---- conv maps computed ahead -------------------------------------------------------------
+    # Each CayleyConv's spectral map depends only on its own two parameters, and the step's first
+    # convolution waits for it.  With maps_ahead the map of step t+1 is computed at the end of step
+    # t into fixed buffers (CayleyConv.pipeline_on): on one rank inside the backward, as soon as the
+    # layer's gradient is final (its map backward), the layer's parameters get their Adam update
+    # (FiodeAdam.step_params) and the next map is computed on the layer's stream while the rest of
+    # the backward runs; on N ranks (gradients final only after the all-reduce) after the optimizer
+    # step.  The maps are the same kernels on the same parameters as at the start of the next step,
+    # so the results are unchanged.  Parameters changed outside the replays: call refresh_maps().
+    def _maps_ahead_on(self):
+        from .cayley import CayleyConv
+        from .optim import _KernelStepMixin
+        self.early = self.single and isinstance(self.opt, _KernelStepMixin)
+        for c in self.module.modules():
+            if isinstance(c, CayleyConv) and c.pipeline_on():
+                self.piped.append(c)
+                if self.early:
+                    c._store["on_grads"] = (lambda gw, ga, c=c: self._update_layer(c, gw, ga))
+
+    def _update_layer(self, c, gw, ga):
+        self.opt.step_params([(c.weight, gw), (c.alpha, ga)])
+        c.refresh_map()
+
+    def _refresh_late(self):
+        if not self.early:
+            for c in self.piped:
+                c.refresh_map()
+
+    def refresh_maps(self) -> None:
+        """Recompute the maps computed ahead from the current parameters (after loading a
+        checkpoint or any update outside the replays)."""
+        for c in self.piped:
+            c.refresh_map()
+
+    def close(self) -> None:
+        """Back to maps computed at the start of each step (eager training of the same module)."""
+        for c in self.piped:
+            c.pipeline_off()
+        self.piped = []
 
     def _snapshot(self):
         """Copies of what a warm-up iteration changes: parameters, optimizer state (None where a

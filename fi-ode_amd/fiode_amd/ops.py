@@ -516,9 +516,10 @@ def spectral_supported(weight_shape, n: int) -> bool:
     return L.lib().fiode_spectral_workspace_bytes(ct.byref(cfg)) > 0
 
 
-def spectral_cayley_forward(weight: torch.Tensor, alpha: torch.Tensor, n: int):
+def spectral_cayley_forward(weight: torch.Tensor, alpha: torch.Tensor, n: int, out=None):
     """fiode_spectral_cayley_forward: Q complex64 [n (n/2+1), cout, cin] = cayley(alpha Wf / ||Wf||)
-    per rFFT frequency.  Returns (Q, inv, workspace); inv and workspace feed the backward."""
+    per rFFT frequency.  Returns (Q, inv, workspace); inv and workspace feed the backward.  ``out``:
+    a previous call's (Q, inv, workspace) to overwrite (a map computed ahead into fixed buffers)."""
     dev = weight.device
     cout, cin = int(weight.shape[0]), int(weight.shape[1])
     weight = _need(weight, "weight", tuple(weight.shape), torch.float32, dev)
@@ -529,9 +530,16 @@ def spectral_cayley_forward(weight: torch.Tensor, alpha: torch.Tensor, n: int):
     if nb == 0:
         raise ValueError(f"spectral Cayley: unsupported layer {tuple(weight.shape)} at n={n}")
     nf, K = n * (n // 2 + 1), min(cout, cin)
-    Q = torch.empty((nf, cout, cin), dtype=torch.complex64, device=dev)
-    inv = torch.empty((nf, K, K), dtype=torch.complex64, device=dev)
-    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    if out is not None:
+        Q, inv, ws = out
+        _need(Q, "Q", (nf, cout, cin), torch.complex64, dev)
+        _need(inv, "inv", (nf, K, K), torch.complex64, dev)
+        if ws.numel() < nb or not Q.is_contiguous() or not inv.is_contiguous():
+            raise ValueError("spectral Cayley: out buffers too small or not contiguous")
+    else:
+        Q = torch.empty((nf, cout, cin), dtype=torch.complex64, device=dev)
+        inv = torch.empty((nf, K, K), dtype=torch.complex64, device=dev)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
     L.check(lib.fiode_spectral_cayley_forward(_stream(dev), ct.byref(cfg), weight.data_ptr(), alpha.data_ptr(),
                                               Q.data_ptr(), inv.data_ptr(), ws.data_ptr(), ws.numel()),
             "fiode_spectral_cayley_forward")

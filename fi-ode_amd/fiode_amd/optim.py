@@ -41,6 +41,40 @@ def _kernel_ok(group, params: List[torch.Tensor]) -> bool:
 class _KernelStepMixin:
     _decoupled = False
 
+    def _done_set(self) -> set:
+        d = self.__dict__.get("_fiode_done")
+        if d is None:
+            d = self.__dict__["_fiode_done"] = set()
+        return d
+
+    @torch.no_grad()
+    def step_params(self, pairs) -> None:
+        """Update only the given (parameter, gradient) pairs now, with their groups' settings and
+        the same kernel as step(); the next step() skips them (it updates the rest and clears the
+        marks).  For updating a layer as soon as its gradient is final (GraphTrainStep's maps
+        computed ahead).  The parameters must be covered by the kernel (ROCm float32, ...)."""
+        done = self._done_set()
+        for group in self.param_groups:
+            ids = {id(p) for p in group["params"]}
+            sel = [(p, g) for p, g in pairs if id(p) in ids]
+            if not sel:
+                continue
+            saved = [p.grad for p, _ in sel]
+            try:
+                for p, g in sel:
+                    p.grad = g
+                params = [p for p, _ in sel]
+                if not _kernel_ok(group, params):
+                    raise RuntimeError("FiodeAdam.step_params: parameters not covered by the kernel")
+                pw, grads, m, v, mx, steps = [], [], [], [], [], []
+                self._init_group({**group, "params": params}, pw, grads, m, v, mx, steps)
+                if not self._launch(group, pw, grads, m, v, steps):
+                    raise RuntimeError("FiodeAdam.step_params: the parameters' step counts differ")
+            finally:
+                for (p, _), g0 in zip(sel, saved):
+                    p.grad = g0
+            done.update(id(p) for p, _ in sel)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -48,39 +82,23 @@ class _KernelStepMixin:
             with torch.enable_grad():
                 loss = closure()
         fallback = []
+        done = self._done_set()
         for group in self.param_groups:
-            params = [p for p in group["params"] if p.grad is not None]
+            params = [p for p in group["params"] if p.grad is not None and id(p) not in done]
+            if not params:
+                continue
             if not _kernel_ok(group, params):
+                if done:
+                    raise RuntimeError("FiodeAdam: torch fallback after step_params is not supported")
                 fallback.append(group)
                 continue
             pw, grads, m, v, mx, steps = [], [], [], [], [], []
-            self._init_group(group, pw, grads, m, v, mx, steps)     # torch's lazy state creation
-            n = len(pw)
-            on_dev = [s.device.type == "cuda" for s in steps]
-            if all(on_dev):
-                torch._foreach_add_(steps, 1)
-                host_step = 0.0
-            else:
-                if torch.cuda.is_current_stream_capturing():
-                    raise RuntimeError("FiodeAdam: capturing the step in a graph needs capturable=True "
-                                       "(device step counts)")
-                if any(on_dev) or len({float(s) for s in steps}) != 1:
-                    fallback.append(group)          # mixed step placement / counts: torch's path
-                    continue
-                for s in steps:
-                    s += 1
-                host_step = float(steps[0])
-            beta1, beta2 = group["betas"]
-            cfg = L.AdamConfig(n, int(bool(group.get("decoupled_weight_decay", self._decoupled))),
-                               int(group["maximize"]), 0, float(group["lr"]), float(beta1), float(beta2),
-                               float(group["eps"]), float(group["weight_decay"]), host_step)
-            arr = ct.c_void_p * n
-            step_ptrs = arr(*[s.data_ptr() for s in steps]) if all(on_dev) else None
-            L.check(L.lib().fiode_adam_step(
-                _stream(pw[0].device), ct.byref(cfg), arr(*[t.data_ptr() for t in pw]),
-                arr(*[t.data_ptr() for t in grads]), arr(*[t.data_ptr() for t in m]),
-                arr(*[t.data_ptr() for t in v]), (ct.c_int64 * n)(*[t.numel() for t in pw]), step_ptrs),
-                "fiode_adam_step")
+            self._init_group({**group, "params": params}, pw, grads, m, v, mx, steps)   # torch's lazy state creation
+            if not self._launch(group, pw, grads, m, v, steps):
+                if done:
+                    raise RuntimeError("FiodeAdam: host step counts after step_params are not supported")
+                fallback.append(group)
+        done.clear()
         if fallback:
             kept = self.param_groups
             self.param_groups = fallback
@@ -89,6 +107,36 @@ class _KernelStepMixin:
             finally:
                 self.param_groups = kept
         return loss
+
+    def _launch(self, group, pw, grads, m, v, steps) -> bool:
+        """The kernel update of one group's tensors; False (nothing done) when the host step counts
+        cannot take it (mixed placement or counts: torch's path)."""
+        n = len(pw)
+        on_dev = [s.device.type == "cuda" for s in steps]
+        if all(on_dev):
+            torch._foreach_add_(steps, 1)
+            host_step = 0.0
+        else:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FiodeAdam: capturing the step in a graph needs capturable=True "
+                                   "(device step counts)")
+            if any(on_dev) or len({float(s) for s in steps}) != 1:
+                return False                    # mixed step placement / counts: torch's path
+            for s in steps:
+                s += 1
+            host_step = float(steps[0])
+        beta1, beta2 = group["betas"]
+        cfg = L.AdamConfig(n, int(bool(group.get("decoupled_weight_decay", self._decoupled))),
+                           int(group["maximize"]), 0, float(group["lr"]), float(beta1), float(beta2),
+                           float(group["eps"]), float(group["weight_decay"]), host_step)
+        arr = ct.c_void_p * n
+        step_ptrs = arr(*[s.data_ptr() for s in steps]) if all(on_dev) else None
+        L.check(L.lib().fiode_adam_step(
+            _stream(pw[0].device), ct.byref(cfg), arr(*[t.data_ptr() for t in pw]),
+            arr(*[t.data_ptr() for t in grads]), arr(*[t.data_ptr() for t in m]),
+            arr(*[t.data_ptr() for t in v]), (ct.c_int64 * n)(*[t.numel() for t in pw]), step_ptrs),
+            "fiode_adam_step")
+        return True
 
 
 class FiodeAdam(_KernelStepMixin, torch.optim.Adam):

@@ -31,7 +31,7 @@ def make(setup):
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
-    return GraphTrainStep(mod, opt, x, y)
+    return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False))
 
 
 def nogroup(m):
@@ -179,6 +179,30 @@ def split_ode(m):
     m.split_ode_wgrad = "ode"
 
 
+def conv_maps_cached(m):
+    """probe only: the conv layers' spectral maps computed once (detached), no map forward or
+    backward in the step -- the upper bound of hiding them entirely"""
+    import types
+    from fiode_amd.cayley import CayleyConv
+
+    def prefetch(self, stream):
+        if self._n is None or not self._alpha_init:
+            return CayleyConv.prefetch(self, stream)
+        if getattr(self, "_cachedQ", None) is None:
+            with torch.no_grad():
+                self._cachedQ = self.spectral_weight(self._n, self.weight.device).detach().clone()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pre = (self._cachedQ, ev)
+    for c in m.modules():
+        if isinstance(c, CayleyConv):
+            c.prefetch = types.MethodType(prefetch, c)
+
+
+def no_ahead(m):
+    m._no_ahead = True
+
+
 def torch_adam(m):
     m._torch_adam = True
 
@@ -187,7 +211,7 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "no_ahead": no_ahead, "conv_maps_cached": conv_maps_cached, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
