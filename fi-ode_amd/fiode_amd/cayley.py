@@ -241,6 +241,30 @@ class _DenseCayleyFn(torch.autograd.Function):
                                    lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
 
 
+class _DenseCayleyStoredFn(torch.autograd.Function):
+    """The Q of a CayleyLinear whose dense map was computed AHEAD into fixed buffers (CayleyLinear
+    pipeline_on / refresh_map; see _SpectralCayleyStoredFn): forward hands out the stored Q,
+    backward is _DenseCayleyFn's from the stored norm and inverse, then ``store["on_grads"]``."""
+
+    @staticmethod
+    def forward(ctx, W, alpha, store: dict):
+        ctx.save_for_backward(W, alpha)
+        ctx.store = store
+        return store["Q"].detach().reshape(W.shape)
+
+    @staticmethod
+    def backward(ctx, gQ):
+        W, alpha = ctx.saved_tensors
+        st = ctx.store
+        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
+        al = alpha.detach().reshape(-1).contiguous().float()
+        gW, ga = _dense_backward(Wb, al, st["nrm"], st["inv"], gQ, W.shape, alpha.shape)
+        hook = st.get("on_grads")
+        if hook is not None:
+            hook(gW, ga)
+        return gW, ga, None
+
+
 class _DenseCayleyGroupFn(torch.autograd.Function):
     """Several dense Cayley maps with the same k = min(cout, cin) (the backbone's 4096 -> 512 and
     512 -> 512 CayleyLinears) in one node: their systems are stacked and inverted by ONE batched
@@ -450,6 +474,7 @@ class CayleyLinear(nn.Linear):
         self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
         self._Q = None
         self._pre = None
+        self._store = None              # map computed ahead (pipeline_on), else None
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -464,9 +489,52 @@ class CayleyLinear(nn.Linear):
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
         the layers before it); the next training forward joins it."""
+        if self._store is not None:
+            return
         self._pre = _prefetch(stream, self.effective_weight)
 
+    # ---- map computed ahead (GraphTrainStep; see CayleyConv.pipeline_on) ------------------------
+    def _dense_map(self):
+        st, M = _dense_prep(self.weight, self.alpha)
+        inv = _block_inverse(M)
+        return _dense_finish(st, inv), st["nrm"], inv
+
+    def pipeline_on(self) -> bool:
+        """Dense (k > 16) maps of ROCm float32 weights only; returns whether the layer is pipelined."""
+        W = self.weight
+        if not (W.is_cuda and W.dtype == torch.float32 and W.dim() == 2 and DENSE_FUSED
+                and not (SMALL_FUSED and _small_ok(W))):
+            return False
+        with torch.no_grad():
+            Q, nrm, inv = self._dense_map()
+        self._store = {"Q": Q, "nrm": nrm, "inv": inv, "stream": torch.cuda.Stream(W.device)}
+        return True
+
+    def pipeline_off(self) -> None:
+        self._store = None
+
+    def refresh_map(self) -> None:
+        """Recompute the stored map from the current parameters (the step-start kernels, then
+        copies into the fixed buffers the captured forward reads)."""
+        st = self._store
+        with torch.no_grad():
+            Q, nrm, inv = self._dense_map()
+            st["Q"].copy_(Q)
+            st["nrm"].copy_(nrm)
+            st["inv"].copy_(inv)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        st = self._store
+        if st is not None and self.training and torch.is_grad_enabled():
+            side = st["stream"]
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                Q = _DenseCayleyStoredFn.apply(self.weight, self.alpha, st)
+            main.wait_stream(side)
+            self._pre = None
+            self._Q = Q.detach()
+            return F.linear(x, Q, self.bias)
         if self._pre is not None and self.training:
             Q = _take(self._pre)
             self._pre = None

@@ -29,7 +29,8 @@ import torch
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
-                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True):
+                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
+                 maps_ahead_linear: bool = False):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
@@ -70,6 +71,7 @@ class GraphTrainStep:
 
         self.single = world == 1
         self.piped, self.early = [], False
+        self.maps_ahead_linear = maps_ahead_linear
         if maps_ahead:
             self._maps_ahead_on()
         self.g_fb = torch.cuda.CUDAGraph()
@@ -100,12 +102,17 @@ class GraphTrainStep:
     # the backward runs; on N ranks (gradients final only after the all-reduce) after the optimizer
     # step.  The maps are the same kernels on the same parameters as at the start of the next step,
     # so the results are unchanged.  Parameters changed outside the replays: call refresh_maps().
+    # maps_ahead_linear: the same for the dense CayleyLinear maps (bit-identical too, but the
+    # executor places their update + 512 x 512 inverse chain on the backbone backward's queue:
+    # 1.684 -> 1.732 ms per step in the interleaved A/B; off).
     def _maps_ahead_on(self):
-        from .cayley import CayleyConv
+        from .cayley import CayleyConv, CayleyLinear
         from .optim import _KernelStepMixin
         self.early = self.single and isinstance(self.opt, _KernelStepMixin)
-        for c in self.module.modules():
-            if isinstance(c, CayleyConv) and c.pipeline_on():
+        kinds = (CayleyConv, CayleyLinear) if self.maps_ahead_linear else (CayleyConv,)
+        root = getattr(self.module, "init_coordinates", self.module)       # the backbone's layers
+        for c in root.modules():
+            if isinstance(c, kinds) and c.pipeline_on():
                 self.piped.append(c)
                 if self.early:
                     c._store["on_grads"] = (lambda gw, ga, c=c: self._update_layer(c, gw, ga))
