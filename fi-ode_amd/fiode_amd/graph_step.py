@@ -30,12 +30,15 @@ import torch
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
-                 maps_ahead_linear: bool = False):
+                 maps_ahead_linear: bool = False, refresh_after_backward: bool = False):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
         self.module, self.opt, self.reducer, self.world, self.act = module, optimizer, reducer, world, act
         self.check_every, self.n_replays = int(check_every), 0
+        self.piped, self.early = [], False
+        self.maps_ahead_linear = maps_ahead_linear
+        self.refresh_after_backward = refresh_after_backward
         dyn = module.dyn_fun
         if module.global_step < dyn.kappa_length:
             raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
@@ -70,8 +73,6 @@ class GraphTrainStep:
         torch.cuda.synchronize(dev)
 
         self.single = world == 1
-        self.piped, self.early = [], False
-        self.maps_ahead_linear = maps_ahead_linear
         if maps_ahead:
             self._maps_ahead_on()
         self.g_fb = torch.cuda.CUDAGraph()
@@ -119,7 +120,18 @@ class GraphTrainStep:
 
     def _update_layer(self, c, gw, ga):
         self.opt.step_params([(c.weight, gw), (c.alpha, ga)])
-        c.refresh_map()
+        if not self.refresh_after_backward:
+            c.refresh_map()
+
+    def _refresh_on_layer_streams(self):
+        """refresh_after_backward: each layer's map recomputed on its own stream (ordered after its
+        early update there), captured after the whole backward."""
+        main = torch.cuda.current_stream()
+        for c in self.piped:
+            st = c._store["stream"]
+            with torch.cuda.stream(st):
+                c.refresh_map()
+            main.wait_stream(st)
 
     def _refresh_late(self):
         if not self.early:
@@ -177,6 +189,8 @@ class GraphTrainStep:
             p.grad = None
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         loss.backward()
+        if getattr(self, "early", False) and self.refresh_after_backward and self.piped:
+            self._refresh_on_layer_streams()
         if self.reducer is not None and self.world > 1:
             self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)

@@ -32,7 +32,8 @@ def make(setup):
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
     return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False),
-                          maps_ahead_linear=getattr(mod, "_ahead_lin", False))
+                          maps_ahead_linear=getattr(mod, "_ahead_lin", False),
+                          refresh_after_backward=getattr(mod, "_late_refresh", False))
 
 
 def nogroup(m):
@@ -208,6 +209,10 @@ def ahead_lin(m):
     m._ahead_lin = True
 
 
+def late_refresh(m):
+    m._late_refresh = True
+
+
 def seed1000(m):
     m.seed = 1000
 
@@ -220,7 +225,7 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "ahead_lin": ahead_lin, "seed1000": seed1000, "lin0": sched(lin=[0, 0, 0], dyn=0), "lin1": sched(lin=[1, 1, 1], dyn=1), "lin2": sched(lin=[2, 2, 2], dyn=2), "at_start": at_start, "no_ahead": no_ahead, "conv_maps_cached": conv_maps_cached, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "ahead_lin": ahead_lin, "seed1000": seed1000, "late_refresh": late_refresh, "lin0": sched(lin=[0, 0, 0], dyn=0), "lin1": sched(lin=[1, 1, 1], dyn=1), "lin2": sched(lin=[2, 2, 2], dyn=2), "at_start": at_start, "no_ahead": no_ahead, "conv_maps_cached": conv_maps_cached, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
