@@ -102,7 +102,8 @@ constexpr int PB = 64;
 // Batched over matrices m = blockIdx.y (pad, pivot) / blockIdx.z (update): matrix m's buffers sit
 // at + m * wstride floats of the workspace, its input / output at + m * n * n.
 __global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* __restrict__ in, float* __restrict__ out,
-                                                   int64_t wstride) {
+                                                   int64_t wstride, const int32_t* __restrict__ skip) {
+  if (skip && *skip) return;                  // (uniform: the caller's inverse is already exact)
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)np * np) return;
   const int64_t m = blockIdx.y;
@@ -114,7 +115,9 @@ __global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* _
 
 typedef fiode_gjb::GJB<PB, 8> PivotGJ;
 __global__ void __launch_bounds__(PivotGJ::NT) k_panel_pivot(int np, int k0, const float* __restrict__ X,
-                                                            float* __restrict__ P, int64_t wstride) {
+                                                            float* __restrict__ P, int64_t wstride,
+                                                            const int32_t* __restrict__ skip) {
+  if (skip && *skip) return;
   extern __shared__ __attribute__((aligned(16))) char piv_smem[];
   PivotGJ::Smem& sm = *reinterpret_cast<PivotGJ::Smem*>(piv_smem);
   const int64_t m = blockIdx.x;
@@ -172,7 +175,8 @@ static_assert(sizeof(UpdGJ::Smem) <= 3 * PB * LDT * sizeof(float), "pivot scratc
 __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
                                                       const float* __restrict__ P, float* __restrict__ Y,
                                                       float* __restrict__ final_out, int n, int64_t wstride,
-                                                      float* __restrict__ P_next) {
+                                                      float* __restrict__ P_next, const int32_t* __restrict__ skip) {
+  if (skip && *skip) return;
   __shared__ __attribute__((aligned(16))) float lds[3][PB][LDT];
   float (*sA)[LDT] = lds[0];    // P, or X_iK (row-major A operands)
   float (*sX)[LDT] = lds[1];    // X_iK for the second product
@@ -264,8 +268,8 @@ extern "C" size_t fiode_block_inverse_workspace_bytes(int32_t n) {
   return (2 * np * np + 2 * (size_t)PB * PB) * sizeof(float);   // ping-pong matrices + two pivot inverses
 }
 
-extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
-                                           void* workspace, size_t workspace_bytes) {
+extern "C" int fiode_block_inverse_cond(void* stream, int32_t batch, int32_t n, const float* in, float* out,
+                                        void* workspace, size_t workspace_bytes, const int32_t* skip) {
   if (batch < 1 || batch > 65535 || n < 1 || n > FIODE_BLOCK_INV_MAX_N || !in || !out || !workspace)
     return FIODE_EINVAL;
   if (workspace_bytes < (size_t)batch * fiode_block_inverse_workspace_bytes(n)) return FIODE_EWORKSPACE;
@@ -276,21 +280,26 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
   float* B = A + (size_t)np * np;
   float* Pb[2] = {B + (size_t)np * np, B + (size_t)np * np + (size_t)PB * PB};
   hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256), (unsigned)batch), dim3(256), 0, st,
-                     n, np, in, A, wstride);
+                     n, np, in, A, wstride, skip);
   // the first pivot block on its own; every later one is inverted by the previous update (look-ahead)
   hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, 0, A,
-                     Pb[0], wstride);
+                     Pb[0], wstride, skip);
   for (int kb = 0; kb < nb; ++kb) {
     const int k0 = kb * PB;
     const bool last = kb == nb - 1;
     hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, Pb[kb & 1], B,
-                       last ? out : nullptr, n, wstride, last ? nullptr : Pb[(kb + 1) & 1]);
+                       last ? out : nullptr, n, wstride, last ? nullptr : Pb[(kb + 1) & 1], skip);
     float* t = A;
     A = B;
     B = t;
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
+                                           void* workspace, size_t workspace_bytes) {
+  return fiode_block_inverse_cond(stream, batch, n, in, out, workspace, workspace_bytes, nullptr);
 }
 
 extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,

@@ -147,6 +147,7 @@ def _load():
         "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_block_inverse": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_block_inverse_batched": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_block_inverse_cond": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, _vp, ct.c_size_t, _vp]),
         "fiode_normalize_hwcb": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp]),
         "fiode_ode_nll": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, _vp]),
         "fiode_ode_loss_mix": (ct.c_int, [_vp, ct.c_int32, _vp, _vp, _vp, ct.c_float, _vp, _vp, _vp]),

@@ -51,6 +51,52 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
     return X
 
 
+# Warm-started inverse of a training step's dense Cayley system.  The weights move a little per
+# optimizer step, so the previous step's inverse X is close to M^-1: NEWTON_ITERS Newton-Schulz
+# steps X <- 2X - X (M X) (two GEMMs and one lerp each, quadratic convergence) reach float32
+# accuracy where the 64-panel elimination is a ~150 us latency chain.  The bound ||I - M X||^2 of
+# the final residual (induced inf-norm of the last step's residual) is checked on the device;
+# above NEWTON_TOL the exact elimination runs after all (fiode_block_inverse_cond skips it
+# otherwise) -- no host sync, safe for any step size.
+WARM_INVERSE = True
+NEWTON_ITERS = 2
+NEWTON_TOL = 1e-5
+
+
+def _warm_inverse(M: torch.Tensor, cache: dict, key=None) -> torch.Tensor:
+    """``key``: identifies the parameters M was formed from (their version counters): a second
+    evaluation of the same system within a step (e.g. the reference-order second backbone pass)
+    returns the first one's inverse, bit for bit."""
+    from . import ops
+    n = M.shape[-1]
+    M2 = M.reshape(n, n)
+    X = cache.get("X")
+    if X is None or X.shape != M2.shape or X.device != M2.device:
+        inv = ops.block_inverse(M2)
+        cache["X"] = inv.clone()
+        cache["eye"] = torch.eye(n, dtype=M.dtype, device=M.device)
+        cache["skip"] = torch.zeros(1, dtype=torch.int32, device=M.device)
+        cache["skipb"] = torch.zeros((), dtype=torch.bool, device=M.device)
+        cache["key"] = key
+        return inv.reshape(M.shape)
+    if key is not None and cache.get("key") == key:
+        return X.clone().reshape(M.shape)
+    cache["key"] = key
+    eye = cache["eye"]
+    res = None
+    for it in range(NEWTON_ITERS):
+        Y = torch.matmul(M2, X)                          # M X = I - R
+        if it == NEWTON_ITERS - 1:
+            # R_{k+1} = R_k^2, so ||R_final|| <= ||R||^2 in the induced inf-norm (max row sum)
+            res = torch.linalg.matrix_norm(Y - eye, ord=float("inf"))
+        X = torch.lerp(torch.matmul(X, Y), X, 2.0)       # X (2I - M X) = 2X - X M X
+    torch.le(res * res, NEWTON_TOL, out=cache["skipb"])
+    cache["skip"].copy_(cache["skipb"])
+    ops.block_inverse(M2, out=X, skip=cache["skip"])
+    cache["X"].copy_(X)
+    return X.reshape(M.shape)
+
+
 class _CayleyInverse(torch.autograd.Function):
     """(I + A)^-1 with torch.linalg.inv's gradient, d(M^-1) = -M^-H dM M^-H -- computed by the
     fiode_batched_inverse kernel instead of getrf/getrs (no pivot search, no info sync)."""
@@ -225,9 +271,13 @@ class _DenseCayleyFn(torch.autograd.Function):
     every elementwise stage between them one HIP kernel (fiode_dense_cayley_*; dense.hip)."""
 
     @staticmethod
-    def forward(ctx, W, alpha):
+    def forward(ctx, W, alpha, inv_cache=None):
         st, M = _dense_prep(W, alpha)
-        inv = _block_inverse(M)
+        if inv_cache is not None and M.shape[0] == 1 and M.shape[-1] > 64:
+            key = None if STEP_TOKEN is None else (STEP_TOKEN, W.data_ptr(), alpha.data_ptr())
+            inv = _warm_inverse(M, inv_cache, key=key)
+        else:
+            inv = _block_inverse(M)
         Q = _dense_finish(st, inv)
         ctx.save_for_backward(st["Wb"], st["al"], st["nrm"], inv)
         ctx.shapes = (W.shape, alpha.shape)
@@ -238,7 +288,7 @@ class _DenseCayleyFn(torch.autograd.Function):
     def backward(ctx, gQ):
         Wb, al, nrm, inv = ctx.saved_tensors
         return _run_on_step_stream(DENSE_BWD_ON_MAIN, ctx.step_stream,
-                                   lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
+                                   lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes)) + (None,)
 
 
 class _DenseCayleyStoredFn(torch.autograd.Function):
@@ -358,7 +408,8 @@ def _small_ok(W: torch.Tensor) -> bool:
     return k <= L.FIODE_SMALL_CAYLEY_MAX_K and R * k <= L.FIODE_SMALL_CAYLEY_MAX_RK
 
 
-def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False) -> torch.Tensor:
+def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False,
+                  inv_cache: Optional[dict] = None) -> torch.Tensor:
     """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293).
     Real matrices on ROCm (one matrix, or a batch with per-matrix norms) take one kernel per
     direction when k = min(cout, cin) <= 16 (_SmallCayleyFn), else the fused stages of
@@ -366,7 +417,7 @@ def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False
     if W.is_cuda and W.dtype == torch.float32 and (W.dim() == 2 or per_matrix) and DENSE_FUSED:
         if SMALL_FUSED and _small_ok(W):
             return _SmallCayleyFn.apply(W, alpha)
-        return _DenseCayleyFn.apply(W, alpha)
+        return _DenseCayleyFn.apply(W, alpha, inv_cache)
     return _CayleyScaledFn.apply(W, alpha, per_matrix)
 
 
@@ -411,20 +462,29 @@ SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 
 
+STEP_TOKEN: Optional[int] = None
+_STEP_COUNT = 0
+
+
 class step_stream_scope:
-    """Context manager: STEP_STREAM = ``stream`` inside, the previous value restored on exit."""
+    """Context manager: STEP_STREAM = ``stream`` inside, the previous value restored on exit; also
+    a fresh STEP_TOKEN (one training forward), under which a dense map evaluated twice reuses its
+    first warm-started inverse (_warm_inverse ``key``)."""
 
     def __init__(self, stream):
         self.stream = stream
 
     def __enter__(self):
-        global STEP_STREAM
+        global STEP_STREAM, STEP_TOKEN, _STEP_COUNT
+        _STEP_COUNT += 1
         self.prev, STEP_STREAM = STEP_STREAM, self.stream
+        self.prev_token, STEP_TOKEN = STEP_TOKEN, _STEP_COUNT
         return self
 
     def __exit__(self, *exc):
-        global STEP_STREAM
+        global STEP_STREAM, STEP_TOKEN
         STEP_STREAM = self.prev
+        STEP_TOKEN = self.prev_token
         return False
 
 
@@ -475,6 +535,7 @@ class CayleyLinear(nn.Linear):
         self._Q = None
         self._pre = None
         self._store = None              # map computed ahead (pipeline_on), else None
+        self._inv_cache = {}            # previous training step's inverse (_warm_inverse)
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -484,7 +545,9 @@ class CayleyLinear(nn.Linear):
         self._Q = None
 
     def effective_weight(self) -> torch.Tensor:
-        return cayley_scaled(self.weight, self.alpha)
+        # training: the inverse is warm-started from the previous step's (_warm_inverse)
+        warm = self._inv_cache if (self.training and WARM_INVERSE and torch.is_grad_enabled()) else None
+        return cayley_scaled(self.weight, self.alpha, inv_cache=warm)
 
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
@@ -496,7 +559,8 @@ class CayleyLinear(nn.Linear):
     # ---- map computed ahead (GraphTrainStep; see CayleyConv.pipeline_on) ------------------------
     def _dense_map(self):
         st, M = _dense_prep(self.weight, self.alpha)
-        inv = _block_inverse(M)
+        # the same warm start as the step-start map (no key: the parameters just changed)
+        inv = _warm_inverse(M, self._inv_cache) if WARM_INVERSE else _block_inverse(M)
         return _dense_finish(st, inv), st["nrm"], inv
 
     def pipeline_on(self) -> bool:

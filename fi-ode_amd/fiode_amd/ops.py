@@ -445,10 +445,12 @@ def batched_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torc
     return out
 
 
-def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  skip: Optional[torch.Tensor] = None) -> torch.Tensor:
     """(n, n) or (b, n, n) float32 -> inverse by 64-wide panel block Gauss-Jordan on the device
     (fiode_block_inverse[_batched]: one launch sequence for the whole batch).  Valid for matrices
-    with positive-definite symmetric part."""
+    with positive-definite symmetric part.  ``skip``: device int32 scalar; nonzero = the launches
+    return at once and ``out`` is left as it is (fiode_block_inverse_cond)."""
     if (M.device.type != "cuda" or M.dtype != torch.float32 or M.dim() not in (2, 3)
             or M.shape[-1] != M.shape[-2]):
         raise ValueError(f"block_inverse: square float32 ROCm matrix expected, got {tuple(M.shape)} {M.dtype} "
@@ -461,8 +463,10 @@ def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.
     lib = L.lib()
     nb = lib.fiode_block_inverse_workspace_bytes(n) * b
     ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}")
-    L.check(lib.fiode_block_inverse_batched(_stream(M.device), b, n, M.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                                            ws.numel()), "fiode_block_inverse_batched")
+    if skip is not None:
+        skip = _need(skip.reshape(1), "skip", (1,), torch.int32, M.device)
+    L.check(lib.fiode_block_inverse_cond(_stream(M.device), b, n, M.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                         ws.numel(), _ptr(skip)), "fiode_block_inverse_cond")
     return out
 
 

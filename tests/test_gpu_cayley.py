@@ -459,3 +459,36 @@ def test_normalize_hwcb_matches_torch(B, C, H, W, with_std):
     ref = (x - n.mu) / n.std if with_std else x - n.mu
     assert torch.equal(y, ref)
     assert y.permute(2, 3, 1, 0).is_contiguous()
+
+
+def test_warm_inverse_converges_and_falls_back():
+    """_warm_inverse (training-step dense maps): from the previous step's inverse, Newton-Schulz
+    refinement matches the exact elimination to float32 accuracy and skips it on the device; from a
+    useless start (zeros: residual 1) the exact elimination runs (fiode_block_inverse_cond)."""
+    from fiode_amd import cayley as CY, ops
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(11)
+    W = (torch.randn(512, 512, generator=g) / 512 ** 0.5).to(dev)
+    alpha = torch.tensor([W.norm().item()], device=dev)
+    st, M = CY._dense_prep(W, alpha)
+    exact = ops.block_inverse(M.reshape(512, 512)).clone()
+    cache = {}
+    first = CY._warm_inverse(M, cache)                   # no previous inverse: exact
+    torch.testing.assert_close(first.reshape(512, 512), exact, rtol=0, atol=0)
+    # a nearby system (the weights after a small step)
+    W2 = W + 1e-3 * (torch.randn(512, 512, generator=g) / 512 ** 0.5).to(dev)
+    st2, M2 = CY._dense_prep(W2, alpha)
+    exact2 = ops.block_inverse(M2.reshape(512, 512)).clone()
+    warm = CY._warm_inverse(M2, cache).reshape(512, 512)
+    torch.cuda.synchronize()
+    assert int(cache["skip"]) == 1                        # converged: the elimination was skipped
+    scale = float(exact2.abs().max())
+    assert float((warm - exact2).abs().max()) / scale < 2e-5
+    eye = torch.eye(512, device=dev)
+    assert float(torch.linalg.matrix_norm(eye - M2.reshape(512, 512) @ warm, ord=float("inf"))) <= 1e-4
+    # useless start: falls back to the exact elimination, bit for bit
+    cache["X"].zero_()
+    fb = CY._warm_inverse(M2, cache).reshape(512, 512)
+    torch.cuda.synchronize()
+    assert int(cache["skip"]) == 0
+    assert torch.equal(fb, exact2)

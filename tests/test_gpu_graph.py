@@ -6,6 +6,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+def _copy_inv_cache(src, dst):
+    """The dense Cayley maps' warm-start inverses (cayley._warm_inverse) are step state too: the twin
+    that replays a step eagerly starts from the same ones."""
+    from fiode_amd.cayley import CayleyLinear
+    for a, b in zip([m for m in src.modules() if isinstance(m, CayleyLinear)],
+                    [m for m in dst.modules() if isinstance(m, CayleyLinear)]):
+        b._inv_cache = {k: v.detach().clone() for k, v in a._inv_cache.items() if torch.is_tensor(v)}
+
+
 def _dev():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
@@ -28,6 +37,7 @@ def test_graph_replay_matches_eager_step(train_ode):
     twin.load_state_dict(mod.state_dict())
     twin.rng_counter = mod.rng_counter.clone()
     twin.seed = mod.seed
+    _copy_inv_cache(mod, twin)
     c0 = int(mod.rng_counter)
     loss = gs.step()
     torch.cuda.synchronize()
@@ -75,6 +85,7 @@ def test_graph_warmup_leaves_no_updates():
     twin.load_state_dict(before)
     twin.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
     twin.seed = mod.seed
+    _copy_inv_cache(mod, twin)
     topt = twin.configure_optimizers(capturable=True)[0][0]
     gs.step()
     topt.zero_grad(set_to_none=True)

@@ -65,15 +65,15 @@ def spin_before(owner, name, once_per_step=True):
 
 variants = [
     ("baseline", None),
-    ("conv0_map_fwd (side stream 0)", (CY._SpectralCayleyFn, "forward")),
     ("linear_map_fwd (side streams 1-2)", (CY.CayleyLinear, "effective_weight")),
     ("dyn_map_fwd (side stream 3)", (__import__("fiode_amd.dynamics", fromlist=["x"]), "cayley_scaled")),
     ("odetrain_fwd (ode stream)", (ops, "odetrain_forward")),
     ("odetrain_bwd", (ops, "odetrain_backward")),
     ("lyap_step (main)", (ops, "lyap_step")),
-    ("sconv_bwd_rfft2", (ops, "sconv_rfft2")),
-    ("spectral_map_bwd", (ops, "spectral_cayley_backward")),
-    ("adam (main, end)", (torch.optim.Adam, "step")),
+    ("sconv_bwd_rfft2 (backbone bwd)", (ops, "sconv_rfft2")),
+    ("conv_map_bwd (layer streams)", (ops, "spectral_cayley_backward")),
+    ("conv_map_refresh (layer streams, x4)", (CY.CayleyConv, "refresh_map")),
+    ("dense_map_bwd (step stream, tail)", (CY, "_dense_backward")),
 ]
 if len(sys.argv) > 1 and sys.argv[1] == "lyap_curve":
     variants = [("baseline", None)]
