@@ -60,6 +60,7 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
 # otherwise) -- no host sync, safe for any step size.
 WARM_INVERSE = True
 NEWTON_ITERS = 2
+WARM_WIDE = True           # also the wide 4096 -> 512 map (its system converges more slowly)
 NEWTON_TOL = 1e-5
 
 
@@ -273,7 +274,8 @@ class _DenseCayleyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W, alpha, inv_cache=None):
         st, M = _dense_prep(W, alpha)
-        if inv_cache is not None and M.shape[0] == 1 and M.shape[-1] > 64:
+        if (inv_cache is not None and M.shape[0] == 1 and M.shape[-1] > 64
+                and (WARM_WIDE or W.shape[-1] == W.shape[-2])):
             key = None if STEP_TOKEN is None else (STEP_TOKEN, W.data_ptr(), alpha.data_ptr())
             inv = _warm_inverse(M, inv_cache, key=key)
         else:
