@@ -57,8 +57,11 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
 # accuracy where the 64-panel elimination is a ~150 us latency chain.  The bound ||I - M X||^2 of
 # the final residual (induced inf-norm of the last step's residual) is checked on the device;
 # above NEWTON_TOL the exact elimination runs after all (fiode_block_inverse_cond skips it
-# otherwise) -- no host sync, safe for any step size.
-WARM_INVERSE = True
+# otherwise) -- no host sync, safe for any step size.  Opt-in: in steady-state training it saves
+# ~40 us per step (1.688 -> 1.646 ms after ~50 replays, tools/ab_step.py), but while Adam's first
+# bias-corrected steps move every weight by ~lr the wide map's refinement fails and the fallback
+# pays both (the bench's 20 steps after 5 warm-ups of a fresh optimizer: 1.67 -> 1.76 ms).
+WARM_INVERSE = False
 NEWTON_ITERS = 2
 WARM_WIDE = True           # also the wide 4096 -> 512 map (its system converges more slowly)
 NEWTON_TOL = 1e-5
