@@ -785,13 +785,28 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
                                        const fiode_dyn_weights* w, const float* x_feat, const float* g_y,
                                        fiode_lyap_grads* grads, float* dbg_gft, void* workspace,
                                        size_t workspace_bytes) {
-  if (!grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
-      !grads->b3 || !grads->x_feat)
-    return FIODE_EINVAL;
-  int rc = fiode_odetrain_backward_x(stream, cfg, dyn, w, x_feat, g_y, grads->x_feat, nullptr, nullptr, dbg_gft,
-                                 workspace, workspace_bytes);
+  // the adjoint sweep, then the weight-gradient chain whose last kernel also forms dL/dx_feat (from
+  // the per-image g_u it reduces): one launch fewer than _x + _weights (k_ot_gx), so the x-gradient
+  // may differ from fiode_odetrain_backward_x's in the last bits (summation order of g_u)
+  OTArgs a{};
+  int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
-  return fiode_odetrain_backward_weights(stream, cfg, dyn, w, x_feat, grads, workspace, workspace_bytes);
+  if (!g_y || !grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 ||
+      !grads->Q3 || !grads->b3 || !grads->x_feat)
+    return FIODE_EINVAL;
+  a.g_y = g_y; a.dbg_gft = dbg_gft;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t lds = sizeof(OtBwdShared);
+  if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(k_ot_bwd<false>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
+  FIODE_HIP_CHECK(hipGetLastError());
+  const OtLayout L = ot_layout(a.B, a.E);
+  fiode_internal::WgradIO io{};
+  io.B = a.B; io.S = a.E; io.x_feat = x_feat; io.Qx = w->Qx; io.h = a.hs; io.a1 = a.a1; io.a2 = a.a2;
+  io.gz2 = a.gz2; io.gz1 = a.gz1; io.gft = a.gft;
+  io.workspace = static_cast<char*>(workspace) + L.wg;
+  io.grads = *grads;
+  return fiode_internal::launch_wgrad(st, io);
 }
 
 // ---- the train_ode loss term: F.nll_loss(torch.log(y_hat), y) (pl_modules.py:494-497) --------

@@ -233,7 +233,8 @@ FIODE_API int fiode_odetrain_backward(void* stream, const fiode_odetrain_config*
  *   _x:       the adjoint sweep (k_ot_bwd) and gx [B][X] = dL/dx_feat, plus gx_add [B][X] times
  *             gx_add_scale[0] (device scalar) when gx_add is given;
  *   _weights: the weight gradients (grads->x_feat ignored); after _x on the same workspace.
- * fiode_odetrain_backward = _x then _weights (same results). */
+ * fiode_odetrain_backward = the same work with dL/dx_feat formed inside the weight-gradient chain
+ * (one launch fewer; its x-gradient may differ from _x's in the last bits: g_u summation order). */
 FIODE_API int fiode_odetrain_backward_x(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
                                         const fiode_dyn_weights* w, const float* x_feat, const float* g_y, float* gx,
                                         const float* gx_add, const float* gx_add_scale, float* dbg_gft,

@@ -149,11 +149,20 @@ def test_fused_loss_node_equals_three_nodes(reuse):
         out[variant] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
                         {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
     lb, ob, gb = out["three"]
-    for variant in ("fused", "split"):
-        la, oa, ga = out[variant]
-        assert torch.equal(la, lb) and oa == ob, variant
-        for n in ga:
-            assert torch.equal(ga[n], gb[n]), (variant, n)
+    la, oa, ga = out["fused"]
+    assert torch.equal(la, lb) and oa == ob
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+    # the split node's dL/dx_feat comes from k_ot_gx (fiode_odetrain_backward_x) instead of the
+    # weight-gradient chain: the same sum in another order, so the backbone's gradients agree to
+    # float32 rounding (the dynamics' weight gradients are identical)
+    la, oa, ga = out["split"]
+    assert torch.equal(la, lb) and oa == ob
+    for n in ga:
+        if n.startswith("model.dyn_fun."):
+            assert torch.equal(ga[n], gb[n]), n
+        else:
+            torch.testing.assert_close(ga[n], gb[n], rtol=1e-4, atol=1e-6 * float(gb[n].abs().max()) + 1e-12)
 
 
 @pytest.mark.parametrize("B", [1, 128, 300])
