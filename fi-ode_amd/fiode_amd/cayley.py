@@ -406,6 +406,48 @@ class _SmallCayleyFn(torch.autograd.Function):
         return gW.reshape(wshape), ga.reshape(ashape)
 
 
+def _small_forward_into(W: torch.Tensor, alpha: torch.Tensor, Q: torch.Tensor, inv: torch.Tensor,
+                        nrm: torch.Tensor) -> None:
+    """fiode_small_cayley_forward of one [cout, cin] matrix into given buffers."""
+    from . import ops, _lib as L
+    cout, cin = W.shape[-2], W.shape[-1]
+    L.check(L.lib().fiode_small_cayley_forward(ops._stream(W.device), 1, cout, cin, W.detach().contiguous().data_ptr(),
+                                               alpha.detach().reshape(-1).contiguous().float().data_ptr(),
+                                               Q.data_ptr(), inv.data_ptr(), nrm.data_ptr()),
+            "fiode_small_cayley_forward")
+
+
+class _SmallCayleyStoredFn(torch.autograd.Function):
+    """The Q of a small (k <= 16) CayleyLinear map computed AHEAD into fixed buffers (see
+    _SpectralCayleyStoredFn): forward hands out the stored Q, backward is _SmallCayleyFn's from the
+    stored norm and inverse, then ``store["on_grads"]``."""
+
+    @staticmethod
+    def forward(ctx, W, alpha, store: dict):
+        ctx.save_for_backward(W, alpha)
+        ctx.store = store
+        return store["Q"].detach().reshape(W.shape)
+
+    @staticmethod
+    def backward(ctx, gQ):
+        from . import ops, _lib as L
+        W, alpha = ctx.saved_tensors
+        st = ctx.store
+        cout, cin = W.shape[-2], W.shape[-1]
+        gQb = gQ.reshape(cout, cin).contiguous().float()
+        gW = torch.empty_like(W)
+        ga = torch.empty(1, dtype=torch.float32, device=W.device)
+        L.check(L.lib().fiode_small_cayley_backward(
+            ops._stream(W.device), 1, cout, cin, W.detach().contiguous().data_ptr(),
+            alpha.detach().reshape(-1).contiguous().float().data_ptr(), st["nrm"].data_ptr(), st["inv"].data_ptr(),
+            gQb.data_ptr(), gW.data_ptr(), ga.data_ptr()), "fiode_small_cayley_backward")
+        ga = ga.reshape(alpha.shape)
+        hook = st.get("on_grads")
+        if hook is not None:
+            hook(gW, ga)
+        return gW, ga, None
+
+
 def _small_ok(W: torch.Tensor) -> bool:
     from . import _lib as L
     cout, cin = W.shape[-2], W.shape[-1]
@@ -568,25 +610,38 @@ class CayleyLinear(nn.Linear):
         inv = _warm_inverse(M, self._inv_cache) if WARM_INVERSE else _block_inverse(M)
         return _dense_finish(st, inv), st["nrm"], inv
 
-    def pipeline_on(self) -> bool:
-        """Dense (k > 16) maps of ROCm float32 weights only; returns whether the layer is pipelined."""
+    def pipeline_on(self, kinds=("dense", "small")) -> bool:
+        """ROCm float32 weights with the fused dense or small map (``kinds``); returns whether
+        the layer is pipelined."""
         W = self.weight
-        if not (W.is_cuda and W.dtype == torch.float32 and W.dim() == 2 and DENSE_FUSED
-                and not (SMALL_FUSED and _small_ok(W))):
+        if not (W.is_cuda and W.dtype == torch.float32 and W.dim() == 2 and DENSE_FUSED):
+            return False
+        small = SMALL_FUSED and _small_ok(W)
+        if ("small" if small else "dense") not in kinds:
             return False
         with torch.no_grad():
-            Q, nrm, inv = self._dense_map()
-        self._store = {"Q": Q, "nrm": nrm, "inv": inv, "stream": torch.cuda.Stream(W.device)}
+            if small:
+                k = min(W.shape)
+                Q = torch.empty_like(W)
+                inv = torch.empty((1, k, k), dtype=torch.float32, device=W.device)
+                nrm = torch.empty(1, dtype=torch.float32, device=W.device)
+                _small_forward_into(W, self.alpha, Q, inv, nrm)
+            else:
+                Q, nrm, inv = self._dense_map()
+        self._store = {"Q": Q, "nrm": nrm, "inv": inv, "small": small, "stream": torch.cuda.Stream(W.device)}
         return True
 
     def pipeline_off(self) -> None:
         self._store = None
 
     def refresh_map(self) -> None:
-        """Recompute the stored map from the current parameters (the step-start kernels, then
-        copies into the fixed buffers the captured forward reads)."""
+        """Recompute the stored map from the current parameters (the step-start kernels; the dense
+        map is then copied into the fixed buffers the captured forward reads)."""
         st = self._store
         with torch.no_grad():
+            if st["small"]:
+                _small_forward_into(self.weight, self.alpha, st["Q"], st["inv"], st["nrm"])
+                return
             Q, nrm, inv = self._dense_map()
             st["Q"].copy_(Q)
             st["nrm"].copy_(nrm)
@@ -599,7 +654,8 @@ class CayleyLinear(nn.Linear):
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                Q = _DenseCayleyStoredFn.apply(self.weight, self.alpha, st)
+                fn = _SmallCayleyStoredFn if st["small"] else _DenseCayleyStoredFn
+                Q = fn.apply(self.weight, self.alpha, st)
             main.wait_stream(side)
             self._pre = None
             self._Q = Q.detach()

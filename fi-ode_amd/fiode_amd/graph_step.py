@@ -110,10 +110,13 @@ class GraphTrainStep:
         from .cayley import CayleyConv, CayleyLinear
         from .optim import _KernelStepMixin
         self.early = self.single and isinstance(self.opt, _KernelStepMixin)
-        kinds = (CayleyConv, CayleyLinear) if self.maps_ahead_linear else (CayleyConv,)
+        lin = self.maps_ahead_linear
+        lin_kinds = ("dense", "small") if lin is True else (("small",) if lin == "small" else ())
         root = getattr(self.module, "init_coordinates", self.module)       # the backbone's layers
         for c in root.modules():
-            if isinstance(c, kinds) and c.pipeline_on():
+            ok = (c.pipeline_on() if isinstance(c, CayleyConv) else
+                  c.pipeline_on(lin_kinds) if isinstance(c, CayleyLinear) and lin_kinds else False)
+            if ok:
                 self.piped.append(c)
                 if self.early:
                     c._store["on_grads"] = (lambda gw, ga, c=c: self._update_layer(c, gw, ga))

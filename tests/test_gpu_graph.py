@@ -108,18 +108,18 @@ def test_maps_ahead_equal_step_start_maps(train_ode):
     x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (32,), generator=g).to(dev)
     out = {}
-    for ahead in ("conv", "conv+linear", None):
+    for ahead in ("conv", "conv+linear", "conv+small", None):
         mod = bench.build_module(dev, seed=0, train_ode=train_ode)
         mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         opt = mod.configure_optimizers(capturable=True)[0][0]
         gs = GraphTrainStep(mod, opt, x, y, warmup=2, maps_ahead=ahead is not None,
-                            maps_ahead_linear=ahead == "conv+linear")
-        assert len(gs.piped) == {"conv": 4, "conv+linear": 6, None: 0}[ahead]
+                            maps_ahead_linear={"conv+linear": True, "conv+small": "small"}.get(ahead, False))
+        assert len(gs.piped) == {"conv": 4, "conv+linear": 7, "conv+small": 5, None: 0}[ahead]
         losses = [float(gs.step()) for _ in range(3)]
         torch.cuda.synchronize()
         out[ahead] = (losses, [p.detach().clone() for p in mod.parameters()])
         gs.close()
-    for ahead in ("conv", "conv+linear"):
+    for ahead in ("conv", "conv+linear", "conv+small"):
         assert out[ahead][0] == out[None][0], ahead
         for a, b in zip(out[ahead][1], out[None][1]):
             assert torch.equal(a, b), ahead

@@ -230,6 +230,10 @@ def warm_square(m):
     cayley.WARM_WIDE = False
 
 
+def ahead_small(m):
+    m._ahead_lin = "small"
+
+
 def seed1000(m):
     m.seed = 1000
 
@@ -242,7 +246,7 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
-ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "ahead_lin": ahead_lin, "seed1000": seed1000, "warm_square": warm_square, "newton3": newton3, "warm_inverse": warm_inverse, "late_refresh": late_refresh, "lin0": sched(lin=[0, 0, 0], dyn=0), "lin1": sched(lin=[1, 1, 1], dyn=1), "lin2": sched(lin=[2, 2, 2], dyn=2), "at_start": at_start, "no_ahead": no_ahead, "conv_maps_cached": conv_maps_cached, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
+ALL = {"default": reset2, "torch_adam": torch_adam, "no_split": no_split, "ahead_lin": ahead_lin, "seed1000": seed1000, "ahead_small": ahead_small, "warm_square": warm_square, "newton3": newton3, "warm_inverse": warm_inverse, "late_refresh": late_refresh, "lin0": sched(lin=[0, 0, 0], dyn=0), "lin1": sched(lin=[1, 1, 1], dyn=1), "lin2": sched(lin=[2, 2, 2], dyn=2), "at_start": at_start, "no_ahead": no_ahead, "conv_maps_cached": conv_maps_cached, "split_own": split_own, "split_ode": split_ode, "dense_bwd_side": dense_bwd_side, "unfused_loss": unfused_loss, "blas_rocblas": blas_rocblas, "ode_bwd_side": ode_bwd_side, "lin_one": lin_one, "lin_one_conv_first": lin_one_conv_first, "conv_first_split": conv_first_split, "lin_first_split": lin_first_split,
        "conv_first": conv_first, "small_bwd_main": small_bwd_main, "ode_on_main": ode_on_main, "grouped": grouped,
        "grouped_linfirst": grouped_ai_linfirst, "lin_first": lin_first}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
