@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
+import os
 from typing import Optional
 
 import torch
@@ -61,7 +62,8 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
 # ~40 us per step (1.688 -> 1.646 ms after ~50 replays, tools/ab_step.py), but while Adam's first
 # bias-corrected steps move every weight by ~lr the wide map's refinement fails and the fallback
 # pays both (the bench's 20 steps after 5 warm-ups of a fresh optimizer: 1.67 -> 1.76 ms).
-WARM_INVERSE = False
+# FIODE_WARM_INVERSE=1 in the environment turns it on (long runs: 1.695 -> 1.635 ms per step).
+WARM_INVERSE = os.environ.get("FIODE_WARM_INVERSE", "0") not in ("", "0")
 NEWTON_ITERS = 2
 WARM_WIDE = True           # also the wide 4096 -> 512 map (its system converges more slowly)
 NEWTON_TOL = 1e-5
