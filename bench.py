@@ -218,6 +218,7 @@ def main():
             metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
                             "mean_active_constraints": sc[2]}, world)   # fused sync_dist
 
+        last = {}
         if args.eager:
             def step():
                 opt.zero_grad(set_to_none=False)
@@ -228,12 +229,13 @@ def main():
                     sync_metrics()
                 opt.step()
                 mod.global_step += 1
+                last["loss"] = loss
         else:
             from fiode_amd.graph_step import GraphTrainStep
             gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world)
 
             def step():
-                gstep.step()                          # hipGraph replay (+ eager RCCL between graphs)
+                last["loss"] = gstep.step()           # hipGraph replay (+ eager RCCL between graphs)
                 if world > 1:
                     sync_metrics()
 
@@ -251,15 +253,21 @@ def main():
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        return float(dt.item()), mod, x, y
+        # health of the timed run, read after the timed region: the sticky status of the persistent
+        # train_ode solve (a timed-out QP-exit exchange poisons the loss with NaN) and the last loss
+        health = {"status": int(mod.device_status()) if hasattr(mod, "device_status") else 0,
+                  "loss_finite": bool(torch.isfinite(last["loss"]).all())}
+        if health["status"] or not health["loss_finite"]:
+            raise RuntimeError(f"unhealthy timed run: {health}")
+        return float(dt.item()), mod, x, y, health
 
     train_ode = args.workload == "rk4"
-    elapsed, mod, x, y = timed_run(train_ode, args.steps, args.warmup)
+    elapsed, mod, x, y, health = timed_run(train_ode, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B_PER_RANK * args.steps / elapsed
     lyap_only = None
     if train_ode and not args.no_secondary:
-        e2, _, _, _ = timed_run(False, args.steps, args.warmup)
+        e2, _, _, _, _ = timed_run(False, args.steps, args.warmup)
         lyap_only = {"images_per_s": round(world * B_PER_RANK * args.steps / e2, 2),
                      "ms_per_step": round(e2 / args.steps * 1e3, 4)}
 
@@ -335,6 +343,7 @@ def main():
            "roofline": roofline,
            "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)},
            "lyapunov_only_step": lyap_only,
+           "device_status": health,
            "runtime_env": {"DEBUG_HIP_FORCE_GRAPH_QUEUES": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES")}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_budget, train_ode=train_ode)

@@ -30,6 +30,7 @@ struct AdamArgs {
   float lr, b1, omb1, b2, omb2, eps, wd;   // fp32 operands; 1 - beta formed in double
   double lr_d, b1_d, b2_d;     // for the bias corrections of device step counts
   float step_size_h, bc2_sqrt_h;  // bias-corrected factors of a host step count
+  double step_h;
   int blk0[MAXT + 1];          // first workgroup of each tensor (prefix sum)
   int64_t numel[MAXT];
   float* p[MAXT];
@@ -37,6 +38,8 @@ struct AdamArgs {
   float* m[MAXT];
   float* v[MAXT];
   const float* t_dev[MAXT];     // per-tensor step count on the device (capturable Adam)
+  const void* lr_dev;          // device learning rate (tensor lr) or null
+  int lr_dev_is_double;
 };
 
 struct Coef {
@@ -61,14 +64,20 @@ __global__ __launch_bounds__(NT) void k_adam(const AdamArgs a) {
   int t = 0;
   while (t + 1 < a.n && a.blk0[t + 1] <= b) ++t;
   Coef c;
-  c.lr = a.lr; c.b1 = a.b1; c.omb1 = a.omb1; c.b2 = a.b2; c.omb2 = a.omb2; c.eps = a.eps; c.wd = a.wd;
+  double lr_d = a.lr_d;
+  float lr = a.lr;
+  if (a.lr_dev) {
+    lr_d = a.lr_dev_is_double ? *(const double*)a.lr_dev : (double)*(const float*)a.lr_dev;
+    lr = (float)lr_d;
+  }
+  c.lr = lr; c.b1 = a.b1; c.omb1 = a.omb1; c.b2 = a.b2; c.omb2 = a.omb2; c.eps = a.eps; c.wd = a.wd;
   c.decoupled = a.decoupled; c.maximize = a.maximize;
   if (a.t_dev[t]) {
     const double step = (double)*a.t_dev[t];
-    c.step_size = (float)(a.lr_d / (1.0 - pow(a.b1_d, step)));
+    c.step_size = (float)(lr_d / (1.0 - pow(a.b1_d, step)));
     c.bc2_sqrt = (float)sqrt(1.0 - pow(a.b2_d, step));
   } else {
-    c.step_size = a.step_size_h;
+    c.step_size = a.lr_dev ? (float)(lr_d / (1.0 - pow(a.b1_d, a.step_h))) : a.step_size_h;
     c.bc2_sqrt = a.bc2_sqrt_h;
   }
 
@@ -115,6 +124,9 @@ extern "C" int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float
   a.lr_d = cfg->lr; a.b1_d = cfg->beta1; a.b2_d = cfg->beta2;
   a.step_size_h = (float)(cfg->lr / (1.0 - pow(cfg->beta1, cfg->step)));
   a.bc2_sqrt_h = (float)sqrt(1.0 - pow(cfg->beta2, cfg->step));
+  a.step_h = cfg->step;
+  a.lr_dev = cfg->lr_dev;
+  a.lr_dev_is_double = cfg->lr_dev_is_double != 0;
   int64_t blocks = 0;
   for (int i = 0; i < a.n; ++i) {
     if (numel[i] < 0 || (numel[i] > 0 && (!params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i])))

@@ -80,10 +80,14 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
+ABI_VERSION = 2            # FIODE_ABI_VERSION (include/fiode.h)
+
+
 class AdamConfig(ct.Structure):
     _fields_ = [("n_tensors", ct.c_int32), ("decoupled", ct.c_int32), ("maximize", ct.c_int32), ("pad_", ct.c_int32),
                 ("lr", ct.c_double), ("beta1", ct.c_double), ("beta2", ct.c_double), ("eps", ct.c_double),
-                ("weight_decay", ct.c_double), ("step", ct.c_double)]
+                ("weight_decay", ct.c_double), ("step", ct.c_double), ("lr_dev", ct.c_void_p),
+                ("lr_dev_is_double", ct.c_int32), ("pad2_", ct.c_int32)]
 
 
 class SconvConfig(ct.Structure):
@@ -185,7 +189,12 @@ _LIB = None
 def lib():
     global _LIB
     if _LIB is None:
-        _LIB = _load()
+        lb = _load()
+        v = lb.fiode_abi_version()
+        if v != ABI_VERSION:
+            raise FiodeLibraryError(f"{LIB_PATH}: ABI version {v}, this package binds {ABI_VERSION} "
+                                    "(stale build: run `make -C fi-ode_amd/csrc`)")
+        _LIB = lb
     return _LIB
 
 

@@ -14,7 +14,6 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
-import os
 from typing import Optional
 
 import torch
@@ -50,57 +49,6 @@ def _block_inverse(M: torch.Tensor) -> torch.Tensor:
         X[..., :, K] = -(Cm @ P)
         X[..., K, K] = P
     return X
-
-
-# Warm-started inverse of a training step's dense Cayley system.  The weights move a little per
-# optimizer step, so the previous step's inverse X is close to M^-1: NEWTON_ITERS Newton-Schulz
-# steps X <- 2X - X (M X) (two GEMMs and one lerp each, quadratic convergence) reach float32
-# accuracy where the 64-panel elimination is a ~150 us latency chain.  The bound ||I - M X||^2 of
-# the final residual (induced inf-norm of the last step's residual) is checked on the device;
-# above NEWTON_TOL the exact elimination runs after all (fiode_block_inverse_cond skips it
-# otherwise) -- no host sync, safe for any step size.  Opt-in: in steady-state training it saves
-# ~40 us per step (1.688 -> 1.646 ms after ~50 replays, tools/ab_step.py), but while Adam's first
-# bias-corrected steps move every weight by ~lr the wide map's refinement fails and the fallback
-# pays both (the bench's 20 steps after 5 warm-ups of a fresh optimizer: 1.67 -> 1.76 ms).
-# FIODE_WARM_INVERSE=1 in the environment turns it on (long runs: 1.695 -> 1.635 ms per step).
-WARM_INVERSE = os.environ.get("FIODE_WARM_INVERSE", "0") not in ("", "0")
-NEWTON_ITERS = 2
-WARM_WIDE = True           # also the wide 4096 -> 512 map (its system converges more slowly)
-NEWTON_TOL = 1e-5
-
-
-def _warm_inverse(M: torch.Tensor, cache: dict, key=None) -> torch.Tensor:
-    """``key``: identifies the parameters M was formed from (their version counters): a second
-    evaluation of the same system within a step (e.g. the reference-order second backbone pass)
-    returns the first one's inverse, bit for bit."""
-    from . import ops
-    n = M.shape[-1]
-    M2 = M.reshape(n, n)
-    X = cache.get("X")
-    if X is None or X.shape != M2.shape or X.device != M2.device:
-        inv = ops.block_inverse(M2)
-        cache["X"] = inv.clone()
-        cache["eye"] = torch.eye(n, dtype=M.dtype, device=M.device)
-        cache["skip"] = torch.zeros(1, dtype=torch.int32, device=M.device)
-        cache["skipb"] = torch.zeros((), dtype=torch.bool, device=M.device)
-        cache["key"] = key
-        return inv.reshape(M.shape)
-    if key is not None and cache.get("key") == key:
-        return X.clone().reshape(M.shape)
-    cache["key"] = key
-    eye = cache["eye"]
-    res = None
-    for it in range(NEWTON_ITERS):
-        Y = torch.matmul(M2, X)                          # M X = I - R
-        if it == NEWTON_ITERS - 1:
-            # R_{k+1} = R_k^2, so ||R_final|| <= ||R||^2 in the induced inf-norm (max row sum)
-            res = torch.linalg.matrix_norm(Y - eye, ord=float("inf"))
-        X = torch.lerp(torch.matmul(X, Y), X, 2.0)       # X (2I - M X) = 2X - X M X
-    torch.le(res * res, NEWTON_TOL, out=cache["skipb"])
-    cache["skip"].copy_(cache["skipb"])
-    ops.block_inverse(M2, out=X, skip=cache["skip"])
-    cache["X"].copy_(X)
-    return X.reshape(M.shape)
 
 
 class _CayleyInverse(torch.autograd.Function):
@@ -277,14 +225,9 @@ class _DenseCayleyFn(torch.autograd.Function):
     every elementwise stage between them one HIP kernel (fiode_dense_cayley_*; dense.hip)."""
 
     @staticmethod
-    def forward(ctx, W, alpha, inv_cache=None):
+    def forward(ctx, W, alpha):
         st, M = _dense_prep(W, alpha)
-        if (inv_cache is not None and M.shape[0] == 1 and M.shape[-1] > 64
-                and (WARM_WIDE or W.shape[-1] == W.shape[-2])):
-            key = None if STEP_TOKEN is None else (STEP_TOKEN, W.data_ptr(), alpha.data_ptr())
-            inv = _warm_inverse(M, inv_cache, key=key)
-        else:
-            inv = _block_inverse(M)
+        inv = _block_inverse(M)
         Q = _dense_finish(st, inv)
         ctx.save_for_backward(st["Wb"], st["al"], st["nrm"], inv)
         ctx.shapes = (W.shape, alpha.shape)
@@ -295,75 +238,7 @@ class _DenseCayleyFn(torch.autograd.Function):
     def backward(ctx, gQ):
         Wb, al, nrm, inv = ctx.saved_tensors
         return _run_on_step_stream(DENSE_BWD_ON_MAIN, ctx.step_stream,
-                                   lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes)) + (None,)
-
-
-class _DenseCayleyStoredFn(torch.autograd.Function):
-    """The Q of a CayleyLinear whose dense map was computed AHEAD into fixed buffers (CayleyLinear
-    pipeline_on / refresh_map; see _SpectralCayleyStoredFn): forward hands out the stored Q,
-    backward is _DenseCayleyFn's from the stored norm and inverse, then ``store["on_grads"]``."""
-
-    @staticmethod
-    def forward(ctx, W, alpha, store: dict):
-        ctx.save_for_backward(W, alpha)
-        ctx.store = store
-        return store["Q"].detach().reshape(W.shape)
-
-    @staticmethod
-    def backward(ctx, gQ):
-        W, alpha = ctx.saved_tensors
-        st = ctx.store
-        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
-        al = alpha.detach().reshape(-1).contiguous().float()
-        gW, ga = _dense_backward(Wb, al, st["nrm"], st["inv"], gQ, W.shape, alpha.shape)
-        hook = st.get("on_grads")
-        if hook is not None:
-            hook(gW, ga)
-        return gW, ga, None
-
-
-class _DenseCayleyGroupFn(torch.autograd.Function):
-    """Several dense Cayley maps with the same k = min(cout, cin) (the backbone's 4096 -> 512 and
-    512 -> 512 CayleyLinears) in one node: their systems are stacked and inverted by ONE batched
-    block inverse (fiode_block_inverse_batched), so the two latency chains of 2 k / 64 dependent
-    launches become one.  apply(W1, alpha1, W2, alpha2, ...) -> (Q1, Q2, ...); the backward is
-    each map's own (_dense_backward; the inverse is not in it)."""
-
-    @staticmethod
-    def forward(ctx, *args):
-        Ws, alphas = args[0::2], args[1::2]
-        k = min(Ws[0].shape[-2:])
-        Mall = torch.empty((len(Ws), k, k), dtype=torch.float32, device=Ws[0].device)
-        sts = [_dense_prep(W, a, M=Mall[i:i + 1])[0] for i, (W, a) in enumerate(zip(Ws, alphas))]
-        invs = _block_inverse(Mall)
-        Qs = [_dense_finish(st, invs[i:i + 1]).reshape(W.shape) for i, (st, W) in enumerate(zip(sts, Ws))]
-        saved = []
-        for i, st in enumerate(sts):
-            saved += [st["Wb"], st["al"], st["nrm"], invs[i:i + 1]]
-        ctx.save_for_backward(*saved)
-        ctx.shapes = [(W.shape, a.shape) for W, a in zip(Ws, alphas)]
-        return tuple(Qs)
-
-    @staticmethod
-    def backward(ctx, *gQs):
-        saved = ctx.saved_tensors
-        out = []
-        for i, (gQ, shp) in enumerate(zip(gQs, ctx.shapes)):
-            if gQ is None:
-                out += [None, None]
-                continue
-            Wb, al, nrm, inv = saved[4 * i:4 * i + 4]
-            out += list(_dense_backward(Wb, al, nrm, inv, gQ, *shp))
-        return tuple(out)
-
-
-def dense_cayley_group(Ws, alphas):
-    """Q_i = cayley(alpha_i W_i / ||W_i||) for 2-D real ROCm matrices with a common k, with one
-    batched inverse (see _DenseCayleyGroupFn)."""
-    args = []
-    for W, a in zip(Ws, alphas):
-        args += [W, a]
-    return _DenseCayleyGroupFn.apply(*args)
+                                   lambda: _dense_backward(Wb, al, nrm, inv, gQ, *ctx.shapes))
 
 
 class _SmallCayleyFn(torch.autograd.Function):
@@ -408,48 +283,6 @@ class _SmallCayleyFn(torch.autograd.Function):
         return gW.reshape(wshape), ga.reshape(ashape)
 
 
-def _small_forward_into(W: torch.Tensor, alpha: torch.Tensor, Q: torch.Tensor, inv: torch.Tensor,
-                        nrm: torch.Tensor) -> None:
-    """fiode_small_cayley_forward of one [cout, cin] matrix into given buffers."""
-    from . import ops, _lib as L
-    cout, cin = W.shape[-2], W.shape[-1]
-    L.check(L.lib().fiode_small_cayley_forward(ops._stream(W.device), 1, cout, cin, W.detach().contiguous().data_ptr(),
-                                               alpha.detach().reshape(-1).contiguous().float().data_ptr(),
-                                               Q.data_ptr(), inv.data_ptr(), nrm.data_ptr()),
-            "fiode_small_cayley_forward")
-
-
-class _SmallCayleyStoredFn(torch.autograd.Function):
-    """The Q of a small (k <= 16) CayleyLinear map computed AHEAD into fixed buffers (see
-    _SpectralCayleyStoredFn): forward hands out the stored Q, backward is _SmallCayleyFn's from the
-    stored norm and inverse, then ``store["on_grads"]``."""
-
-    @staticmethod
-    def forward(ctx, W, alpha, store: dict):
-        ctx.save_for_backward(W, alpha)
-        ctx.store = store
-        return store["Q"].detach().reshape(W.shape)
-
-    @staticmethod
-    def backward(ctx, gQ):
-        from . import ops, _lib as L
-        W, alpha = ctx.saved_tensors
-        st = ctx.store
-        cout, cin = W.shape[-2], W.shape[-1]
-        gQb = gQ.reshape(cout, cin).contiguous().float()
-        gW = torch.empty_like(W)
-        ga = torch.empty(1, dtype=torch.float32, device=W.device)
-        L.check(L.lib().fiode_small_cayley_backward(
-            ops._stream(W.device), 1, cout, cin, W.detach().contiguous().data_ptr(),
-            alpha.detach().reshape(-1).contiguous().float().data_ptr(), st["nrm"].data_ptr(), st["inv"].data_ptr(),
-            gQb.data_ptr(), gW.data_ptr(), ga.data_ptr()), "fiode_small_cayley_backward")
-        ga = ga.reshape(alpha.shape)
-        hook = st.get("on_grads")
-        if hook is not None:
-            hook(gW, ga)
-        return gW, ga, None
-
-
 def _small_ok(W: torch.Tensor) -> bool:
     from . import _lib as L
     cout, cin = W.shape[-2], W.shape[-1]
@@ -457,8 +290,7 @@ def _small_ok(W: torch.Tensor) -> bool:
     return k <= L.FIODE_SMALL_CAYLEY_MAX_K and R * k <= L.FIODE_SMALL_CAYLEY_MAX_RK
 
 
-def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False,
-                  inv_cache: Optional[dict] = None) -> torch.Tensor:
+def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False) -> torch.Tensor:
     """cayley(alpha * W / ||W||) (convert_cayley's parametrisation, classification.py:282-293).
     Real matrices on ROCm (one matrix, or a batch with per-matrix norms) take one kernel per
     direction when k = min(cout, cin) <= 16 (_SmallCayleyFn), else the fused stages of
@@ -466,7 +298,7 @@ def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False
     if W.is_cuda and W.dtype == torch.float32 and (W.dim() == 2 or per_matrix) and DENSE_FUSED:
         if SMALL_FUSED and _small_ok(W):
             return _SmallCayleyFn.apply(W, alpha)
-        return _DenseCayleyFn.apply(W, alpha, inv_cache)
+        return _DenseCayleyFn.apply(W, alpha)
     return _CayleyScaledFn.apply(W, alpha, per_matrix)
 
 
@@ -511,29 +343,20 @@ SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 
 
-STEP_TOKEN: Optional[int] = None
-_STEP_COUNT = 0
-
-
 class step_stream_scope:
-    """Context manager: STEP_STREAM = ``stream`` inside, the previous value restored on exit; also
-    a fresh STEP_TOKEN (one training forward), under which a dense map evaluated twice reuses its
-    first warm-started inverse (_warm_inverse ``key``)."""
+    """Context manager: STEP_STREAM = ``stream`` inside, the previous value restored on exit."""
 
     def __init__(self, stream):
         self.stream = stream
 
     def __enter__(self):
-        global STEP_STREAM, STEP_TOKEN, _STEP_COUNT
-        _STEP_COUNT += 1
+        global STEP_STREAM
         self.prev, STEP_STREAM = STEP_STREAM, self.stream
-        self.prev_token, STEP_TOKEN = STEP_TOKEN, _STEP_COUNT
         return self
 
     def __exit__(self, *exc):
-        global STEP_STREAM, STEP_TOKEN
+        global STEP_STREAM
         STEP_STREAM = self.prev
-        STEP_TOKEN = self.prev_token
         return False
 
 
@@ -583,8 +406,6 @@ class CayleyLinear(nn.Linear):
         self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
         self._Q = None
         self._pre = None
-        self._store = None              # map computed ahead (pipeline_on), else None
-        self._inv_cache = {}            # previous training step's inverse (_warm_inverse)
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -594,74 +415,14 @@ class CayleyLinear(nn.Linear):
         self._Q = None
 
     def effective_weight(self) -> torch.Tensor:
-        # training: the inverse is warm-started from the previous step's (_warm_inverse)
-        warm = self._inv_cache if (self.training and WARM_INVERSE and torch.is_grad_enabled()) else None
-        return cayley_scaled(self.weight, self.alpha, inv_cache=warm)
+        return cayley_scaled(self.weight, self.alpha)
 
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
         the layers before it); the next training forward joins it."""
-        if self._store is not None:
-            return
         self._pre = _prefetch(stream, self.effective_weight)
 
-    # ---- map computed ahead (GraphTrainStep; see CayleyConv.pipeline_on) ------------------------
-    def _dense_map(self):
-        st, M = _dense_prep(self.weight, self.alpha)
-        # the same warm start as the step-start map (no key: the parameters just changed)
-        inv = _warm_inverse(M, self._inv_cache) if WARM_INVERSE else _block_inverse(M)
-        return _dense_finish(st, inv), st["nrm"], inv
-
-    def pipeline_on(self, kinds=("dense", "small")) -> bool:
-        """ROCm float32 weights with the fused dense or small map (``kinds``); returns whether
-        the layer is pipelined."""
-        W = self.weight
-        if not (W.is_cuda and W.dtype == torch.float32 and W.dim() == 2 and DENSE_FUSED):
-            return False
-        small = SMALL_FUSED and _small_ok(W)
-        if ("small" if small else "dense") not in kinds:
-            return False
-        with torch.no_grad():
-            if small:
-                k = min(W.shape)
-                Q = torch.empty_like(W)
-                inv = torch.empty((1, k, k), dtype=torch.float32, device=W.device)
-                nrm = torch.empty(1, dtype=torch.float32, device=W.device)
-                _small_forward_into(W, self.alpha, Q, inv, nrm)
-            else:
-                Q, nrm, inv = self._dense_map()
-        self._store = {"Q": Q, "nrm": nrm, "inv": inv, "small": small, "stream": torch.cuda.Stream(W.device)}
-        return True
-
-    def pipeline_off(self) -> None:
-        self._store = None
-
-    def refresh_map(self) -> None:
-        """Recompute the stored map from the current parameters (the step-start kernels; the dense
-        map is then copied into the fixed buffers the captured forward reads)."""
-        st = self._store
-        with torch.no_grad():
-            if st["small"]:
-                _small_forward_into(self.weight, self.alpha, st["Q"], st["inv"], st["nrm"])
-                return
-            Q, nrm, inv = self._dense_map()
-            st["Q"].copy_(Q)
-            st["nrm"].copy_(nrm)
-            st["inv"].copy_(inv)
-
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        st = self._store
-        if st is not None and self.training and torch.is_grad_enabled():
-            side = st["stream"]
-            main = torch.cuda.current_stream(x.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                fn = _SmallCayleyStoredFn if st["small"] else _DenseCayleyStoredFn
-                Q = fn.apply(self.weight, self.alpha, st)
-            main.wait_stream(side)
-            self._pre = None
-            self._Q = Q.detach()
-            return F.linear(x, Q, self.bias)
         if self._pre is not None and self.training:
             Q = _take(self._pre)
             self._pre = None
@@ -673,29 +434,6 @@ class CayleyLinear(nn.Linear):
         # parameters' AccumulateGrad nodes) alive into the next step
         self._Q = Q.detach()
         return F.linear(x, Q if self.training else self._Q, self.bias)
-
-
-def group_prefetch(lins, stream: torch.cuda.Stream) -> None:
-    """Prefetch the Cayley maps of several CayleyLinears with the same k as one group node on
-    ``stream`` (dense_cayley_group); each layer joins its own Q at its next training forward."""
-    main = torch.cuda.current_stream(stream.device)
-    stream.wait_stream(main)
-    with torch.cuda.stream(stream):
-        Qs = dense_cayley_group([l.weight for l in lins], [l.alpha for l in lins])
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    for l, Q in zip(lins, Qs):
-        l._pre = (Q, ev)
-
-
-def _group_eligible(l) -> bool:
-    """Dense (k > 64: block-inverse) CayleyLinear maps on ROCm; grouped by k by the caller."""
-    W = l.weight
-    return (isinstance(l, CayleyLinear) and W.is_cuda and W.dtype == torch.float32 and W.dim() == 2
-            and DENSE_FUSED and min(W.shape) > 64)
-
-
-group_prefetch.eligible = _group_eligible
 
 
 class _GroupSortFn(torch.autograd.Function):

@@ -29,16 +29,13 @@ import torch
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
-                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
-                 maps_ahead_linear: bool = False, refresh_after_backward: bool = False):
+                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
         self.module, self.opt, self.reducer, self.world, self.act = module, optimizer, reducer, world, act
         self.check_every, self.n_replays = int(check_every), 0
         self.piped, self.early = [], False
-        self.maps_ahead_linear = maps_ahead_linear
-        self.refresh_after_backward = refresh_after_backward
         dyn = module.dyn_fun
         if module.global_step < dyn.kappa_length:
             raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
@@ -93,6 +90,9 @@ class GraphTrainStep:
             if not all(views):
                 raise RuntimeError("p.grad does not point into the reducer's bucket after capture")
         self.scalars = module.last_plan["scalars"]
+        # a float lr is a launch argument baked into the captured optimizer step (a tensor lr is
+        # read on the device: LR schedulers may change it between replays)
+        self._float_lrs = [g["lr"] for g in self.opt.param_groups]
 
     # ---- conv maps computed ahead -------------------------------------------------------------
     # Each CayleyConv's spectral map depends only on its own two parameters, and the step's first
@@ -103,38 +103,28 @@ class GraphTrainStep:
     # the backward runs; on N ranks (gradients final only after the all-reduce) after the optimizer
     # step.  The maps are the same kernels on the same parameters as at the start of the next step,
     # so the results are unchanged.  Parameters changed outside the replays: call refresh_maps().
-    # maps_ahead_linear: the same for the dense CayleyLinear maps (bit-identical too, but the
-    # executor places their update + 512 x 512 inverse chain on the backbone backward's queue:
-    # 1.684 -> 1.732 ms per step in the interleaved A/B; off).
+    # The early per-layer update needs the layer's map backward to run ONCE per step with the
+    # layer's whole gradient: with the reference-order second backbone pass
+    # (ode_reuse_features False) each layer has two map nodes per step, so there the maps are
+    # refreshed after the optimizer step instead (late refresh, correct for any number of uses).
     def _maps_ahead_on(self):
-        from .cayley import CayleyConv, CayleyLinear
-        from .optim import _KernelStepMixin
-        self.early = self.single and isinstance(self.opt, _KernelStepMixin)
-        lin = self.maps_ahead_linear
-        lin_kinds = ("dense", "small") if lin is True else (("small",) if lin == "small" else ())
+        from .cayley import CayleyConv
+        from .optim import _KernelStepMixin, _kernel_ok_params
+        once = getattr(self.module, "ode_reuse_features", True) or not getattr(self.module, "train_ode", False)
+        self.early = self.single and once and isinstance(self.opt, _KernelStepMixin)
         root = getattr(self.module, "init_coordinates", self.module)       # the backbone's layers
         for c in root.modules():
-            ok = (c.pipeline_on() if isinstance(c, CayleyConv) else
-                  c.pipeline_on(lin_kinds) if isinstance(c, CayleyLinear) and lin_kinds else False)
-            if ok:
+            if isinstance(c, CayleyConv) and c.pipeline_on():
                 self.piped.append(c)
-                if self.early:
-                    c._store["on_grads"] = (lambda gw, ga, c=c: self._update_layer(c, gw, ga))
+        if self.early and not all(_kernel_ok_params(self.opt, [c.weight, c.alpha]) for c in self.piped):
+            self.early = False          # a group the kernel does not cover: update in step()
+        if self.early:
+            for c in self.piped:
+                c._store["on_grads"] = (lambda gw, ga, c=c: self._update_layer(c, gw, ga))
 
     def _update_layer(self, c, gw, ga):
         self.opt.step_params([(c.weight, gw), (c.alpha, ga)])
-        if not self.refresh_after_backward:
-            c.refresh_map()
-
-    def _refresh_on_layer_streams(self):
-        """refresh_after_backward: each layer's map recomputed on its own stream (ordered after its
-        early update there), captured after the whole backward."""
-        main = torch.cuda.current_stream()
-        for c in self.piped:
-            st = c._store["stream"]
-            with torch.cuda.stream(st):
-                c.refresh_map()
-            main.wait_stream(st)
+        c.refresh_map()
 
     def _refresh_late(self):
         if not self.early:
@@ -192,8 +182,6 @@ class GraphTrainStep:
             p.grad = None
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         loss.backward()
-        if getattr(self, "early", False) and self.refresh_after_backward and self.piped:
-            self._refresh_on_layer_streams()
         if self.reducer is not None and self.world > 1:
             self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)
@@ -207,6 +195,11 @@ class GraphTrainStep:
         m = self.module
         if m.current_epoch != self.epoch:
             raise RuntimeError("epoch changed: the captured sampler plan is stale, recapture the step")
+        for g, lr in zip(self.opt.param_groups, self._float_lrs):
+            if not torch.is_tensor(lr) and g["lr"] != lr:
+                raise RuntimeError(f"learning rate changed since capture ({lr} -> {g['lr']}): the captured step "
+                                   "bakes a float lr in; use a tensor lr (Adam(..., lr=torch.tensor(lr, "
+                                   "device=...), capturable=True)) or recapture the step")
         if x is not None:
             self.static_x.copy_(x, non_blocking=True)
         if y is not None:

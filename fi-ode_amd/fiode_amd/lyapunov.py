@@ -151,7 +151,7 @@ class LyapODELossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_feat, x_ode, Q1, b1, Qx, bx, Q2, b2, Q3, b3, h0, y, plan: dict, oplan: dict, p: float,
-                ode_stream, wtok=None, holder=None):
+                ode_stream):
         from .cayley import _prefetch, _take
         w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
         w = {k: v.detach().contiguous() for k, v in w.items()}
@@ -191,7 +191,6 @@ class LyapODELossFn(torch.autograd.Function):
         ctx.ode = (gunit, xo, w, oplan, ws)
         ctx.p = float(p)
         ctx.split = x_ode is not None
-        ctx.holder = holder
         return total
 
     @staticmethod
@@ -199,21 +198,6 @@ class LyapODELossFn(torch.autograd.Function):
         gunit, xo, w, oplan, ws = ctx.ode
         ctx.ode = None
         g_y = gunit * go
-        if ctx.holder is not None:
-            # weight gradients in _ODEWeightGradFn (its own node, on its own stream): here only the
-            # adjoint sweep and dL/dx_feat, so the backbone's backward starts right after them
-            s = go * (1.0 - ctx.p)
-            lyap_x = ctx.lyap[0]
-            if ctx.split:
-                gxo = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
-                gx = lyap_x * s
-            else:
-                gx = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws, gx_add=lyap_x,
-                                             gx_add_scale=s)
-                gxo = None
-            ctx.holder.update(ode=(xo, w, oplan, ws), lyap_w=ctx.lyap[1:], scale=s)
-            ctx.lyap = ctx.holder = None
-            return (gx, gxo) + (None,) * 14 + (go, None)
         gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
         keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         ode = [gr[k] for k in keys]
@@ -225,33 +209,7 @@ class LyapODELossFn(torch.autograd.Function):
         else:
             torch._foreach_add_(ode, lyap)
             gx, gxo = ode[0], None
-        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None, None, None)
-
-
-class _ODEWeightGradFn(torch.autograd.Function):
-    """The weight-gradient half of LyapODELossFn's backward as a node of its own: forward returns a
-    token LyapODELossFn consumes; backward (run on the stream the forward ran on -- a side stream,
-    see LyapunovLearning._lyap_ode_loss) sums the solve's weight gradients
-    (fiode_odetrain_backward_weights) and adds the fused step's, scaled by go * (1 - p): the same
-    float32 operations as the one-node backward, off the path to the backbone's backward."""
-
-    @staticmethod
-    def forward(ctx, Q1, b1, Qx, bx, Q2, b2, Q3, b3, holder: dict):
-        ctx.holder = holder
-        return Q1.new_zeros(())
-
-    @staticmethod
-    def backward(ctx, _g):
-        h, ctx.holder = ctx.holder, None
-        xo, w, oplan, ws = h.pop("ode")
-        lyap_w, s = h.pop("lyap_w"), h.pop("scale")
-        gr = ops.odetrain_backward_weights(xo, w, oplan["dyn"], oplan["cfg"], ws)
-        ode = [gr[k] for k in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
-        torch._foreach_add_(ode, torch._foreach_mul(lyap_w, s))
-        st = torch.cuda.current_stream(xo.device)
-        for t in (xo, ws, s, *lyap_w, *w.values()):     # produced on other streams, freed after this
-            t.record_stream(st)
-        return tuple(ode) + (None,)
+        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None)
 
 
 class DecisionBoundary(nn.Module):
@@ -283,15 +241,6 @@ class UniformInitFun(nn.Module):
     def forward(self, x, dyn=None):
         h0 = tuple(getattr(self, f"h0_{i}")[None].repeat(x.shape[0], 1).to(x.device) for i in range(len(self.h_dims)))
         return self.param_map(x), h0
-
-
-# Capture order of the Cayley-map prefetch in the training step: after the step's input kernels
-# (the hipGraph executor dispatches in capture order; maps captured ahead of the input
-# normalisation held the conv stack back): 2.41 -> 2.32 ms per step in the interleaved A/B of
-# tools/ab_step.py, better than every deferral of the linear / dynamics maps tried.  The linear /
-# dynamics maps captured ahead of the conv maps ("lin_first"): 2.143 -> 2.090 ms (round 2 A/B, 6
-# interleaved rounds; one batched launch sequence for both 512 x 512 maps: 2.209).
-DEFAULT_PREFETCH_SCHEDULE = {"after_input": True, "order": "lin_first"}
 
 
 class LyapunovLearning(nn.Module):
@@ -345,10 +294,6 @@ class LyapunovLearning(nn.Module):
         # the configs[1] loss as one autograd node (LyapODELossFn); False: three nodes (the Lyapunov
         # step, the solve, the mix) as in round 1
         self.fused_ode_loss = True
-        # the fused loss node's weight gradients as a separate node (_ODEWeightGradFn) on a side
-        # stream ("own") or the solve's stream ("ode"), off the path from the solve's backward to
-        # the backbone's: no measurable gain (scheduling probes), off
-        self.split_ode_wgrad = False
         self._side_streams = None
         self.logged: Dict[str, float] = {}
         self._out = None
@@ -477,17 +422,14 @@ class LyapunovLearning(nn.Module):
         overlap each other and the convolutions.  Layers join them when they reach them (autograd
         runs their backward on the same streams).
 
-        ``prefetch_schedule`` = {"lin": [k0, k1, k2], "dyn": kd}: the map of linear layer i (of the
-        dynamics) is launched once conv layer k_i of the backbone has been launched (-1: at the
-        start of the step).  The hipGraph executor dispatches nodes in capture order over a few
-        hardware queues, so maps captured ahead of the main stream's first kernels can hold those
-        kernels back; deferring them past the first conv layers measured -0.16 ms per step
-        (tools/stream_probe.py)."""
-        sched = getattr(self, "prefetch_schedule", None)
-        if sched is None:
-            sched = dict(DEFAULT_PREFETCH_SCHEDULE)
-        if sched.get("after_input") and not getattr(self, "_in_input_hook", False):
-            # capture the map launches after the step's input kernels (see docstring)
+        Capture order: the hipGraph executor dispatches nodes in capture order over a few hardware
+        queues, so maps captured ahead of the main stream's first kernels hold those kernels back.
+        The launches are therefore captured right after the step's input kernels (a hook on the
+        backbone's first layer), the linear / dynamics maps first, then the conv maps (conv maps
+        computed one step ahead by GraphTrainStep skip their launch here).  Measured alternatives
+        (deferral past conv layers, one stream per map, one chain for all
+        linear maps, one batched inverse for both 512 x 512 systems) were all slower or equal."""
+        if not getattr(self, "_in_input_hook", False):
             bb = self.init_coordinates.param_map
             target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb
 
@@ -508,55 +450,11 @@ class LyapunovLearning(nn.Module):
         for m in self.init_coordinates.modules():
             if hasattr(m, "prefetch") and m is not self.dyn_fun:
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
-        # conv_streams "split": each conv map on a stream of its own (else one chain on s[0])
-        if sched.get("conv_streams") == "split":
-            if getattr(self, "_conv_streams", None) is None:
-                self._conv_streams = [s[0]] + [torch.cuda.Stream(device) for _ in range(len(convs) - 1)]
-            cst = self._conv_streams
-        else:
-            cst = [s[0]] * len(convs)
-        if sched.get("order", "conv_first") == "conv_first":
-            for c, st in zip(convs, cst):
-                c.prefetch(st)
-        klin = list(sched.get("lin", [-1] * len(lins))) + [-1] * len(lins)
-        jobs = []
-        if getattr(self, "group_lin_maps", False) and not sched.get("lin"):
-            # the linear maps with a common k > 64 (4096 -> 512, 512 -> 512): one node, one batched inverse
-            # (off by default: tools/ab_step.py measured no gain -- 2.47 vs 2.44 ms interleaved)
-            from .cayley import group_prefetch
-            by_k: Dict[int, list] = {}
-            for l in lins:
-                if group_prefetch.eligible(l):
-                    by_k.setdefault(min(l.weight.shape), []).append(l)
-            big = max(by_k.values(), key=len) if by_k else []
-            if len(big) > 1:
-                jobs.append((-1, (lambda big=big: group_prefetch(big, s[1]))))
-                lins = [l for l in lins if l not in big]
-                klin = [-1] * len(lins)
-        if sched.get("lin_streams") == "one":
-            # every linear map and the dynamics maps as one chain on s[1] (fewer parallel branches
-            # for the graph executor to map onto its queues)
-            jobs += [(klin[i], (lambda l=l: l.prefetch(s[1]))) for i, l in enumerate(lins)]
-            jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[1])))
-        else:
-            jobs += [(klin[i], (lambda l=l, st=s[2 + min(i, 1)]: l.prefetch(st))) if jobs else
-                     (klin[i], (lambda l=l, st=s[1 + min(i, 2)]: l.prefetch(st))) for i, l in enumerate(lins)]
-            jobs.append((sched.get("dyn", -1), lambda: self.dyn_fun.prefetch(s[3])))
-        for k, fn in jobs:
-            if k < 0:
-                fn()
-        if sched.get("order", "conv_first") != "conv_first":
-            for c, st in zip(convs, cst):
-                c.prefetch(st)
-        later = [(k, fn) for k, fn in jobs if k >= 0]
-        bb = self.init_coordinates.param_map
-        target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb
-        if later:
-            def hook(i):
-                for k, fn in later:
-                    if k == i:
-                        fn()
-            target.after_conv_hook = hook
+        for i, l in enumerate(lins):
+            l.prefetch(s[1 + min(i, 2)])
+        self.dyn_fun.prefetch(s[3])
+        for c in convs:
+            c.prefetch(s[0])
 
     def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
         """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""
@@ -670,25 +568,8 @@ class LyapunovLearning(nn.Module):
                 self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
             stream = self._ode_stream
         p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
-        wtok = holder = None
-        if self.split_ode_wgrad and static_state.is_cuda and torch.is_grad_enabled():
-            # the weight-gradient node forks onto its own stream (joined here: a captured graph
-            # sees a fork / join), so its backward runs beside the backbone's
-            if self.split_ode_wgrad == "ode" and stream is not None:
-                ws_stream = stream
-            else:
-                if getattr(self, "_wgrad_stream", None) is None:
-                    self._wgrad_stream = torch.cuda.Stream(static_state.device)
-                ws_stream = self._wgrad_stream
-            main = torch.cuda.current_stream(static_state.device)
-            ws_stream.wait_stream(main)
-            holder = {}
-            with torch.cuda.stream(ws_stream):
-                wtok = _ODEWeightGradFn.apply(w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"], w["b3"],
-                                              holder)
-            main.wait_stream(ws_stream)
         total = LyapODELossFn.apply(static_state, x_ode, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
-                                    w["b3"], h0, y, plan, oplan, p, stream, wtok, holder)
+                                    w["b3"], h0, y, plan, oplan, p, stream)
         sc = plan["scalars"]
         self.log("kappa", plan["kappa"])
         self.log("effective_batch_size", sc[1])

@@ -7,8 +7,12 @@ incremented as torch does, then ``fiode_adam_step`` applies torch's fused Adam f
 float32 ROCm tensors of a param group in a single launch (torch's fused multi-tensor Adam is ~3
 launches and ~50 us for the KWLarge model's 2.6 M parameters; this one streams p/g/m/v once).
 
-Groups the kernel does not cover (CPU or non-float32 parameters, amsgrad, differentiable, tensor
-lr, more than FIODE_ADAM_MAX_TENSORS tensors) go through torch's own Adam.step unchanged.
+A tensor lr (torch's way to schedule the learning rate under graph capture: LR schedulers update
+it in place) is read by the kernel on the device, so a captured step follows the schedule; a float
+lr is a launch argument, baked into a captured graph (GraphTrainStep refuses to replay after it
+changed).  Groups the kernel does not cover (CPU or non-float32 parameters, amsgrad,
+differentiable, more than FIODE_ADAM_MAX_TENSORS tensors, a tensor lr off the parameters' device)
+go through torch's own Adam.step unchanged.
 """
 from __future__ import annotations
 
@@ -24,11 +28,14 @@ MAX_TENSORS = 64          # FIODE_ADAM_MAX_TENSORS (include/fiode.h)
 
 
 def _kernel_ok(group, params: List[torch.Tensor]) -> bool:
-    if group["amsgrad"] or group["differentiable"] or torch.is_tensor(group["lr"]):
+    if group["amsgrad"] or group["differentiable"]:
         return False
     if not params or len(params) > MAX_TENSORS:
         return False
     dev = params[0].device
+    lr = group["lr"]
+    if torch.is_tensor(lr) and (lr.device != dev or lr.numel() != 1 or lr.dtype not in (torch.float32, torch.float64)):
+        return False
     for p in params:
         g = p.grad
         if (p.device != dev or dev.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous()
@@ -36,6 +43,30 @@ def _kernel_ok(group, params: List[torch.Tensor]) -> bool:
                 or g.device != dev):
             return False
     return True
+
+
+def _kernel_ok_params(opt, params: List[torch.Tensor]) -> bool:
+    """Whether the kernel will cover these parameters' updates (group settings, placement, dtype;
+    gradients are not looked at): what step_params needs."""
+    if not isinstance(opt, _KernelStepMixin):
+        return False
+    ids = {id(p) for p in params}
+    for group in opt.param_groups:
+        sel = [p for p in group["params"] if id(p) in ids]
+        if not sel:
+            continue
+        if group["amsgrad"] or group["differentiable"] or len(group["params"]) > MAX_TENSORS:
+            return False
+        dev = sel[0].device
+        lr = group["lr"]
+        if torch.is_tensor(lr) and (lr.device != dev or lr.numel() != 1
+                                    or lr.dtype not in (torch.float32, torch.float64)):
+            return False
+        if any(p.device != dev or dev.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous()
+               for p in sel):
+            return False
+        ids -= {id(p) for p in sel}
+    return not ids
 
 
 class _KernelStepMixin:
@@ -126,9 +157,13 @@ class _KernelStepMixin:
                 s += 1
             host_step = float(steps[0])
         beta1, beta2 = group["betas"]
+        lr = group["lr"]
+        lr_t = lr if torch.is_tensor(lr) else None
         cfg = L.AdamConfig(n, int(bool(group.get("decoupled_weight_decay", self._decoupled))),
-                           int(group["maximize"]), 0, float(group["lr"]), float(beta1), float(beta2),
-                           float(group["eps"]), float(group["weight_decay"]), host_step)
+                           int(group["maximize"]), 0, 0.0 if lr_t is not None else float(lr), float(beta1),
+                           float(beta2), float(group["eps"]), float(group["weight_decay"]), host_step,
+                           lr_t.data_ptr() if lr_t is not None else None,
+                           int(lr_t is not None and lr_t.dtype == torch.float64), 0)
         arr = ct.c_void_p * n
         step_ptrs = arr(*[s.data_ptr() for s in steps]) if all(on_dev) else None
         L.check(L.lib().fiode_adam_step(

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FIODE_ABI_VERSION 1
+#define FIODE_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define FIODE_API __attribute__((visibility("default")))
@@ -386,7 +386,10 @@ FIODE_API int fiode_spectral_cayley_backward(void* stream, const fiode_spectral_
  * fiode_amd/optim.py FiodeAdam): one launch updates every parameter tensor (adam.hip).  The host
  * arrays hold n_tensors device pointers each; tensors are contiguous float32 of numel[i] elements.
  * step: host array of device pointers to each tensor's step count after this step's increment
- * (capturable Adam; an entry or the array may be NULL: cfg->step is used). */
+ * (capturable Adam; an entry or the array may be NULL: cfg->step is used).  lr_dev (may be NULL):
+ * a device scalar holding the learning rate (torch's tensor lr, which LR schedulers update in
+ * place; float32, or float64 when lr_dev_is_double): read by the kernel at run time, so a captured
+ * step follows schedule changes; else cfg->lr (a value baked into a captured launch). */
 #define FIODE_ADAM_MAX_TENSORS 64
 typedef struct fiode_adam_config {
   int32_t n_tensors;
@@ -397,6 +400,9 @@ typedef struct fiode_adam_config {
    * lr / (1 - beta1^t) are formed in double, then rounded to the fp32 the update runs in */
   double lr, beta1, beta2, eps, weight_decay;
   double step;
+  const void* lr_dev;
+  int32_t lr_dev_is_double;
+  int32_t pad2_;
 } fiode_adam_config;
 FIODE_API int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float* const* params,
                               const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from fiode_amd import _lib
     lib = _lib.lib()
-    assert lib.fiode_abi_version() == 1
+    assert lib.fiode_abi_version() == _lib.ABI_VERSION == 2
     assert lib.fiode_error_string(2).decode().startswith("unsupported shape")
     cfg = _lib.LyapConfig(128, 256, 204, 1, 2, 2.0, 0, 0)
     dyn = _lib.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 30, 1e-4)

@@ -424,27 +424,6 @@ def test_batched_block_inverse_equals_single():
         assert torch.equal(inv[i], ops.block_inverse(Ms[i].contiguous()))
 
 
-def test_dense_cayley_group_equals_separate_maps():
-    """dense_cayley_group (one node, one batched inverse) = each map's _DenseCayleyFn, bit for bit,
-    forward and backward (the 4096 -> 512 and 512 -> 512 backbone shapes)."""
-    from fiode_amd.cayley import _DenseCayleyFn, dense_cayley_group
-    dev = _dev()
-    g = torch.Generator(device="cpu").manual_seed(11)
-    Ws = [torch.randn(512, 4096, generator=g).to(dev) * 0.02, torch.randn(512, 512, generator=g).to(dev) * 0.05]
-    als = [torch.tensor([1.5]).to(dev), torch.tensor([0.8]).to(dev)]
-    Gs = [torch.randn(W.shape, generator=g).to(dev) for W in Ws]
-    A = [W.clone().requires_grad_(True) for W in Ws]
-    Aa = [a.clone().requires_grad_(True) for a in als]
-    Qs = dense_cayley_group(A, Aa)
-    sum((Q * G).sum() for Q, G in zip(Qs, Gs)).backward()
-    for i in range(2):
-        W, a = Ws[i].clone().requires_grad_(True), als[i].clone().requires_grad_(True)
-        Q = _DenseCayleyFn.apply(W, a)
-        (Q * Gs[i]).sum().backward()
-        assert torch.equal(Q, Qs[i])
-        assert torch.equal(W.grad, A[i].grad) and torch.equal(a.grad, Aa[i].grad)
-
-
 @pytest.mark.parametrize("B,C,H,W,with_std", [(128, 3, 32, 32, True), (5, 3, 7, 9, True), (70, 2, 8, 8, False)])
 def test_normalize_hwcb_matches_torch(B, C, H, W, with_std):
     """Normalize on ROCm (fiode_normalize_hwcb): bit-identical to (x - mu) / std, returned as an
@@ -461,34 +440,19 @@ def test_normalize_hwcb_matches_torch(B, C, H, W, with_std):
     assert y.permute(2, 3, 1, 0).is_contiguous()
 
 
-def test_warm_inverse_converges_and_falls_back():
-    """_warm_inverse (training-step dense maps): from the previous step's inverse, Newton-Schulz
-    refinement matches the exact elimination to float32 accuracy and skips it on the device; from a
-    useless start (zeros: residual 1) the exact elimination runs (fiode_block_inverse_cond)."""
-    from fiode_amd import cayley as CY, ops
-    dev = torch.device("cuda:0")
-    g = torch.Generator().manual_seed(11)
-    W = (torch.randn(512, 512, generator=g) / 512 ** 0.5).to(dev)
-    alpha = torch.tensor([W.norm().item()], device=dev)
-    st, M = CY._dense_prep(W, alpha)
-    exact = ops.block_inverse(M.reshape(512, 512)).clone()
-    cache = {}
-    first = CY._warm_inverse(M, cache)                   # no previous inverse: exact
-    torch.testing.assert_close(first.reshape(512, 512), exact, rtol=0, atol=0)
-    # a nearby system (the weights after a small step)
-    W2 = W + 1e-3 * (torch.randn(512, 512, generator=g) / 512 ** 0.5).to(dev)
-    st2, M2 = CY._dense_prep(W2, alpha)
-    exact2 = ops.block_inverse(M2.reshape(512, 512)).clone()
-    warm = CY._warm_inverse(M2, cache).reshape(512, 512)
+def test_conditional_block_inverse_skip_flag():
+    """fiode_block_inverse_cond: with the device skip flag set every launch of the elimination
+    returns at once (the output buffer keeps what the caller put there); with it clear the result
+    is the unconditional inverse, bit for bit."""
+    from fiode_amd import ops
+    dev = _dev()
+    M = _system(1, 256, torch.float32, dev, scale=3.0, seed=4)[0].float().contiguous()
+    exact = ops.block_inverse(M)
+    out = torch.full_like(M, 7.0)
+    skip = torch.ones(1, dtype=torch.int32, device=dev)
+    ops.block_inverse(M, out=out, skip=skip)
     torch.cuda.synchronize()
-    assert int(cache["skip"]) == 1                        # converged: the elimination was skipped
-    scale = float(exact2.abs().max())
-    assert float((warm - exact2).abs().max()) / scale < 2e-5
-    eye = torch.eye(512, device=dev)
-    assert float(torch.linalg.matrix_norm(eye - M2.reshape(512, 512) @ warm, ord=float("inf"))) <= 1e-4
-    # useless start: falls back to the exact elimination, bit for bit
-    cache["X"].zero_()
-    fb = CY._warm_inverse(M2, cache).reshape(512, 512)
-    torch.cuda.synchronize()
-    assert int(cache["skip"]) == 0
-    assert torch.equal(fb, exact2)
+    assert bool((out == 7.0).all())
+    skip.zero_()
+    ops.block_inverse(M, out=out, skip=skip)
+    assert torch.equal(out, exact)

@@ -6,15 +6,6 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _copy_inv_cache(src, dst):
-    """The dense Cayley maps' warm-start inverses (cayley._warm_inverse) are step state too: the twin
-    that replays a step eagerly starts from the same ones."""
-    from fiode_amd.cayley import CayleyLinear
-    for a, b in zip([m for m in src.modules() if isinstance(m, CayleyLinear)],
-                    [m for m in dst.modules() if isinstance(m, CayleyLinear)]):
-        b._inv_cache = {k: v.detach().clone() for k, v in a._inv_cache.items() if torch.is_tensor(v)}
-
-
 def _dev():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
@@ -37,7 +28,6 @@ def test_graph_replay_matches_eager_step(train_ode):
     twin.load_state_dict(mod.state_dict())
     twin.rng_counter = mod.rng_counter.clone()
     twin.seed = mod.seed
-    _copy_inv_cache(mod, twin)
     c0 = int(mod.rng_counter)
     loss = gs.step()
     torch.cuda.synchronize()
@@ -85,7 +75,6 @@ def test_graph_warmup_leaves_no_updates():
     twin.load_state_dict(before)
     twin.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
     twin.seed = mod.seed
-    _copy_inv_cache(mod, twin)
     topt = twin.configure_optimizers(capturable=True)[0][0]
     gs.step()
     topt.zero_grad(set_to_none=True)
@@ -96,11 +85,14 @@ def test_graph_warmup_leaves_no_updates():
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=k)
 
 
-@pytest.mark.parametrize("train_ode", [False, True])
-def test_maps_ahead_equal_step_start_maps(train_ode):
+@pytest.mark.parametrize("train_ode,reuse", [(False, True), (True, True), (True, False)])
+def test_maps_ahead_equal_step_start_maps(train_ode, reuse):
     """GraphTrainStep(maps_ahead=True) -- each conv layer's Cayley map for the next step computed
     inside the current one, right after the layer's early Adam update -- gives the same losses and
-    parameters, bit for bit, as maps computed at the start of every step, over several replays."""
+    parameters, bit for bit, as maps computed at the start of every step, over several replays.
+    With the reference-order second backbone pass (ode_reuse_features False) every conv map is used
+    twice per step: there the early per-layer update is off and the maps are refreshed after the
+    optimizer step (still bit-identical)."""
     import bench
     from fiode_amd.graph_step import GraphTrainStep
     dev = _dev()
@@ -108,18 +100,89 @@ def test_maps_ahead_equal_step_start_maps(train_ode):
     x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (32,), generator=g).to(dev)
     out = {}
-    for ahead in ("conv", "conv+linear", "conv+small", None):
+    for ahead in (True, False):
         mod = bench.build_module(dev, seed=0, train_ode=train_ode)
+        mod.ode_reuse_features = reuse
         mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         opt = mod.configure_optimizers(capturable=True)[0][0]
-        gs = GraphTrainStep(mod, opt, x, y, warmup=2, maps_ahead=ahead is not None,
-                            maps_ahead_linear={"conv+linear": True, "conv+small": "small"}.get(ahead, False))
-        assert len(gs.piped) == {"conv": 4, "conv+linear": 7, "conv+small": 5, None: 0}[ahead]
+        gs = GraphTrainStep(mod, opt, x, y, warmup=2, maps_ahead=ahead)
+        assert len(gs.piped) == (4 if ahead else 0)
+        assert gs.early == (ahead and (reuse or not train_ode))
         losses = [float(gs.step()) for _ in range(3)]
         torch.cuda.synchronize()
         out[ahead] = (losses, [p.detach().clone() for p in mod.parameters()])
         gs.close()
-    for ahead in ("conv", "conv+linear", "conv+small"):
-        assert out[ahead][0] == out[None][0], ahead
-        for a, b in zip(out[ahead][1], out[None][1]):
-            assert torch.equal(a, b), ahead
+    assert out[True][0] == out[False][0]
+    for a, b in zip(out[True][1], out[False][1]):
+        assert torch.equal(a, b)
+
+
+def test_float_lr_change_refused_tensor_lr_followed():
+    """A float lr is baked into the captured optimizer step: changing it after capture makes step()
+    raise instead of silently replaying the old value.  A tensor lr (capturable LR scheduling) is read
+    on the device: a scheduler's in-place change is followed by the replays (the replayed step equals
+    an eager step of a twin at the new lr)."""
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(8)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    mod = bench.build_module(dev, seed=0, train_ode=False)
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y, warmup=1)
+    gs.step()
+    opt.param_groups[0]["lr"] = 1e-3
+    with pytest.raises(RuntimeError, match="learning rate changed"):
+        gs.step()
+    gs.close()
+    from fiode_amd.optim import FiodeAdam
+    res = {}
+    for lr_kind in ("tensor", "float"):
+        m = bench.build_module(dev, seed=0, train_ode=False)
+        m.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        params = list(m.parameters())
+        lr0 = torch.tensor(5e-3, device=dev) if lr_kind == "tensor" else 5e-3
+        o = FiodeAdam(params, lr=lr0, capturable=True, fused=True)
+        if lr_kind == "tensor":
+            st = GraphTrainStep(m, o, x, y, warmup=1)
+            st.step()
+            lr0.fill_(1e-3)                      # what a scheduler does to a tensor lr
+            st.step()
+            st.close()
+        else:
+            st = GraphTrainStep(m, o, x, y, warmup=1)
+            st.step()
+            st.close()
+            for pg in o.param_groups:
+                pg["lr"] = 1e-3
+            st = GraphTrainStep(m, o, x, y, warmup=1)      # recapture at the new float lr
+            st.step()
+            st.close()
+        torch.cuda.synchronize()
+        res[lr_kind] = [p.detach().clone() for p in params]
+    for a, b in zip(res["tensor"], res["float"]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+
+
+def test_graph_replays_without_runtime_queue_override():
+    """The captured configs[1] step (bench shape: B=128, S=256, train_ode rk4) replays correctly
+    with the HIP runtime's own graph-executor settings: DEBUG_HIP_FORCE_GRAPH_QUEUES is not set in
+    this process (bench.py sets it only as a tuning default when run as the program).  30 replays,
+    every loss finite, the device status clean."""
+    import os
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    assert "DEBUG_HIP_FORCE_GRAPH_QUEUES" not in os.environ
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    mod = bench.build_module(dev, seed=0, train_ode=True)
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y)
+    losses = torch.stack([gs.step().detach().clone() for _ in range(30)])
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(losses).all())
+    gs.check_status()
+    assert mod.device_status() == 0

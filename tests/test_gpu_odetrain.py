@@ -127,21 +127,17 @@ def test_fused_loss_node_equals_three_nodes(reuse):
     """LyapODELossFn (the configs[1] loss as one autograd node) = the three-node graph
     (LyapunovLossFn + ODETrainFn + ODELossMixFn): same loss and the same gradients bit for bit --
     the node sums ode + lyap * ((1 - p) go) exactly as autograd's accumulation does, with the same
-    Philox draws (same seed / offset) and the solve on its side stream in both.  Also with the
-    node's weight gradients split off into their own node on another stream."""
+    Philox draws (same seed / offset) and the solve on its side stream in both."""
     import bench
     dev = _dev()
     x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
     yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
     out = {}
-    for variant in ("fused", "split", "three"):
+    for variant in ("fused", "three"):
         mod = bench.build_module(dev, seed=0, train_ode=True)
         mod.parallel_cayley = False
         mod.ode_reuse_features = reuse
         mod.fused_ode_loss = variant != "three"
-        # "split": the node's weight gradients as a second node on its own stream (_ODEWeightGradFn,
-        # fiode_odetrain_backward_x / _weights)
-        mod.split_ode_wgrad = "own" if variant == "split" else False
         mod._rng_offset = 0
         loss = mod.compute_loss(x, yb, 32, "relu")
         loss.backward()
@@ -153,16 +149,27 @@ def test_fused_loss_node_equals_three_nodes(reuse):
     assert torch.equal(la, lb) and oa == ob
     for n in ga:
         assert torch.equal(ga[n], gb[n]), n
-    # the split node's dL/dx_feat comes from k_ot_gx (fiode_odetrain_backward_x) instead of the
-    # weight-gradient chain: the same sum in another order, so the backbone's gradients agree to
-    # float32 rounding (the dynamics' weight gradients are identical)
-    la, oa, ga = out["split"]
-    assert torch.equal(la, lb) and oa == ob
-    for n in ga:
-        if n.startswith("model.dyn_fun."):
-            assert torch.equal(ga[n], gb[n]), n
-        else:
-            torch.testing.assert_close(ga[n], gb[n], rtol=1e-4, atol=1e-6 * float(gb[n].abs().max()) + 1e-12)
+
+
+def test_split_backward_entry_points_equal_one_call():
+    """fiode_odetrain_backward_x (adjoint sweep + dL/dx_feat in k_ot_gx) followed by
+    fiode_odetrain_backward_weights = the one-call fiode_odetrain_backward: the weight gradients bit
+    for bit; dL/dx_feat is the same sum in another order (float32 rounding)."""
+    ops, dev, P, x, h0, labels, cfg, E, masks, w, dyn = _case(128, 0.1, False, 31)
+    xt, h0t = torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev)
+    mk = torch.from_numpy(masks).to(dev)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    gy = torch.randn(128, 10, generator=g).to(dev)
+    y, st, ws = ops.odetrain_forward(xt, h0t, w, dyn, cfg, masks=mk)
+    one, _ = ops.odetrain_backward(gy, xt, w, dyn, cfg, ws)
+    one = {k: v.clone() for k, v in one.items()}
+    y, st, ws = ops.odetrain_forward(xt, h0t, w, dyn, cfg, masks=mk)
+    gx = ops.odetrain_backward_x(gy, xt, w, dyn, cfg, ws)
+    wg = ops.odetrain_backward_weights(xt, w, dyn, cfg, ws)
+    torch.cuda.synchronize()
+    for k in KEYS:
+        assert torch.equal(wg[k], one[k]), k
+    torch.testing.assert_close(gx, one["x_feat"], rtol=1e-5, atol=1e-6 * float(one["x_feat"].abs().max()))
 
 
 @pytest.mark.parametrize("B", [1, 128, 300])

@@ -96,3 +96,43 @@ def test_fiode_adam_graph_replay_equals_eager():
     for x, y in zip(a, b):
         assert torch.equal(x.detach(), y.detach())
     assert float(oa.state[a[0]]["step"]) == 5.0
+
+
+def test_tensor_lr_followed_by_captured_step():
+    """A tensor lr (torch's capturable LR scheduling: schedulers update it in place) is read by the
+    kernel on the device, so a captured step follows a change made between replays; the values equal
+    torch's Adam run eagerly with the same float lr sequence."""
+    ps, _ = _params(4)
+    a = [torch.nn.Parameter(p.to(DEV)) for p in ps]
+    b = [torch.nn.Parameter(p.to(DEV)) for p in ps]
+    lr_t = torch.tensor(1e-3, device=DEV)
+    oa = FiodeAdam(a, lr=lr_t, capturable=True)
+    ob = torch.optim.Adam(b, lr=1e-3, capturable=True)
+    grads = [torch.zeros_like(x) for x in a]
+    for x, gr in zip(a, grads):
+        x.grad = gr
+    for y in b:
+        y.grad = torch.zeros_like(y)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        oa.step()
+    torch.cuda.current_stream().wait_stream(s)
+    ob.step()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        oa.step()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    for lr in (1e-3, 4e-3, 2.5e-4):
+        lr_t.fill_(lr)                              # what CosineAnnealingLR / MultiStepLR do to a tensor lr
+        for pg in ob.param_groups:
+            pg["lr"] = lr
+        for gr, y in zip(grads, b):
+            r = torch.randn(gr.shape, generator=g, device=DEV)
+            gr.copy_(r)
+            y.grad.copy_(r)
+        graph.replay()
+        ob.step()
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x.detach(), y.detach(), rtol=RTOL, atol=ATOL)
