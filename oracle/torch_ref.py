@@ -75,8 +75,11 @@ class _PinnedActiveSet(Function):
     noise for inactive coordinates (see fiode_oracle.eval_dot), so chained checks pin it."""
 
     @staticmethod
-    def forward(ctx, lower, nominal, act):
-        v = _NoUpperProjection.forward(ctx, lower, nominal)
+    def forward(ctx, lower, nominal, act, mu=None):
+        if mu is None:
+            v = _NoUpperProjection.forward(ctx, lower, nominal)
+        else:       # the exit iteration's mu pinned too: v = max(nominal - mu, lower) (:242-244)
+            v = torch.maximum(nominal - mu.to(nominal.dtype)[:, None], lower)
         ctx.act = act
         return v
 
@@ -87,11 +90,11 @@ class _PinnedActiveSet(Function):
         cnt = na.sum(dim=-1, keepdim=True).to(g.dtype)
         corr = torch.where(cnt > 0, (g * na).sum(dim=-1, keepdim=True) / cnt.clamp(min=1), torch.zeros_like(cnt))
         d = g - corr
-        return torch.where(act, d, torch.zeros_like(d)), torch.where(act, torch.zeros_like(d), d), None
+        return torch.where(act, d, torch.zeros_like(d)), torch.where(act, torch.zeros_like(d), d), None, None
 
 
 def eval_dot(h, x_rows, W: Dict[str, torch.Tensor], alpha_1, alpha_2, sigma_1, scale_nominal,
-             mask1=None, mask2=None, p=0.5, stash=None, act=None):
+             mask1=None, mask2=None, p=0.5, stash=None, act=None, mu=None):
     """classification.py:96-115 (eval_dot) with dropout masks injected.  ``stash`` (a dict)
     receives the QP inputs (lower, nominal) so a checker can pin the QP's active-set test."""
     z = F.linear(h, W["Q1"], W["b1"]) + F.linear(x_rows, W["Qx"], W["bx"])
@@ -111,7 +114,7 @@ def eval_dot(h, x_rows, W: Dict[str, torch.Tensor], alpha_1, alpha_2, sigma_1, s
         stash["lower"] = lower.detach().clone()
         stash["nominal"] = ft.detach().clone()
     if act is not None:
-        return _PinnedActiveSet.apply(lower, ft, act)
+        return _PinnedActiveSet.apply(lower, ft, act, mu)
     return _NoUpperProjection.apply(lower, ft)
 
 
@@ -185,11 +188,13 @@ def rk4_grid32(t0: float, t1: float, step_size: float):
 
 
 def ode_train_loss(x_feat, h0, y, W: Dict[str, torch.Tensor], masks, t0=0.0, t1=1.0, step_size=0.1, *,
-                   alpha_1=100.0, alpha_2=20.0, sigma_1=0.02, scale_nominal=True, p=0.5, acts=None):
+                   alpha_1=100.0, alpha_2=20.0, sigma_1=0.02, scale_nominal=True, p=0.5, acts=None, mus=None):
     """pl_modules.py:490-497: y_hat = odeint(h_dot, h0, [t0, t1], method='rk4', step_size) in train
     mode (torchdiffeq 0.2.2 rk4_alt_step_func op order), loss_ode = nll_loss(log(y_hat), y).
     masks: [E,2,B,M] uint8 keep masks per func() call; acts: optional per-eval pinned QP active
-    sets [E][B,C] bool.  Returns (loss_ode, y_hat)."""
+    sets [E][B,C] bool; mus: optional per-eval pinned exit mu [E][B] (with acts: the linearisation
+    points of another implementation's forward, so a float64 run checks its float32 backward).
+    Returns (loss_ode, y_hat)."""
     grid = rk4_grid32(t0, t1, step_size)
     third = 1.0 / 3.0
     e = [0]
@@ -200,7 +205,7 @@ def ode_train_loss(x_feat, h0, y, W: Dict[str, torch.Tensor], masks, t0=0.0, t1=
         m1 = masks[i, 0] if masks is not None else None
         m2 = masks[i, 1] if masks is not None else None
         return eval_dot(hh, x_feat, W, alpha_1, alpha_2, sigma_1, scale_nominal, m1, m2, p,
-                        act=None if acts is None else acts[i])
+                        act=None if acts is None else acts[i], mu=None if mus is None else mus[i])
     yy = h0
     for a, b in zip(grid[:-1], grid[1:]):
         dt = b - a

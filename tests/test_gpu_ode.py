@@ -102,7 +102,8 @@ def test_ivp_forward_through_module():
 def test_dopri5_large_batch_matches_oracle(B):
     """BASELINE configs[4]'s validation solve size (dopri5 tol 1e-3, models.py:235-241): the solve
     runs one workgroup per 16-row tile (>= B/32 CUs), same NFE / accepted / rejected steps as the
-    oracle's torchdiffeq-0.2.2 restatement, states within 1e-3."""
+    oracle's torchdiffeq-0.2.2 restatement, states within 2e-4 (as at B=128: with the step sequence
+    identical only the MLP's float32 rounding differs)."""
     ops, dev, P, x, h0, cfg, w = _setup(B, 30 + B // 1024, False)
     times = O.linspace32(0.0, 1.0, 2)
     ref, st_ref = O.dopri5(O.make_ode_func(x, P, cfg), h0, 0.0, 1.0, rtol=1e-3, atol=1e-3, times=times)
@@ -115,7 +116,7 @@ def test_dopri5_large_batch_matches_oracle(B):
     assert s[6] >= B // 32 and s[6] * s[7] * 16 >= B, s       # workgroups x tiles x 16 rows cover B
     assert (s[0], s[1], s[2]) == (st_ref.nfe, st_ref.n_accept, st_ref.n_reject), (s[:3], st_ref)
     err = float(np.abs(sol.cpu().numpy() - ref).max())
-    assert err <= 1e-3, err
+    assert err <= 2e-4, err
 
 
 @pytest.mark.parametrize("B,method", [(8192, "dopri5"), (5000, "rk4")])

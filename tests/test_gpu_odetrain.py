@@ -4,10 +4,11 @@ oracle.fiode_oracle.rk4_train) and torch autograd through the reference-order RK
 (oracle.torch_ref.ode_train_loss) with the same dropout masks.
 
 Tolerances: forward 2e-4 absolute on the simplex state (MLP accumulation order can move a
-stage's batch-global QP exit by one bisection step, as in test_gpu_ode).  Gradients: relative
-2e-3 of each tensor's max-abs (float32 chains of 40 stage VJPs, MFMA vs torch accumulation
-order); the QP active sets of the torch autograd are pinned to the device's (v, mu, nominal),
-because the reference's active-set test is float32 rounding noise on inactive coordinates."""
+stage's batch-global QP exit by one bisection step, as in test_gpu_ode).  Gradients: 2e-4 of each
+tensor's max-abs against float64 torch autograd through the reference-order RK4 stages, evaluated
+at the device's linearisation points: the QP active sets (the reference's active-set test is
+float32 rounding noise on inactive coordinates) and each eval's exit mu are pinned to the
+device's, so the remaining difference is the device's float32 rounding over 40 stage VJPs."""
 import numpy as np
 import pytest
 import torch
@@ -71,19 +72,22 @@ def test_backward_matches_torch_autograd(B, step, scale_nominal):
     sv = ops.odetrain_saved(ws, cfg)
     act = ((sv["v"] - sv["nominal"]) + sv["mu"][..., None] > 0).cpu()          # [B,E,C]
     acts = [act[:, e] for e in range(E)]
-    leaves = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).clone().requires_grad_(True) for k in KEYS}
-    xf = torch.from_numpy(x).clone().requires_grad_(True)
-    loss, yy = T.ode_train_loss(xf, torch.from_numpy(h0), torch.from_numpy(labels), leaves, torch.from_numpy(masks),
-                                0.0, 1.0, step, scale_nominal=scale_nominal, p=0.5, acts=acts)
+    mus = [sv["mu"][:, e].double().cpu() for e in range(E)]
+    # float64 autograd at the device's linearisation points (QP active sets and exit mu pinned)
+    leaves = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).double().requires_grad_(True) for k in KEYS}
+    xf = torch.from_numpy(x).double().requires_grad_(True)
+    loss, yy = T.ode_train_loss(xf, torch.from_numpy(h0).double(), torch.from_numpy(labels), leaves,
+                                torch.from_numpy(masks), 0.0, 1.0, step, scale_nominal=scale_nominal, p=0.5, acts=acts,
+                                mus=mus)
     loss.backward()
     ref = {k: leaves[k].grad for k in KEYS}
     ref["x_feat"] = xf.grad
     for k in KEYS + ("x_feat",):
-        g = grads[k].cpu()
+        g = grads[k].cpu().double()
         r = ref[k]
         scale = float(r.abs().max()) + 1e-12
         err = float((g - r).abs().max()) / scale
-        assert err <= 2e-3, (k, err, scale)
+        assert err <= 2e-4, (k, err, scale)
 
 
 def test_philox_masks_fresh_per_offset():
