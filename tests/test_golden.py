@@ -98,7 +98,7 @@ def test_gpu_lyap_step_matches_fixture():
     db = {k: v.cpu().numpy() for k, v in dbg.items()}
     assert np.array_equal(db["V"], d["V"])
     P = O.DynParams(**{k: np.ascontiguousarray(d["P_" + k]) for k in ops.WEIGHT_KEYS})
-    inp = O.StepInputs(x_feat=d["x_feat"], y=d["y"], h=d["h"], mask1=d["mask1"], mask2=d["mask2"],
+    inp = O.StepInputs(x_feat=d["x_feat"], y=d["y"], h=d["h"], S=S, mask1=d["mask1"], mask2=d["mask2"],
                        lmask1=d["lmask1"], lmask2=d["lmask2"], kappa=float(d["kappa"]))
     free = O.lyapunov_step(inp, P, O.DynConfig())
     inp.qp_inputs = (db["qp_lower"], db["qp_nominal"][0])
