@@ -194,7 +194,7 @@ __device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const
 //     and its slope -k there (Newton from the all-active root mean(nom): 3 steps, no sorting);
 //   * six points around mu* -- where the exact sum is +-(tol +- d) and +-d, d = FIODE_QP_CERT_ULPS
 //     ulps of the terms' magnitude -- each CERTIFIED by one qp_eps evaluation (a point whose
-//     evaluation does not confirm its side is replaced by -+inf: no claim);
+//     evaluation does not confirm its side is replaced by NaN: no claim);
 //   * per bisection iteration the decisions (eps > 0, eps < 0, |eps| < tol) are then comparisons
 //     of the midpoint with the certified points, bit-identical to evaluating eps_fl there; only a
 //     midpoint in an uncertified band (|eps| within d of 0 or of tol) takes the direct evaluation.
@@ -248,13 +248,15 @@ __device__ __forceinline__ void qp_thresholds(const float (&lower)[C], const flo
   const float pD = mu + d * rk, pE = mu + (tol - d) * rk, pF = mu + (tol + d) * rk;
   const float eA = qp_eps(lower, nom, pA), eB = qp_eps(lower, nom, pB), eC = qp_eps(lower, nom, pC);
   const float eD = qp_eps(lower, nom, pD), eE = qp_eps(lower, nom, pE), eF = qp_eps(lower, nom, pF);
-  const float inf = __builtin_inff();
-  t.A = eA >= tol ? pA : -inf;
-  t.B = eB < tol ? pB : inf;
-  t.Cc = eC > 0.f ? pC : -inf;
-  t.D = eD < 0.f ? pD : inf;
-  t.E = eE > -tol ? pE : -inf;
-  t.F = eF <= -tol ? pF : inf;
+  // an uncertified point becomes NaN: every comparison with it is false, so it claims nothing
+  // (an infinite sentinel would still claim mu = +-inf)
+  const float none = __builtin_nanf("");
+  t.A = eA >= tol ? pA : none;
+  t.B = eB < tol ? pB : none;
+  t.Cc = eC > 0.f ? pC : none;
+  t.D = eD < 0.f ? pD : none;
+  t.E = eE > -tol ? pE : none;
+  t.F = eF <= -tol ? pF : none;
 }
 
 // Iterations [0, to] of qp_bisect_seq (from its bracket), decided by the certified thresholds.  A
