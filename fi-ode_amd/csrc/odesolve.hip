@@ -23,11 +23,13 @@
 #include "common.h"
 #include "tile.h"
 #include "tile16.h"
+#include "dopri5.h"
 #include "../../include/fiode.h"
 
 namespace {
 using namespace fiode_tile;
 using namespace fiode_t16;
+using namespace fiode_dp;
 
 constexpr int OS_TMAX = 16;      // tiles per workgroup (LDS: 3.5 KB per tile)
 constexpr int OS_XV = 4;         // float64 values per reduction exchange (at most)
@@ -202,17 +204,6 @@ struct StageIn {
   int i;           // dopri5 stage (IN_DP)
   float dt;        // step (rk4, dopri5) or h0 (IN_H0)
 };
-
-// torchdiffeq 0.2.2 dopri5 tableau (float32 copies, as RKAdaptiveStepsizeODESolver casts it)
-__device__ const float DP_BETA[6][6] = {
-    {1.0f / 5, 0, 0, 0, 0, 0},
-    {3.0f / 40, 9.0f / 40, 0, 0, 0, 0},
-    {(float)(44.0 / 45), (float)(-56.0 / 15), (float)(32.0 / 9), 0, 0, 0},
-    {(float)(19372.0 / 6561), (float)(-25360.0 / 2187), (float)(64448.0 / 6561), (float)(-212.0 / 729), 0, 0},
-    {(float)(9017.0 / 3168), (float)(-355.0 / 33), (float)(46732.0 / 5247), (float)(49.0 / 176),
-     (float)(-5103.0 / 18656), 0},
-    {(float)(35.0 / 384), 0, (float)(500.0 / 1113), (float)(125.0 / 192), (float)(-2187.0 / 6784),
-     (float)(11.0 / 84)}};
 
 // The float32 expression orders of the oracle / torchdiffeq: rk4_alt_step_func (3/8 rule) and the
 // dopri5 stage sums acc = sum_j k_j (beta_ij dt), y_i = y + acc.
@@ -425,15 +416,6 @@ __device__ void os_rk4(const OsArgs& a, const float* Q2s, const float* Q3s, OsSh
     __syncthreads();
   }
 }
-
-__device__ const float DP_CERR[7] = {(float)(35.0 / 384 - 1951.0 / 21600), 0, (float)(500.0 / 1113 - 22642.0 / 50085),
-                                     (float)(125.0 / 192 - 451.0 / 720), (float)(-2187.0 / 6784 - -12231.0 / 42400),
-                                     (float)(11.0 / 84 - 649.0 / 6300), (float)(-1.0 / 60.0)};
-__device__ const float DP_CMID[7] = {(float)(6025192743.0 / 30085553152.0 / 2), 0,
-                                     (float)(51252292925.0 / 65400821598.0 / 2),
-                                     (float)(-2691868925.0 / 45128329728.0 / 2),
-                                     (float)(187940372067.0 / 1594534317056.0 / 2),
-                                     (float)(-1776094331.0 / 19743644256.0 / 2), (float)(11237099.0 / 235043384.0 / 2)};
 
 __device__ __forceinline__ float rms_from_sum(double sumsq, size_t n) { return (float)sqrt(sumsq / (double)n); }
 

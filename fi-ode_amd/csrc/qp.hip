@@ -9,37 +9,10 @@
 // and re-runs each row to exactly iteration K.
 #include "common.h"
 #include "tile.h"
-#include "tile16.h"
 #include "../../include/fiode.h"
 
 namespace {
 using namespace fiode_tile;
-
-// The certified-threshold bisection of the persistent solves (tile16.h qp_thresholds /
-// qp_bisect_thr / qp_bisect_frozen) on arbitrary rows, one row per lane, all `iters` iterations:
-// every midpoint and the 64-row wave's convergence mask, for the parity test against the plain
-// sequential bisection.
-__global__ __launch_bounds__(64) void k_qp_trace(int n, const float* lower, const float* nominal, float tol,
-                                                 int iters, float* mu_out, uint32_t* mask_out) {
-  __shared__ float rec[64][33];
-  const int lane = threadIdx.x;
-  const int r = blockIdx.x * 64 + lane;
-  const bool valid = r < n;
-  const int rr = valid ? r : n - 1;
-  float lo_[C], nm[C];
-  load_row10(lower + (size_t)rr * C, lo_);
-  load_row10(nominal + (size_t)rr * C, nm);
-  float lo, hi;
-  fiode_t16::qp_bracket(lo_, nm, lo, hi);
-  fiode_t16::QpThr th;
-  fiode_t16::qp_thresholds(lo_, nm, tol, th);
-  int fz;
-  const uint32_t conv = fiode_t16::qp_bisect_thr(lo_, nm, iters - 1, tol, th, lo, hi, &rec[lane][0], valid, fz);
-  fiode_t16::qp_bisect_frozen(lo_, nm, iters - 1, lo, hi, &rec[lane][0], fz);
-  if (valid)
-    for (int it = 0; it < iters; ++it) mu_out[(size_t)r * iters + it] = rec[lane][it];
-  if (lane == 0) mask_out[blockIdx.x] = conv;
-}
 
 __global__ __launch_bounds__(256) void k_qp_mask(int n, const float* lower, const float* nominal, int max_iter,
                                                  float tol, uint32_t* word) {
@@ -244,15 +217,3 @@ extern "C" const char* fiode_error_string(int code) {
 }
 
 extern "C" int fiode_abi_version(void) { return FIODE_ABI_VERSION; }
-
-extern "C" int fiode_qp_bisect_trace(void* stream, int32_t n, int32_t c, const float* lower, const float* nominal,
-                                     int32_t iters, float tol, float* mu, uint32_t* wave_masks) {
-  if (c != FIODE_C) return FIODE_ESHAPE;
-  if (n < 0 || iters < 1 || iters > 32) return FIODE_EINVAL;
-  if (n == 0) return FIODE_OK;
-  if (!lower || !nominal || !mu || !wave_masks) return FIODE_EINVAL;
-  hipLaunchKernelGGL(k_qp_trace, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, lower, nominal,
-                     tol, iters, mu, wave_masks);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
-}

@@ -185,139 +185,6 @@ __device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const
   return ~wave_or16(open) & span;
 }
 
-// ---- the same bisection decided by certified thresholds --------------------------------------
-// eps_fl(mu) = qp_eps above is a NON-INCREASING function of the float mu: every term
-// max(fl(nom_j - mu), lower_j) is (rounding is monotone) and fl(a + b) is non-decreasing in each
-// operand.  So one evaluation eps_fl(m) > 0 certifies eps_fl(mu) > 0 for EVERY mu <= m, and so on
-// for < 0 and the +-tol tests.  Per row and eval:
-//   * the exact-arithmetic root mu* of the piecewise-linear, convex sum_j max(nom_j - mu, lower_j)
-//     and its slope -k there (Newton from the all-active root mean(nom): 3 steps, no sorting);
-//   * six points around mu* -- where the exact sum is +-(tol +- d) and +-d, d = FIODE_QP_CERT_ULPS
-//     ulps of the terms' magnitude -- each CERTIFIED by one qp_eps evaluation (a point whose
-//     evaluation does not confirm its side is replaced by NaN: no claim);
-//   * per bisection iteration the decisions (eps > 0, eps < 0, |eps| < tol) are then comparisons
-//     of the midpoint with the certified points, bit-identical to evaluating eps_fl there; only a
-//     midpoint in an uncertified band (|eps| within d of 0 or of tol) takes the direct evaluation.
-// The decisions never depend on how good mu* is (only how often the direct evaluation runs):
-// NaN inputs give NaN thresholds, every comparison false, and the plain bisection.
-#ifndef FIODE_QP_THRESH
-#define FIODE_QP_THRESH 1         // 0: the sequential bisection everywhere (A/B builds)
-#endif
-#ifndef FIODE_QP_CERT_ULPS
-#define FIODE_QP_CERT_ULPS 8.0f
-#endif
-struct QpThr {
-  float A;    // mu <= A:       eps >= tol   (|eps| < tol false, eps > 0)
-  float B;    // mu >= B:       eps <  tol
-  float Cc;   // mu <= Cc:      eps >  0
-  float D;    // mu >= D:       eps <  0
-  float E;    // mu <= E:       eps > -tol
-  float F;    // mu >= F:       eps <= -tol
-};
-
-__device__ __forceinline__ void qp_thresholds(const float (&lower)[C], const float (&nom)[C], float tol, QpThr& t) {
-  float b[C];
-  float sl = 0.f, sn = 0.f;
-#pragma unroll
-  for (int j = 0; j < C; ++j) {
-    b[j] = nom[j] - lower[j];
-    sl += lower[j];
-    sn += nom[j];
-  }
-  float mu = sn * (1.0f / C);          // the root if every coordinate is on its nominal side
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {         // Newton on the convex non-increasing sum (monotone from a side)
-    float e = sl, k = 0.f;
-#pragma unroll
-    for (int j = 0; j < C; ++j) {
-      const float tj = b[j] - mu;
-      e += fmaxf(tj, 0.f);
-      k += tj > 0.f ? 1.f : 0.f;
-    }
-    mu = k > 0.f ? mu + e * __builtin_amdgcn_rcpf(k) : mu;
-  }
-  float k = 0.f, mag = 0.f;
-#pragma unroll
-  for (int j = 0; j < C; ++j) {
-    k += b[j] - mu > 0.f ? 1.f : 0.f;
-    mag += fabsf(nom[j] - mu) + fabsf(lower[j]);
-  }
-  const float rk = __builtin_amdgcn_rcpf(fmaxf(k, 1.f));
-  const float d = FIODE_QP_CERT_ULPS * 0x1p-24f * mag;
-  const float pA = mu - (tol + d) * rk, pB = mu - (tol - d) * rk, pC = mu - d * rk;
-  const float pD = mu + d * rk, pE = mu + (tol - d) * rk, pF = mu + (tol + d) * rk;
-  const float eA = qp_eps(lower, nom, pA), eB = qp_eps(lower, nom, pB), eC = qp_eps(lower, nom, pC);
-  const float eD = qp_eps(lower, nom, pD), eE = qp_eps(lower, nom, pE), eF = qp_eps(lower, nom, pF);
-  // an uncertified point becomes NaN: every comparison with it is false, so it claims nothing
-  // (an infinite sentinel would still claim mu = +-inf)
-  const float none = __builtin_nanf("");
-  t.A = eA >= tol ? pA : none;
-  t.B = eB < tol ? pB : none;
-  t.Cc = eC > 0.f ? pC : none;
-  t.D = eD < 0.f ? pD : none;
-  t.E = eE > -tol ? pE : none;
-  t.F = eF <= -tol ? pF : none;
-}
-
-// Iterations [0, to] of qp_bisect_seq (from its bracket), decided by the certified thresholds.  A
-// lane whose midpoint falls in the uncertified sign band while its whole bracket already lies in
-// the certified |eps| < tol region is FROZEN there: its later convergence bits are known (every
-// later midpoint lies in the bracket), only its exact midpoints are not -- qp_bisect_frozen
-// computes them afterwards (the caller runs it in the shadow of the exit exchange).  Returns the
-// wave's convergence mask like qp_bisect_seq; fz = the lane's freeze iteration (or 32).
-__device__ __forceinline__ uint32_t qp_bisect_thr(const float (&lower)[C], const float (&nom)[C], int to, float tol,
-                                                  const QpThr& t, float& lo, float& hi, float* mu_rec, bool valid,
-                                                  int& fz) {
-  uint32_t open = 0;
-  bool frozen = false;
-  fz = 32;
-  for (int it = 0; it <= to; ++it) {
-    const float mu = __fmaf_rn(hi - lo, 0.5f, lo);
-    mu_rec[it] = mu;
-    bool pos = mu <= t.Cc, neg = mu >= t.D;
-    bool cf = (mu <= t.A) | (mu >= t.F);
-    bool ct = (mu >= t.B) & (mu <= t.E);
-    const bool fresh = !frozen & !(pos | neg) & (lo >= t.B) & (hi <= t.E);
-    if (fresh) fz = it;
-    frozen |= fresh;
-    const bool need = !frozen & (!(pos | neg) | !(cf | ct));
-    if (__any(need)) {                  // wave-uniform: the direct evaluation for the uncertain lanes
-      const float eps = qp_eps(lower, nom, mu);
-      if (need) {
-        pos = eps > 0.f;
-        neg = eps < 0.f;
-        ct = fabsf(eps) < tol;
-      }
-    }
-    if (frozen) {
-      ct = true;
-      pos = neg = false;
-    }
-    open |= ((valid && !ct) ? 1u : 0u) << it;
-    lo = pos ? mu : lo;
-    hi = neg ? mu : hi;
-  }
-  const uint32_t span = to >= 31 ? 0xFFFFFFFFu : ((2u << to) - 1u);
-  return ~wave_or16(open) & span;
-}
-
-// The exact midpoints of the frozen lanes from their freeze iteration to `to` (direct evaluations,
-// qp_bisect_seq's op order); leaves (lo, hi) exact for a later resume.
-__device__ __forceinline__ void qp_bisect_frozen(const float (&lower)[C], const float (&nom)[C], int to, float& lo,
-                                                 float& hi, float* mu_rec, int fz) {
-  for (int it = 0; it <= to; ++it) {
-    const bool act = it >= fz;
-    if (!__any(act)) continue;
-    const float mu = __fmaf_rn(hi - lo, 0.5f, lo);
-    const float eps = qp_eps(lower, nom, mu);
-    if (act) {
-      mu_rec[it] = mu;
-      lo = eps > 0.f ? mu : lo;
-      hi = eps < 0.f ? mu : hi;
-    }
-  }
-}
-
 
 // The weights one wave (hidden part p) reads in the MLP of a tile, held in registers for the whole
 // persistent kernel (108 VGPRs; the kernels run one wave per SIMD, 512 registers): no LDS reads on
@@ -469,14 +336,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   const bool pr = prof && blockIdx.x == 0 && threadIdx.x == 0;      // phase timing (diagnostic builds)
   const uint64_t t0 = prof ? wall_clock64() : 0;
   qp_bracket(lower, nominal, lo, hi);
-#if FIODE_QP_THRESH
-  QpThr th;
-  qp_thresholds(lower, nominal, tol, th);
-  int fz;
-  uint32_t conv = qp_bisect_thr(lower, nominal, kspec, tol, th, lo, hi, mu_rec_row, valid, fz);
-#else
   uint32_t conv = qp_bisect_seq(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, true, valid);
-#endif
   const uint64_t t1 = prof ? wall_clock64() : 0;
   if (pr) atomicAdd(prof + 6, (unsigned long long)(t1 - t0));
   const int ntiles = gridDim.x;
@@ -484,19 +344,11 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
     // drop_block (test hook, FIODE_DEBUG_DROP_PUBLISH): that workgroup never publishes epoch 1,
     // as if it were not resident -- exercises the timeout path
     if (lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block)) publish_mask(slots + blockIdx.x, epoch, conv);
-#if FIODE_QP_THRESH
-    qp_bisect_frozen(lower, nominal, kspec, lo, hi, mu_rec_row, fz);    // while the other tiles publish
-#endif
     const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane, dead);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
     if (lane == 0) shK = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
   }
-#if FIODE_QP_THRESH
-  else {
-    qp_bisect_frozen(lower, nominal, kspec, lo, hi, mu_rec_row, fz);
-  }
-#endif
   __syncthreads();
   if (pr) {
     atomicAdd(prof + 7, (unsigned long long)(wall_clock64() - t1));

@@ -173,7 +173,6 @@ def _load():
         "fiode_spectral_cayley_backward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp, _vp,
                                                       _vp, ct.c_size_t]),
         "fiode_adam_step": (ct.c_int, [_vp, ct.POINTER(AdamConfig), _vp, _vp, _vp, _vp, _vp, _vp]),
-        "fiode_qp_bisect_trace": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, _vp, _vp, ct.c_int32, ct.c_float, _vp, _vp]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

@@ -142,14 +142,6 @@ FIODE_API int fiode_qp_forward(void* stream, int32_t n, int32_t c, const float* 
                      int32_t max_iter, float tol, float* v, float* mu, int32_t* exit_iter,
                      void* workspace, size_t workspace_bytes);
 
-/* Diagnostic / parity entry: the certified-threshold form of the bisection used by the persistent
- * solves (barrier_projection.py:241-255 decided by comparisons with certified points, see
- * tile16.h), one row per lane, all `iters` iterations without the batch exit: mu[n][iters] = every
- * midpoint, wave_masks[ceil(n/64)] = bit it set iff every row of that 64-row group has |eps| < tol
- * at iteration it.  Equal, bit for bit, to the sequential bisection's. */
-FIODE_API int fiode_qp_bisect_trace(void* stream, int32_t n, int32_t c, const float* lower, const float* nominal,
-                                    int32_t iters, float tol, float* mu, uint32_t* wave_masks);
-
 /* FastBarrierProjectionNoUpper backward (barrier_projection.py:271-311), O(C) per row. */
 FIODE_API int fiode_qp_backward(void* stream, int32_t n, int32_t c, const float* g, const float* v,
                       const float* mu, const float* lower, const float* nominal, float* g_lower,

@@ -33,7 +33,7 @@ class _NoUpperProjection(Function):
     def forward(ctx, lower, nominal):
         with torch.no_grad():
             n = nominal.shape[0]
-            mu = torch.zeros((n, 1))
+            mu = torch.zeros((n, 1), dtype=nominal.dtype)
             hi = torch.ones_like(mu) * (nominal - lower).max(dim=-1).values[:, None]
             lo = torch.ones_like(mu) * nominal.min(dim=-1).values[:, None]
             v = torch.zeros_like(nominal)
@@ -56,13 +56,13 @@ class _NoUpperProjection(Function):
         n, c = v.shape
         act = (v - nominal + mu) > 0
         na = ~act
-        rec_na = (1 / na.sum(dim=-1))[:, None, None].expand(-1, c, c)
+        rec_na = (1 / na.sum(dim=-1).to(g.dtype))[:, None, None].expand(-1, c, c)
         eye = torch.eye(c, dtype=torch.bool)[None]
-        jn = torch.zeros((n, c, c))
+        jn = torch.zeros((n, c, c), dtype=g.dtype)
         m = na[:, None, :] & na[:, :, None]
         jn[m] = -rec_na[m]
         jn[eye & na[:, :, None]] += 1
-        jl = torch.zeros((n, c, c))
+        jl = torch.zeros((n, c, c), dtype=g.dtype)
         m2 = act[:, None, :] & na[:, :, None]
         jl[m2] = -rec_na[m2]
         jl[eye & act[:, :, None]] += 1

@@ -1,7 +1,7 @@
 """Phase timing of k_ot_fwd (needs tools/libfiode_prof.so built with -DOT_PROFILE; not a test)."""
 import ctypes as ct, os, sys, pathlib
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-os.environ["FIODE_LIB"] = str(ROOT / "tools" / "libfiode_prof.so")
+os.environ.setdefault("FIODE_LIB", str(ROOT / "tools" / "libfiode_prof.so"))
 sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
 import numpy as np, torch
 from fiode_amd import _lib as L, ops

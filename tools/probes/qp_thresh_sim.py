@@ -3,6 +3,15 @@ on the QP inputs of a train_ode solve: checks that the certified-threshold decis
 float32 bisection's own decisions bit for bit, and counts how many iterations of each 16-row wave
 would still need the direct eps evaluation (the fallback).
 
+Measured outcome (round 3): a HIP implementation of this scheme in k_ot_fwd
+(Newton root + six certified points per row and eval, comparisons per iteration, frozen lanes
+finished in the exit exchange's shadow) was bit-identical to the sequential bisection on every
+seeded solve and on adversarial rows, but SLOWER: k_ot_fwd 263 -> 359 us (bisection phase 1.97 ->
+3.24 us per eval).  At one wave per SIMD the per-row setup (3 Newton steps, 6 certificate
+evaluations) costs more dependent VALU time than the ~17 sequential iterations it replaces, and
+the late iterations (rows converged, bracket inside the rounding band of the root) still need the
+direct evaluation.  Not kept.
+
 python tools/probes/qp_thresh_sim.py [newton_iters] [delta_ulps]
 """
 import pathlib
