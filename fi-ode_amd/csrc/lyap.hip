@@ -56,6 +56,7 @@ constexpr int SLAB_Q2 = 0, SLAB_Q3 = 16384, SLAB_Q1 = 16384 + 1280, SLAB_B2 = 16
               SLAB_B1 = 16384 + 2560 + 128, SLAB_B3 = 16384 + 2560 + 256;
 
 struct LyapArgs {
+  const int32_t* s_used;   // launch_wgrad: optional device count of the rows per image that are data
   int N, S, B, S1;
   int sampler, dropout_mode, bit_mode;
   uint32_t thr8;
@@ -583,7 +584,8 @@ __global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   const int b = blockIdx.x / a.parts, p = blockIdx.x - b * a.parts;
   const int r0 = b * a.S + p * a.chunk;
-  const int r1 = min(r0 + a.chunk, (b + 1) * a.S);
+  int r1 = min(r0 + a.chunk, (b + 1) * a.S);
+  if (a.s_used) r1 = min(r1, b * a.S + a.s_used[0]);      // rows past the device count are not data
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
   f32x16 acc2[4], acc3 = f16_zero(), acc1 = f16_zero();
 #pragma unroll
@@ -928,6 +930,7 @@ size_t wgrad_bytes(int B, int S) {
 int launch_wgrad(hipStream_t st, const WgradIO& io) {
   LyapArgs a{};
   a.B = io.B; a.S = io.S; a.N = io.B * io.S;
+  a.s_used = io.s_used;
   parts_for(a.B, a.S, a.parts, a.chunk);
   a.sampler = FIODE_SAMPLER_GIVEN;
   a.h_in = io.h; a.x_feat = io.x_feat; a.Qx = io.Qx;

@@ -22,11 +22,13 @@
 #include "tile.h"
 #include "tile16.h"
 #include "wgrad.h"
+#include "dopri5.h"
 #include "../../include/fiode.h"
 
 namespace {
 using namespace fiode_tile;
 using namespace fiode_t16;
+using namespace fiode_dp;
 
 
 struct OTArgs {
@@ -68,6 +70,14 @@ struct OTArgs {
 #ifdef OT_PROFILE
   unsigned long long* prof;    // [9] wall-clock ticks per phase (workgroup 0, lane 0); [16 + e] eval e's exit K
 #endif
+  // dopri5 (method FIODE_ODE_DOPRI5): E = 2 + 6 A is the eval capacity, the solve's own count is in imeta
+  int method, A;
+  double rtol, atol, t0d, t1d;
+  float* ys;                   // [A][B][C] the state y_n attempt n starts from
+  double* alog;                // [A][ALOG_W] per attempt (ALOG_*)
+  double* meta;                // [META_N] initial-step scalars (META_*)
+  int32_t* imeta;              // [8]: nfe, attempts, status (read by the backward and the weight chain)
+  unsigned long long* xr;      // [2 parities][ntiles][2 OT_XV] float64 reduction granules
 };
 
 // float32 grid of FixedGridODESolver: t_k = k*h + t0, last point = t1
@@ -579,6 +589,658 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
 #undef OT_VJP
 }
 
+// =============================================================================================
+// train_ode with adaptive dopri5 (cifar_train.yaml:30,32: train_ode_solver dopri5, train_ode_tol
+// 1e-3; pl_modules.py:490-500 -> models.py:235-241 odeint, use_adjoint False at pl_modules.py:303):
+// torchdiffeq 0.2.2's RKAdaptiveStepsizeODESolver in TRAIN mode, backpropagated directly through
+// everything it computes -- the stages, the error ratio of accepted AND rejected attempts (it sets
+// the next step size), the step-size controller, the initial-step selection and the interpolation
+// point of the output.  oracle/dopri5_train.py restates the algorithm (dopri5_train) and this
+// kernel's reverse sweep (dopri5_adjoint), checked there against torch autograd.
+//
+// Same tiles, MLP and QP exit as the rk4 solve (ot_eval / ot_vjp: one persistent workgroup per
+// 16-row tile, hidden units split over 4 waves, rows replicated in every wave).  The solve's
+// batch couplings beyond the QP exits -- the RMS norms of the initial step and every attempt's error
+// ratio, and in the backward every attempt's dt adjoint -- are float64 sums over all rows that
+// every workgroup forms identically (ot_batch_sum: per-tile partials exchanged through tagged
+// granules and added in tile order).  The controller (dt, t, accept) runs redundantly and
+// identically in every thread.  Stage derivatives k_0..k_6 of the current attempt live in LDS
+// (every wave its own copy); the saved per-eval arrays (hs, a1, a2, ft, v, mu, nominal) are the rk4
+// solve's, at row (b, e) = b E + e with E = 2 + 6 A the capacity; eval e of attempt n is 2 + 6n + i.
+constexpr int OT_XV = 4;          // float64 values per reduction exchange (at most)
+enum { ALOG_T = 0, ALOG_DT, ALOG_RATIO, ALOG_ACCEPT, ALOG_FIDX, ALOG_E0, ALOG_W = 8 };
+enum { META_D0 = 0, META_D1, META_D2, META_H0, META_H1, META_CLAMP0, META_CLAMP1, META_DT0, META_R2, META_N = 16 };
+
+// sum over all rows (every workgroup gets the same float64 values): the caller's per-lane values
+// count only on wave 0's owner lanes (q = 0, valid rows: the caller zeroes the others)
+template <int NV>
+__device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& ep, const double (&mine)[NV],
+                             double (&out)[NV]) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    double w[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      double s = mine[i];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+      w[i] = s;
+    }
+    const int G = gridDim.x;
+    unsigned long long* buf = a.xr + (size_t)(ep & 1u) * G * 2 * OT_XV;
+    if (lane == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(w[v]);
+        publish_mask(buf + (size_t)blockIdx.x * 2 * OT_XV + 2 * v, ep, (uint32_t)(bits >> 32));
+        publish_mask(buf + (size_t)blockIdx.x * 2 * OT_XV + 2 * v + 1, ep, (uint32_t)bits);
+      }
+    }
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    for (int base = 0; base < G; base += 64) {
+      const int t = base + lane;
+      unsigned spins = 0;
+      for (;;) {
+        bool ok = true;
+        unsigned long long x[2 * NV];
+#pragma unroll
+        for (int g = 0; g < 2 * NV; ++g) {
+          x[g] = 0;
+          if (t < G) {
+            x[g] = __hip_atomic_load((gu64_t*)(buf + (size_t)t * 2 * OT_XV + g), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && (unsigned)(x[g] >> 32) == ep;
+          }
+        }
+        if (__all(ok)) {
+          if (t < G) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+              acc[v] += __longlong_as_double((long long)(((x[2 * v] & 0xFFFFFFFFull) << 32) | (x[2 * v + 1] & 0xFFFFFFFFull)));
+          }
+          break;
+        }
+        if (dead || ++spins > (1u << 22)) {     // ~0.5 s: a workgroup is not resident
+          if (lane == 0) {
+            atomicMax(a.stats ? a.stats + 3 : a.imeta + 2, 4);
+            dead = 1;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) acc[v] += __shfl_xor(acc[v], o, 64);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) red[v] = acc[v];
+  }
+  ++ep;
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) out[v] = red[v];
+  __syncthreads();
+}
+
+struct OdpShared {
+  OtShared ot;
+  float kst[4][7][TR][C];      // [wave][stage][row][c]: the current attempt's k_0..k_6
+  double red[OT_XV];
+};
+
+__device__ __forceinline__ double rms_of(double sumsq, double n) { return sqrt(sumsq / n); }
+
+__global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  OdpShared& S = *reinterpret_cast<OdpShared*>(smem);
+  OtShared& sh = S.ot;
+  if (threadIdx.x == 0) {
+    sh.Kprev = a.d.max_iter - 1;
+    sh.dead = 0;
+  }
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x * TR + j;
+  const bool valid = b < a.B;
+  const bool own = valid && q == 0;            // lanes whose row values count in the batch sums
+  const int bb = valid ? b : a.B - 1;
+  T16W w;
+  load_t16w(a.Q1, a.Q2, M, a.Q3, M, a.b2, a.b3, p, q, j, w);
+  for (int t = threadIdx.x; t < TR * M; t += blockDim.x) {
+    const int rb = blockIdx.x * TR + t / M, i = t % M;
+    if (rb < a.B) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < FIODE_X; ++c) s = __fmaf_rn(a.Qx[i * FIODE_X + c], a.x_feat[(size_t)rb * FIODE_X + c], s);
+      a.u[(size_t)rb * M + i] = (s + a.bx[i]) + a.b1[i];
+    }
+  }
+  __syncthreads();
+  f32x4v uacc[8];
+#pragma unroll
+  for (int hb = 0; hb < 8; ++hb) {
+    const f32x4 uv = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 16 * hb + 4 * q);
+    uacc[hb] = f32x4v{uv[0], uv[1], uv[2], uv[3]};
+  }
+  const uint4* kwp = reinterpret_cast<const uint4*>(a.kw);
+  auto fetch = [&](int e, uint32_t (&w1)[4], uint32_t& w2) {
+    if (a.dropout_mode == FIODE_DROPOUT_OFF) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w1[t] = 0xFFFFFFFFu;
+      w2 = 0xFFFFFFFFu;
+      return;
+    }
+    const uint4 q1 = kwp[((size_t)e * 2 + 0) * a.B + bb];
+    w1[0] = q1.x; w1[1] = q1.y; w1[2] = q1.z; w1[3] = q1.w;
+    w2 = reinterpret_cast<const uint32_t*>(kwp + ((size_t)e * 2 + 1) * a.B + bb)[p];
+  };
+  float (*ks)[TR][C] = S.kst[p];
+  // every lane of the row writes the same values into its wave's copy, so no lane reads another's
+  auto kput = [&](int s, const float (&v)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) ks[s][j][c] = v[c];
+  };
+  auto kget = [&](int s, float (&v)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = ks[s][j][c];
+  };
+  int e = 0;
+  uint32_t kc1[4], kc2;
+  fetch(0, kc1, kc2);
+  auto eval = [&](const float (&h)[C], float (&k)[C]) {
+    uint32_t kn1[4] = {0u, 0u, 0u, 0u}, kn2 = 0u;
+    if (e + 1 < a.E) fetch(e + 1, kn1, kn2);
+    ot_eval(a, w, sh, e, p, b, valid, lane, q, j, uacc, kc1, kc2, h, k);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kc1[t] = kn1[t];
+    kc2 = kn2;
+    ++e;
+  };
+  const double NBC = (double)a.B * C;
+  const float rtol = (float)a.rtol, atol = (float)a.atol;
+  unsigned rep = 1;
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  // ---- _select_initial_step(order 4), float32 (odesolve.hip os_dopri5's expressions) ----------
+  float y[C], fcur[C];
+  load_row10(a.h0 + (size_t)bb * C, y);
+  eval(y, fcur);
+  double s01[2] = {0.0, 0.0};
+  if (own) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float sc = atol + fabsf(y[c]) * rtol;
+      const float q0 = y[c] / sc, qq = fcur[c] / sc;
+      s01[0] += (double)q0 * q0;
+      s01[1] += (double)qq * qq;
+    }
+  }
+  ot_batch_sum<2>(a, S.red, sh.dead, rep, s01, s01);
+  const float d0 = (float)rms_of(s01[0], NBC), d1 = (float)rms_of(s01[1], NBC);
+  const bool clamp0 = d0 < 1e-5f || d1 < 1e-5f;
+  const float h0s = clamp0 ? 1e-6f : (0.01f * d0) / d1;
+  double dt;
+  {
+    float yi[C], f1[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) yi[c] = y[c] + h0s * fcur[c];
+    eval(yi, f1);
+    double s2[1] = {0.0};
+    if (own) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float sc = atol + fabsf(y[c]) * rtol;
+        const float qv = (f1[c] - fcur[c]) / sc;
+        s2[0] += (double)qv * qv;
+      }
+    }
+    ot_batch_sum<1>(a, S.red, sh.dead, rep, s2, s2);
+    const float r2 = (float)rms_of(s2[0], NBC);
+    const float d2 = r2 / h0s;
+    const bool clamp1 = d1 <= 1e-15f && d2 <= 1e-15f;
+    const float h1 = clamp1 ? fmaxf(1e-6f, h0s * 1e-3f) : powf(0.01f / fmaxf(d1, d2), 1.0f / 5.0f);
+    dt = (double)fminf(100.0f * h0s, h1);
+    if (lead) {
+      a.meta[META_D0] = d0; a.meta[META_D1] = d1; a.meta[META_D2] = d2; a.meta[META_H0] = h0s;
+      a.meta[META_H1] = h1; a.meta[META_CLAMP0] = clamp0; a.meta[META_CLAMP1] = clamp1; a.meta[META_R2] = r2;
+      a.meta[META_DT0] = dt;
+    }
+  }
+  // ---- attempts -------------------------------------------------------------------------------
+  double tcur = a.t0d, tprev = tcur, tnext = tcur;
+  const double tmax = a.t1d;
+  int n = 0, nacc = 0, nrej = 0, status = 0, fidx = 0;
+  float yprev[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) yprev[c] = y[c];
+  float dt32L = 0.f;
+  while (tmax > tnext) {
+    if (n >= a.A || !(tcur + dt > tcur)) {
+      status = n >= a.A ? 2 : 3;           // attempt capacity exhausted / dt underflow
+      break;
+    }
+    const float dt32 = (float)dt;
+    if (p == 0 && q == 0 && valid) store_row10(a.ys + ((size_t)n * a.B + b) * C, y);
+    if (lead) {
+      double* lg = a.alog + (size_t)n * ALOG_W;
+      lg[ALOG_T] = tcur; lg[ALOG_DT] = dt; lg[ALOG_FIDX] = fidx; lg[ALOG_E0] = e;
+    }
+    kput(0, fcur);
+    float hin[C];
+    for (int i = 0; i < 6; ++i) {
+      float acc[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = 0.f;
+      for (int jj = 0; jj <= i; ++jj) {
+        float f[C];
+        kget(jj, f);
+        const float co = DP_BETA[i][jj] * dt32;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) hin[c] = y[c] + acc[c];
+      float kn[C];
+      eval(hin, kn);
+      kput(i + 1, kn);
+    }
+    // y_new = the stage-5 input (FSAL); batch-global RMS error ratio
+    double ps[1] = {0.0};
+    if (own) {
+      float err[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) err[c] = 0.f;
+      for (int jj = 0; jj < 7; ++jj) {
+        float f[C];
+        kget(jj, f);
+        const float co = DP_CERR[jj] * dt32;
+#pragma unroll
+        for (int c = 0; c < C; ++c) err[c] = err[c] + f[c] * co;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float etol = atol + rtol * fmaxf(fabsf(y[c]), fabsf(hin[c]));
+        const float qv = err[c] / etol;
+        ps[0] += (double)qv * qv;
+      }
+    }
+    ot_batch_sum<1>(a, S.red, sh.dead, rep, ps, ps);
+    const float ratio = (float)rms_of(ps[0], NBC);
+    const bool accept = ratio <= 1.0f;
+    if (lead) {
+      double* lg = a.alog + (size_t)n * ALOG_W;
+      lg[ALOG_RATIO] = ratio;
+      lg[ALOG_ACCEPT] = accept ? 1.0 : 0.0;
+    }
+    if (accept) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        yprev[c] = y[c];
+        y[c] = hin[c];
+      }
+      kget(6, fcur);
+      fidx = e - 1;
+      dt32L = dt32;
+      tprev = tcur;
+      tnext = tcur + dt;
+      tcur = tcur + dt;
+      ++nacc;
+    } else {
+      ++nrej;
+    }
+    // _optimal_step_size (float64)
+    if (ratio == 0.f) {
+      dt = dt * DP_IFACTOR;
+    } else {
+      const double df = ratio < 1.0f ? 1.0 : DP_DFACTOR;
+      dt = dt * fmin(DP_IFACTOR, fmax(DP_SAFETY / pow((double)ratio, 1.0 / 5.0), df));
+    }
+    ++n;
+  }
+  // ---- dense output at t1 (torchdiffeq _interp_evaluate of the last accepted step) -----------
+  float out[C];
+  if (status == 0 && nacc > 0 && !sh.dead) {
+    const float x = (float)((tmax - tprev) / (tnext - tprev));
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+    for (int jj = 0; jj < 7; ++jj) {
+      float f[C];
+      kget(jj, f);
+      const float co = DP_CMID[jj] * dt32L;
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
+    }
+    float fa[C], fb[C];
+    kget(0, fa);
+    kget(6, fb);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float y0 = yprev[c], y1 = y[c], ym = y0 + acc[c];
+      const float ci1 = dt32L * fa[c];
+      const float ci2 = (((dt32L * (fb[c] - 4.0f * fa[c])) - 11.0f * y0) - 5.0f * y1) + 16.0f * ym;
+      const float ci3 = (((dt32L * (5.0f * fa[c] - 3.0f * fb[c])) + 18.0f * y0) + 14.0f * y1) - 32.0f * ym;
+      const float ci4 = ((2.0f * dt32L) * (fb[c] - fa[c]) - 8.0f * (y1 + y0)) + 16.0f * ym;
+      float total = y0 + x * ci1;
+      float xp = x * x;
+      total = total + xp * ci2;
+      xp = xp * x;
+      total = total + xp * ci3;
+      xp = xp * x;
+      total = total + xp * ci4;
+      out[c] = total;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) out[c] = __builtin_nanf("");   // failed solve: the loss turns NaN
+  }
+  if (p == 0 && valid && q == 0) store_row10(a.y_out + (size_t)b * C, out);
+  if (lead) {
+    a.stats[0] = e;
+    a.stats[1] = nacc;
+    if (status) atomicMax(a.stats + 3, status);
+    a.stats[4] = nacc;
+    a.stats[5] = nrej;
+    a.stats[6] = n;
+    a.imeta[0] = e;
+    a.imeta[1] = n;
+    a.imeta[2] = status ? status : (sh.dead ? 4 : 0);
+  }
+}
+
+// ---- backward: the reverse sweep of oracle/dopri5_train.py dopri5_adjoint ---------------------
+struct OdpBwdShared {
+  OtBwdShared ot;
+  float gk[4][7][TR][C];       // [wave][stage][row][c]: adjoints of the attempt's k_0..k_6
+  double red[OT_XV];
+  int dead;
+};
+
+template <bool SN>
+__global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  OdpBwdShared& S = *reinterpret_cast<OdpBwdShared*>(smem);
+  if (threadIdx.x == 0) S.dead = 0;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  VjpW wv;
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+#pragma unroll
+    for (int hb = 0; hb < 8; ++hb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wv.q2t[o][hb][t] = a.Q2[(16 * hb + 4 * q + t) * M + 16 * (2 * p + o) + j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wv.q1t[o][t] = j < C ? a.Q1[(16 * (2 * p + o) + 4 * q + t) * C + j] : 0.f;
+  }
+  float q3t[8][3];
+#pragma unroll
+  for (int hb = 0; hb < 8; ++hb)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) q3t[hb][s] = 4 * s + q < C ? a.Q3[(4 * s + q) * M + 16 * hb + j] : 0.f;
+  const int b = blockIdx.x * TR + j;
+  const bool valid = b < a.B;
+  const bool own = valid && q == 0;
+  const int bb = valid ? b : a.B - 1;
+  const int nfe = a.imeta[0], A = a.imeta[1];
+  const bool failed = a.imeta[2] != 0 || A < 1;
+  __syncthreads();
+  float (*gks)[TR][C] = S.gk[p];
+  auto gadd = [&](int s, const float (&v)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) gks[s][j][c] += v[c];
+  };
+  auto gget = [&](int s, float (&v)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = gks[s][j][c];
+  };
+  auto krow = [&](int e, float (&v)[C]) { load_row10(a.vw + ((size_t)bb * a.E + e) * C, v); };
+  float gout[C];
+  if (valid) load_row10(a.g_y + (size_t)b * C, gout);
+  else
+#pragma unroll
+    for (int c = 0; c < C; ++c) gout[c] = 0.f;
+  if (failed)
+#pragma unroll
+    for (int c = 0; c < C; ++c) gout[c] = __builtin_nanf("");     // a failed forward: NaN gradients
+  const double NBC = (double)a.B * C;
+  const float rtol = (float)a.rtol, atol = (float)a.atol;
+  unsigned rep = 1;
+  int buf = 0;
+  VjpIn cur, nxt;
+  VjpRow crw, nrw;
+  int ecur = nfe - 1;
+  load_vjp_in(a, p, ecur, b, valid, q, cur);
+  vjp_row_math<SN>(a, cur, crw);
+  // evals visited nfe-1, nfe-2, ..., 0 (attempts in reverse, stages 5..0; then evals 1, 0)
+  auto vjp = [&](const float (&g)[C], float (&gY)[C]) {
+    load_vjp_in(a, p, ecur - 1, b, valid, q, nxt);
+    ot_vjp<SN>(a, wv, q3t, S.ot, buf, p, ecur, b, valid, lane, q, j, cur, crw, nxt, nrw, g, gY);
+    cur = nxt;
+    crw = nrw;
+    buf ^= 1;
+    --ecur;
+  };
+  float gy[C], gf[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) gy[c] = gf[c] = 0.f;
+  double g_dt_next = 0.0, g_t_next = 0.0;
+  for (int n = A - 1; n >= 0; --n) {
+    const double* lg = a.alog + (size_t)n * ALOG_W;
+    const double tn = lg[ALOG_T], dtn = lg[ALOG_DT];
+    const float ratio = (float)lg[ALOG_RATIO];
+    const bool accept = lg[ALOG_ACCEPT] != 0.0;
+    const int fidx = (int)lg[ALOG_FIDX], e0 = (int)lg[ALOG_E0];
+    const float dts = (float)dtn;
+    // controller: dt_{n+1} = dt_n * factor(ratio_n)
+    double fac, dfac = 0.0;
+    if (ratio == 0.f) {
+      fac = DP_IFACTOR;
+    } else {
+      const double df = ratio < 1.0f ? 1.0 : DP_DFACTOR;
+      const double mid = DP_SAFETY / pow((double)ratio, 1.0 / 5.0);
+      fac = fmin(DP_IFACTOR, fmax(mid, df));
+      if (mid > df && mid < DP_IFACTOR) dfac = -0.2 * mid / (double)ratio;
+    }
+    const double g_ratio = g_dt_next * dtn * dfac;
+    double g_dt = g_dt_next * fac;
+    const bool last = n == A - 1;
+    // rows
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int c = 0; c < C; ++c) gks[s][j][c] = 0.f;
+    float yn[C], ynew[C], g_yn[C], g_ynew[C];
+    load_row10(a.ys + ((size_t)n * a.B + bb) * C, yn);
+    load_row10(a.hs + ((size_t)bb * a.E + e0 + 5) * C, ynew);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      g_yn[c] = accept ? 0.f : gy[c];
+      g_ynew[c] = accept ? gy[c] : 0.f;
+    }
+    if (accept) gadd(6, gf);
+    else gadd(0, gf);
+    double pdt = 0.0, px = 0.0;
+    float x = 0.f;
+    double x64 = 0.0;
+    if (last) {                      // the output: y_hat = interpolant of this attempt at x
+      x64 = (a.t1d - tn) / ((tn + dtn) - tn);
+      x = (float)x64;
+      float ym[C], fa[C], fb[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) ym[c] = 0.f;
+      for (int jj = 0; jj < 7; ++jj) {
+        float f[C];
+        krow(jj == 0 ? fidx : e0 + jj - 1, f);
+        const float co = DP_CMID[jj] * dts;
+#pragma unroll
+        for (int c = 0; c < C; ++c) ym[c] = ym[c] + f[c] * co;
+      }
+      krow(fidx, fa);
+      krow(e0 + 5, fb);
+      const float x2 = x * x, x3 = x2 * x, x4 = x3 * x;
+      float g_ym[C], gfa[C], gfb[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float y0 = yn[c], y1 = ynew[c], yc = y0 + ym[c];
+        const float cd = dts * fa[c];
+        const float cc = (((dts * (fb[c] - 4.0f * fa[c])) - 11.0f * y0) - 5.0f * y1) + 16.0f * yc;
+        const float cb = (((dts * (5.0f * fa[c] - 3.0f * fb[c])) + 18.0f * y0) + 14.0f * y1) - 32.0f * yc;
+        const float ca = ((2.0f * dts) * (fb[c] - fa[c]) - 8.0f * (y1 + y0)) + 16.0f * yc;
+        const float go = gout[c];
+        px += (double)go * ((double)cd + 2.0 * x * cc + 3.0 * (double)x2 * cb + 4.0 * (double)x3 * ca);
+        const float ga = go * x4, gb = go * x3, gc = go * x2, gd = go * x;
+        g_ym[c] = (16.0f * ga - 32.0f * gb) + 16.0f * gc;
+        g_yn[c] += ((((go - 8.0f * ga) + 18.0f * gb) - 11.0f * gc)) + g_ym[c];
+        g_ynew[c] += (-8.0f * ga + 14.0f * gb) - 5.0f * gc;
+        gfa[c] = dts * (((-2.0f * ga + 5.0f * gb) - 4.0f * gc) + gd);
+        gfb[c] = dts * ((2.0f * ga - 3.0f * gb) + gc);
+        pdt += (double)ga * 2.0 * (fb[c] - fa[c]) + (double)gb * (5.0 * fa[c] - 3.0 * fb[c]) +
+               (double)gc * (fb[c] - 4.0 * fa[c]) + (double)gd * fa[c];
+      }
+      for (int jj = 0; jj < 7; ++jj) {
+        float f[C], t[C];
+        krow(jj == 0 ? fidx : e0 + jj - 1, f);
+        const float co = DP_CMID[jj] * dts;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          t[c] = g_ym[c] * co;
+          pdt += (double)g_ym[c] * f[c] * DP_CMID[jj];
+        }
+        gadd(jj, t);
+      }
+      gadd(0, gfa);
+      gadd(6, gfb);
+    }
+    if (g_ratio != 0.0) {            // ratio = rms(err / etol), etol = atol + rtol max(|y_n|, |y_new|)
+      float err[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) err[c] = 0.f;
+      float kk[7][C];
+      for (int jj = 0; jj < 7; ++jj) {
+        krow(jj == 0 ? fidx : e0 + jj - 1, kk[jj]);
+        const float co = DP_CERR[jj] * dts;
+#pragma unroll
+        for (int c = 0; c < C; ++c) err[c] = err[c] + kk[jj][c] * co;
+      }
+      float g_err[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float etol = atol + rtol * fmaxf(fabsf(yn[c]), fabsf(ynew[c]));
+        const double qv = (double)err[c] / etol;
+        const double gq = g_ratio * qv / (NBC * (double)ratio);
+        g_err[c] = (float)(gq / etol);
+        const float g_etol = (float)(-gq * qv / etol);
+        if (fabsf(yn[c]) >= fabsf(ynew[c])) g_yn[c] += g_etol * rtol * (yn[c] > 0.f ? 1.f : (yn[c] < 0.f ? -1.f : 0.f));
+        else g_ynew[c] += g_etol * rtol * (ynew[c] > 0.f ? 1.f : (ynew[c] < 0.f ? -1.f : 0.f));
+      }
+      for (int jj = 0; jj < 7; ++jj) {
+        float t[C];
+        const float co = DP_CERR[jj] * dts;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          t[c] = g_err[c] * co;
+          pdt += (double)g_err[c] * kk[jj][c] * DP_CERR[jj];
+        }
+        gadd(jj, t);
+      }
+    }
+    // stages in reverse: k_{i+1} = f(Y_i), Y_i = y_n + sum_{j <= i} k_j beta_ij dt; y_new = Y_5
+    for (int i = 5; i >= 0; --i) {
+      float g[C], gY[C];
+      gget(i + 1, g);
+      vjp(g, gY);
+      if (i == 5)
+#pragma unroll
+        for (int c = 0; c < C; ++c) gY[c] += g_ynew[c];
+#pragma unroll
+      for (int c = 0; c < C; ++c) g_yn[c] += gY[c];
+      for (int jj = 0; jj <= i; ++jj) {
+        float f[C], t[C];
+        krow(jj == 0 ? fidx : e0 + jj - 1, f);
+        const float co = DP_BETA[i][jj] * dts;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          t[c] = gY[c] * co;
+          pdt += (double)gY[c] * f[c] * DP_BETA[i][jj];
+        }
+        gadd(jj, t);
+      }
+    }
+    double red[2] = {own ? pdt : 0.0, own ? px : 0.0};
+    ot_batch_sum<2>(a, S.red, S.dead, rep, red, red);
+    g_dt += red[0];
+    double g_t;
+    if (last) {
+      g_dt += -red[1] * x64 / dtn;   // x = (t1 - t_n) / (t_n + dt_n - t_n)
+      g_t = -red[1] / dtn;
+    } else {
+      g_t = g_t_next;
+      if (accept) g_dt += g_t_next;  // t_{n+1} = t_n + dt_n
+    }
+    g_t_next = g_t;
+    g_dt_next = g_dt;
+#pragma unroll
+    for (int c = 0; c < C; ++c) gy[c] = g_yn[c];
+    gget(0, gf);
+  }
+  // ---- the initial step: dt_0 = min(100 h0, h1) -----------------------------------------------
+  const double d1 = a.meta[META_D1], d2 = a.meta[META_D2], h0 = a.meta[META_H0], h1 = a.meta[META_H1];
+  const double r2 = a.meta[META_R2];
+  const bool clamp0 = a.meta[META_CLAMP0] != 0.0, clamp1 = a.meta[META_CLAMP1] != 0.0;
+  double g_h0 = (100.0 * h0 <= h1) ? g_dt_next * 100.0 : 0.0;
+  const double g_h1 = (h1 < 100.0 * h0) ? g_dt_next : 0.0;
+  double g_d1 = 0.0, g_d2 = 0.0;
+  if (clamp1) {
+    if (h0 * 1e-3 > 1e-6) g_h0 += 1e-3 * g_h1;
+  } else {
+    const bool m2 = d2 > d1;
+    const double m = m2 ? d2 : d1;
+    const double g_m = g_h1 * (-0.2) * h1 / m;
+    if (m2) g_d2 += g_m;
+    else g_d1 += g_m;
+  }
+  const double g_r2 = g_d2 / h0;     // d2 = r2 / h0
+  g_h0 += -g_d2 * d2 / h0;
+  float y0[C], f0[C], f1[C], gf1[C], gf0[C];
+  load_row10(a.hs + ((size_t)bb * a.E + 0) * C, y0);
+  krow(0, f0);
+  krow(1, f1);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float sc = atol + fabsf(y0[c]) * rtol;
+    const float wv_ = (f1[c] - f0[c]) / sc;
+    const float gw = r2 > 0.0 ? (float)(g_r2 * wv_ / (NBC * r2)) : 0.f;
+    gf1[c] = gw / sc;
+    gf0[c] = gf[c] - gw / sc;
+  }
+  float gyi[C];
+  vjp(gf1, gyi);                     // eval 1: f1 = f(y0 + h0 f0)
+  double sh0 = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    gf0[c] += (float)h0 * gyi[c];
+    sh0 += (double)gyi[c] * f0[c];
+  }
+  double red1[1] = {own ? sh0 : 0.0};
+  ot_batch_sum<1>(a, S.red, S.dead, rep, red1, red1);
+  g_h0 += red1[0];
+  if (!clamp0) g_d1 += -g_h0 * h0 / d1;   // h0 = 0.01 d0 / d1
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float sc = atol + fabsf(y0[c]) * rtol;
+    gf0[c] += (float)((g_d1 * ((double)f0[c] / sc) / (NBC * d1)) / sc);
+  }
+  float gy0[C];
+  vjp(gf0, gy0);                     // eval 0: f0 = f(y0)
+  (void)gy0;
+}
+
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int grid_iters(const fiode_odetrain_config* cfg) {
@@ -589,10 +1251,30 @@ int grid_iters(const fiode_odetrain_config* cfg) {
   return (int)n;
 }
 
+// the solve's shape: E evals (rk4) or the eval capacity 2 + 6 A (dopri5); -1 if invalid
+int solve_shape(const fiode_odetrain_config* cfg, int& E, int& A, int& niters) {
+  if (cfg->method == FIODE_ODE_DOPRI5) {
+    if (cfg->max_attempts < 1 || cfg->max_attempts > FIODE_ODETRAIN_MAX_ATTEMPTS) return -1;
+    if (!(cfg->rtol > 0.0) || !(cfg->atol > 0.0) || !(cfg->t1 > cfg->t0)) return -1;
+    A = cfg->max_attempts;
+    E = 2 + 6 * A;
+    niters = 0;
+    return 0;
+  }
+  if (cfg->method != FIODE_ODE_RK4) return -1;
+  const int n = grid_iters(cfg);
+  if (n < 0) return -1;
+  niters = n;
+  E = 4 * (n - 1);
+  A = 0;
+  return 0;
+}
+
 struct OtLayout {
-  size_t u, y, k, hs, ftw, vw, muw, nomw, loww, a1, a2, gz2, gz1, gft, xs, kw, wg, total;
+  size_t u, y, k, hs, ftw, vw, muw, nomw, loww, a1, a2, gz2, gz1, gft, xs, xr, kw, wg, ys, alog, meta, imeta, total;
 };
-OtLayout ot_layout(int B, int E) {
+// E: evals (rk4) or the eval capacity 2 + 6 A (dopri5, A > 0: attempt capacity)
+OtLayout ot_layout(int B, int E, int A = 0) {
   OtLayout L;
   const size_t R = (size_t)B * E;
   size_t o = 0;
@@ -610,9 +1292,15 @@ OtLayout ot_layout(int B, int E) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  L.xs = o; o += al((size_t)E * 2 * ((B + TR - 1) / TR) * 8 + 1024);
+  const size_t nt = (size_t)(B + TR - 1) / TR;
+  L.xs = o; o += (size_t)E * 2 * nt * 8 + 1024;     // the reduction granules follow: one clear for both
+  L.xr = o; o += al(A > 0 ? 2 * nt * 2 * OT_XV * 8 : 0);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
+  L.ys = o; o += al((size_t)A * B * C * 4);
+  L.alog = o; o += al((size_t)A * ALOG_W * 8);
+  L.meta = o; o += al(META_N * 8);
+  L.imeta = o; o += al(8 * 4);
   L.total = o;
   return L;
 }
@@ -626,10 +1314,11 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   if (cfg->batch <= 0 || cfg->batch > FIODE_ODE_MAX_BATCH) return FIODE_EINVAL;
   if (cfg->dropout_mode < 0 || cfg->dropout_mode > 2) return FIODE_EINVAL;
   if (!w->Q1 || !w->b1 || !w->Qx || !w->bx || !w->Q2 || !w->b2 || !w->Q3 || !w->b3) return FIODE_EINVAL;
-  const int n = grid_iters(cfg);
-  if (n < 0) return FIODE_EINVAL;
-  a.B = cfg->batch; a.niters = n; a.E = 4 * (n - 1);
-  const OtLayout L = ot_layout(a.B, a.E);
+  int E, A, n;
+  if (solve_shape(cfg, E, A, n) < 0) return FIODE_EINVAL;
+  a.B = cfg->batch; a.niters = n; a.E = E; a.A = A; a.method = cfg->method;
+  a.rtol = cfg->rtol; a.atol = cfg->atol; a.t0d = cfg->t0; a.t1d = cfg->t1;
+  const OtLayout L = ot_layout(a.B, a.E, a.A);
   if (workspace_bytes < L.total) return FIODE_EWORKSPACE;
   a.t0 = (float)cfg->t0; a.t1 = (float)cfg->t1; a.hstep = (float)cfg->step_size;
   a.dropout_mode = dyn->dropout > 0.f ? cfg->dropout_mode : FIODE_DROPOUT_OFF;
@@ -658,34 +1347,53 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.gz1 = reinterpret_cast<float*>(ws + L.gz1);
   a.gft = reinterpret_cast<float*>(ws + L.gft);
   a.xslots = reinterpret_cast<unsigned long long*>(ws + L.xs);
+  a.xr = reinterpret_cast<unsigned long long*>(ws + L.xr);
   a.kw = reinterpret_cast<uint32_t*>(ws + L.kw);
+  a.ys = reinterpret_cast<float*>(ws + L.ys);
+  a.alog = reinterpret_cast<double*>(ws + L.alog);
+  a.meta = reinterpret_cast<double*>(ws + L.meta);
+  a.imeta = reinterpret_cast<int32_t*>(ws + L.imeta);
 #ifdef OT_PROFILE
   a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + TR - 1) / TR) + 8;
 #endif
   return FIODE_OK;
 }
 
+// the adjoint sweep (weight operands in registers: VjpW): rk4 k_ot_bwd, dopri5 k_odp_bwd
+hipError_t launch_sweep(const OTArgs& a, hipStream_t st) {
+  const dim3 grid((a.B + TR - 1) / TR);
+  if (a.method == FIODE_ODE_DOPRI5) {
+    if (a.d.scale_nominal) hipLaunchKernelGGL(k_odp_bwd<true>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
+    else hipLaunchKernelGGL(k_odp_bwd<false>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
+  } else {
+    if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, grid, dim3(256), sizeof(OtBwdShared), st, a);
+    else hipLaunchKernelGGL(k_ot_bwd<false>, grid, dim3(256), sizeof(OtBwdShared), st, a);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int32_t fiode_odetrain_evals(const fiode_odetrain_config* cfg) {
   if (!cfg) return -1;
-  const int n = grid_iters(cfg);
-  return n < 0 ? -1 : 4 * (n - 1);
+  int E, A, n;
+  return solve_shape(cfg, E, A, n) < 0 ? -1 : E;
 }
 
 extern "C" size_t fiode_odetrain_workspace_bytes(const fiode_odetrain_config* cfg) {
   if (!cfg || cfg->batch <= 0) return 0;
-  const int n = grid_iters(cfg);
-  if (n < 0) return 0;
-  return ot_layout(cfg->batch, 4 * (n - 1)).total;
+  int E, A, n;
+  if (solve_shape(cfg, E, A, n) < 0) return 0;
+  return ot_layout(cfg->batch, E, A).total;
 }
 
 extern "C" int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets) {
   if (!cfg || !offsets || cfg->batch <= 0) return FIODE_EINVAL;
-  const int n = grid_iters(cfg);
-  if (n < 0) return FIODE_EINVAL;
-  const OtLayout L = ot_layout(cfg->batch, 4 * (n - 1));
-  const size_t o[FIODE_ODETRAIN_NSAVED] = {L.hs, L.ftw, L.vw, L.muw, L.nomw, L.a1, L.a2, L.gft, L.loww};
+  int E, A, n;
+  if (solve_shape(cfg, E, A, n) < 0) return FIODE_EINVAL;
+  const OtLayout L = ot_layout(cfg->batch, E, A);
+  const size_t o[FIODE_ODETRAIN_NSAVED] = {L.hs, L.ftw, L.vw, L.muw, L.nomw, L.a1, L.a2, L.gft, L.loww,
+                                           A ? L.ys : 0, A ? L.alog : 0, A ? L.meta : 0};
   for (int i = 0; i < FIODE_ODETRAIN_NSAVED; ++i) offsets[i] = (int64_t)o[i];
   return FIODE_OK;
 }
@@ -703,14 +1411,19 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   a.drop_block = fiode_internal::debug_drop_publish();
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int ntiles = (a.B + TR - 1) / TR;
-  const size_t lds = sizeof(OtShared);     // the weights live in registers (tile16.h T16W)
   // k_ot_masks zeroes the exchange granules (tags) and the status words before every forward, and
   // draws the dropout keep words when dropout is on
-  a.nslots = (int)(((size_t)a.E * 2 * ntiles * 8 + 1024) / 8);
+  const OtLayout L = ot_layout(a.B, a.E, a.A);
+  a.nslots = (int)((L.kw - L.xs) / 8);
   const int nthreads = a.nslots > a.E * a.B ? a.nslots : a.E * a.B;
   hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_ot_fwd, dim3(ntiles), dim3(256), lds, st, a);
+  if (a.method == FIODE_ODE_DOPRI5) {
+    hipLaunchKernelGGL(k_odp_fwd, dim3(ntiles), dim3(256), sizeof(OdpShared), st, a);
+  } else {
+    // the weights live in registers (tile16.h T16W)
+    hipLaunchKernelGGL(k_ot_fwd, dim3(ntiles), dim3(256), sizeof(OtShared), st, a);
+  }
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }
@@ -721,15 +1434,16 @@ namespace {
 // (m ascending, fused multiply-adds as k_lyap_static_grads), then optionally + add[b][x] * scale[0]
 // (the other loss term's x_feat gradient and its upstream scale: the combined gradient in one
 // launch).  One workgroup per image, one thread per hidden unit.
-__global__ __launch_bounds__(M) void k_ot_gx(int E, const float* __restrict__ gz1, const float* __restrict__ Qx,
-                                             const float* __restrict__ add, const float* __restrict__ scale,
-                                             float* __restrict__ gx) {
+__global__ __launch_bounds__(M) void k_ot_gx(int E, const int32_t* __restrict__ e_used, const float* __restrict__ gz1,
+                                             const float* __restrict__ Qx, const float* __restrict__ add,
+                                             const float* __restrict__ scale, float* __restrict__ gx) {
   __shared__ float gu[M];
   const int b = blockIdx.x, m = threadIdx.x;
   const float* p = gz1 + (size_t)b * E * M + m;
+  const int En = e_used ? min(E, e_used[0]) : E;     // dopri5: the evals the solve made
   float s = 0.f;
 #pragma unroll 8
-  for (int e = 0; e < E; ++e) s += p[(size_t)e * M];
+  for (int e = 0; e < En; ++e) s += p[(size_t)e * M];
   gu[m] = s;
   __syncthreads();
   if (m < FIODE_X) {
@@ -752,11 +1466,9 @@ extern "C" int fiode_odetrain_backward_x(void* stream, const fiode_odetrain_conf
   if (!g_y || !gx || (gx_add && !gx_add_scale)) return FIODE_EINVAL;
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = sizeof(OtBwdShared);     // weight operands in registers (VjpW)
-  if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(k_ot_bwd<false>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
-  FIODE_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_ot_gx, dim3(a.B), dim3(M), 0, st, a.E, (const float*)a.gz1, w->Qx, gx_add, gx_add_scale, gx);
+  FIODE_HIP_CHECK(launch_sweep(a, st));
+  hipLaunchKernelGGL(k_ot_gx, dim3(a.B), dim3(M), 0, st, a.E, a.method == FIODE_ODE_DOPRI5 ? (const int32_t*)a.imeta : nullptr,
+                     (const float*)a.gz1, w->Qx, gx_add, gx_add_scale, gx);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }
@@ -771,9 +1483,10 @@ extern "C" int fiode_odetrain_backward_weights(void* stream, const fiode_odetrai
   if (!grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
       !grads->b3)
     return FIODE_EINVAL;
-  const OtLayout L = ot_layout(a.B, a.E);
+  const OtLayout L = ot_layout(a.B, a.E, a.A);
   fiode_internal::WgradIO io{};
   io.B = a.B; io.S = a.E; io.x_feat = x_feat; io.Qx = w->Qx; io.h = a.hs; io.a1 = a.a1; io.a2 = a.a2;
+  io.s_used = a.method == FIODE_ODE_DOPRI5 ? a.imeta : nullptr;     // the evals the solve made
   io.gz2 = a.gz2; io.gz1 = a.gz1; io.gft = a.gft;
   io.workspace = static_cast<char*>(workspace) + L.wg;
   io.grads = *grads;
@@ -796,13 +1509,11 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
     return FIODE_EINVAL;
   a.g_y = g_y; a.dbg_gft = dbg_gft;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = sizeof(OtBwdShared);
-  if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(k_ot_bwd<false>, dim3((a.B + TR - 1) / TR), dim3(256), lds, st, a);
-  FIODE_HIP_CHECK(hipGetLastError());
-  const OtLayout L = ot_layout(a.B, a.E);
+  FIODE_HIP_CHECK(launch_sweep(a, st));
+  const OtLayout L = ot_layout(a.B, a.E, a.A);
   fiode_internal::WgradIO io{};
   io.B = a.B; io.S = a.E; io.x_feat = x_feat; io.Qx = w->Qx; io.h = a.hs; io.a1 = a.a1; io.a2 = a.a2;
+  io.s_used = a.method == FIODE_ODE_DOPRI5 ? a.imeta : nullptr;     // the evals the solve made
   io.gz2 = a.gz2; io.gz1 = a.gz1; io.gft = a.gft;
   io.workspace = static_cast<char*>(workspace) + L.wg;
   io.grads = *grads;

@@ -18,6 +18,7 @@ struct WgradIO {
   const float *gz2, *gz1;         // [B*S][M] gradients at the layer-2 / layer-1 pre-activations
   const float* gft;               // [B*S][C] gradient at the MLP output
   void* workspace;                // wgrad_bytes(B, S)
+  const int32_t* s_used;          // optional device count: only rows s < s_used[0] of each image count
   fiode_lyap_grads grads;         // outputs (all overwritten)
 };
 size_t wgrad_bytes(int B, int S);

@@ -73,7 +73,8 @@ class OdeConfig(ct.Structure):
 
 class OdeTrainConfig(ct.Structure):
     _fields_ = [("batch", ct.c_int32), ("dropout_mode", ct.c_int32), ("seed", ct.c_uint64), ("offset", ct.c_uint64),
-                ("t0", ct.c_double), ("t1", ct.c_double), ("step_size", ct.c_double)]
+                ("t0", ct.c_double), ("t1", ct.c_double), ("step_size", ct.c_double), ("method", ct.c_int32),
+                ("max_attempts", ct.c_int32), ("rtol", ct.c_double), ("atol", ct.c_double)]
 
 
 class SpectralConfig(ct.Structure):

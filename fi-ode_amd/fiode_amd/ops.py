@@ -271,15 +271,20 @@ def odeint_dyn(x_feat: torch.Tensor, h0: torch.Tensor, times: torch.Tensor, weig
 
 
 def odetrain_config(B: int, t0: float, t1: float, step_size: float, dropout_mode: int, seed: int = 0,
-                    offset: int = 0) -> L.OdeTrainConfig:
+                    offset: int = 0, method: str = "rk4", rtol: float = 1e-3, atol: float = 1e-3,
+                    max_attempts: int = 64) -> L.OdeTrainConfig:
+    """The differentiable train_ode solve: method 'rk4' (step_size) or 'dopri5' (rtol, atol; at most
+    max_attempts adaptive step attempts -- the eval capacity is 2 + 6 max_attempts)."""
+    m = {"rk4": L.FIODE_ODE_RK4, "dopri5": L.FIODE_ODE_DOPRI5}[method]
     return L.OdeTrainConfig(int(B), int(dropout_mode), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
-                            float(t0), float(t1), float(step_size))
+                            float(t0), float(t1), float(step_size), m, int(max_attempts), float(rtol), float(atol))
 
 
 def odetrain_evals(cfg: L.OdeTrainConfig) -> int:
     E = L.lib().fiode_odetrain_evals(ct.byref(cfg))
     if E < 0:
-        raise ValueError("odetrain: invalid time grid (need t1 > t0, step_size > 0, <= 1024 steps)")
+        raise ValueError("odetrain: invalid solve (rk4: t1 > t0, step_size > 0, <= 1024 steps; dopri5: rtol, atol > 0, "
+                         "1 <= max_attempts <= 1024)")
     return E
 
 
@@ -318,14 +323,20 @@ def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, 
 def odetrain_saved(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> Dict[str, torch.Tensor]:
     """Views of the forward's saved arrays in an odetrain workspace (for checkers)."""
     B, E = int(cfg.batch), odetrain_evals(cfg)
-    off = (ct.c_int64 * 9)()
+    off = (ct.c_int64 * 12)()
     L.check(L.lib().fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)),
             "fiode_odetrain_saved_offsets")
     f = lambda i, n: ws[off[i]:off[i] + 4 * n].view(torch.float32)
     R = B * E
-    return dict(h=f(0, R * C).view(B, E, C), ftilde=f(1, R * C).view(B, E, C), v=f(2, R * C).view(B, E, C),
-                mu=f(3, R).view(B, E), nominal=f(4, R * C).view(B, E, C), a1=f(5, R * M).view(B, E, M),
-                a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C), lower=f(8, R * C).view(B, E, C))
+    out = dict(h=f(0, R * C).view(B, E, C), ftilde=f(1, R * C).view(B, E, C), v=f(2, R * C).view(B, E, C),
+               mu=f(3, R).view(B, E), nominal=f(4, R * C).view(B, E, C), a1=f(5, R * M).view(B, E, M),
+               a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C), lower=f(8, R * C).view(B, E, C))
+    if cfg.method == L.FIODE_ODE_DOPRI5:
+        A = int(cfg.max_attempts)
+        out["ys"] = f(9, A * B * C).view(A, B, C)
+        out["attempts"] = ws[off[10]:off[10] + 8 * 8 * A].view(torch.float64).view(A, 8)
+        out["init"] = ws[off[11]:off[11] + 8 * 16].view(torch.float64)
+    return out
 
 
 def odetrain_backward(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,

@@ -184,24 +184,36 @@ FIODE_API int fiode_odeint(void* stream, const fiode_ode_config* cfg, const fiod
                            const double* times, float* solution, int32_t* stats, double* dstats,
                            void* workspace, size_t workspace_bytes);
 
-/* ---- Differentiable RK4 solve for train_ode (pl_modules.py:490-500; models.py:235-241) -------
- * y_hat = odeint(IVP.h_dot, (h0,), [t0, t1], method='rk4', options.step_size) with the dynamics in
- * TRAIN mode (fresh dropout masks per func() call), backpropagated through every stage.
- * evals E = 4 * (niters - 1), niters = ceil((t1 - t0) / step_size + 1) in float32. */
+/* ---- Differentiable solve for train_ode (pl_modules.py:490-500; models.py:235-241) -----------
+ * y_hat = odeint(IVP.h_dot, (h0,), [t0, t1], method, ...) with the dynamics in TRAIN mode (fresh
+ * dropout masks per func() call), backpropagated directly through the solve (use_adjoint False):
+ *   FIODE_ODE_RK4:    options.step_size; evals E = 4 * (niters - 1), niters = ceil((t1 - t0) /
+ *                     step_size + 1) in float32;
+ *   FIODE_ODE_DOPRI5: rtol, atol (make_solver_params('dopri5', tol): rtol = atol = tol), torchdiffeq
+ *                     0.2.2's adaptive solver incl. the gradient through its step-size controller;
+ *                     E = 2 + 6 max_attempts is the eval CAPACITY (the solve's count: stats[0]);
+ *                     more attempts than max_attempts (torchdiffeq: unbounded) -> stats[3] = 2 and a
+ *                     NaN y_out.  Eval e of attempt n is 2 + 6 n + i (evals 0, 1: initial step). */
 typedef struct fiode_odetrain_config {
   int32_t batch;         /* B (<= FIODE_ODE_MAX_BATCH)                                          */
   int32_t dropout_mode;  /* FIODE_DROPOUT_*; GIVEN: masks [E][2][B][M] uint8 0/1               */
   uint64_t seed;         /* Philox key                                                          */
   uint64_t offset;       /* Philox counter offset                                               */
   double t0, t1;         /* ts = [t0, t1] (linspace(0, t_max, 2))                               */
-  double step_size;      /* make_solver_params('rk4', tol): options.step_size = tol             */
+  double step_size;      /* rk4: make_solver_params('rk4', tol): options.step_size = tol        */
+  int32_t method;        /* FIODE_ODE_RK4 (0) or FIODE_ODE_DOPRI5                               */
+  int32_t max_attempts;  /* dopri5: attempt capacity (1 .. FIODE_ODETRAIN_MAX_ATTEMPTS)         */
+  double rtol, atol;     /* dopri5                                                              */
 } fiode_odetrain_config;
+#define FIODE_ODETRAIN_MAX_ATTEMPTS 1024
 
 FIODE_API int32_t fiode_odetrain_evals(const fiode_odetrain_config* cfg);
 /* The workspace also carries the forward's saved activations to the backward. */
 FIODE_API size_t fiode_odetrain_workspace_bytes(const fiode_odetrain_config* cfg);
-/* y_out [B][C] = y(t1); stats (device int32[8]): nfe, steps, last QP exit iteration.
- * offset_dev: optional device addend of the Philox offset (graph replay). */
+/* y_out [B][C] = y(t1); stats (device int32[8]): nfe, accepted steps, last QP exit iteration, status
+ * (0 ok, 2 attempt capacity exhausted, 3 dt underflow, 4 a cross-workgroup exchange timed out), and
+ * for dopri5 n_accept, n_reject, attempts.  offset_dev: optional device addend of the Philox offset
+ * (graph replay). */
 FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
                                      const fiode_dyn_weights* w, const float* x_feat, const float* h0,
                                      const uint8_t* masks, const uint64_t* offset_dev, float* y_out,
@@ -209,9 +221,11 @@ FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* 
 /* Byte offsets inside the workspace of the forward's saved arrays, for checkers (offsets:
  * int64[FIODE_ODETRAIN_NSAVED]): [0] stage inputs [B][E][C], [1] MLP outputs [B][E][C], [2] QP
  * outputs v [B][E][C], [3] QP mu [B][E], [4] QP nominal [B][E][C], [5] a1 [B][E][M], [6] a2
- * [B][E][M], [7] dL/d mlp output [B][E][C] (after the backward), [8] QP lower bound [B][E][C].
- * Row (b, e) = b*E + e. */
-#define FIODE_ODETRAIN_NSAVED 9
+ * [B][E][M], [7] dL/d mlp output [B][E][C] (after the backward), [8] QP lower bound [B][E][C];
+ * dopri5 only (else 0): [9] y_n of every attempt [A][B][C] float, [10] the attempt log [A][8]
+ * double (t_n, dt_n, error ratio, accepted, eval of k_0, eval of stage 0), [11] the initial step
+ * [16] double (d0, d1, d2, h0, h1, clamp0, clamp1, dt0, rms(f1 - f0)).  Row (b, e) = b*E + e. */
+#define FIODE_ODETRAIN_NSAVED 12
 FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets);
 /* Given g_y = dL/dy(t1) [B][C]: all weight gradients and dL/dx_feat (overwritten).  Must follow
  * fiode_odetrain_forward on the same workspace.  dbg_gft: optional [B][E][C] dL/d mlp output. */
