@@ -51,7 +51,7 @@ FLOP_ROW = {"k_lyap_fwd": 2 * FLOP_ROW_FWD_PASS,                   # loss pass +
             "k_lyap_bwd": 2 * (128 * 128 + 128 * 10) + FLOP_ROW_FWD_PASS}
 
 
-def build_module(dev, seed=0, train_ode=False):
+def build_module(dev, seed=0, train_ode=False, solver="rk4"):
     from fiode_amd.dynamics import OrthoClassDynProjectSimplexLips
     from fiode_amd.lyapunov import LyapunovLearning, UniformInitFun, DecisionBoundary
     from fiode_amd.models import make_ortho_KWLarge_Concat
@@ -70,7 +70,8 @@ def build_module(dev, seed=0, train_ode=False):
                            sampler_scheduler=sched, dynamics=dyn, init_fun=UniformInitFun((10,), backbone),
                            lya_cand=DecisionBoundary(on_simplex=True), t_max=1.0, opt_name="Adam", lr=5e-3,
                            train_ode=train_ode, train_ode_epoch=TRAIN_ODE_EPOCH,
-                           train_ode_solver="rk4" if train_ode else "dopri5", train_ode_tol=0.1 if train_ode else 1e-3,
+                           train_ode_solver=solver if train_ode else "dopri5",
+                           train_ode_tol=(0.1 if solver == "rk4" else 1e-3) if train_ode else 1e-3,
                            val_ode_solver="dopri5", val_ode_tol=1e-3,
                            weight_decay=0.0, warmup=-1, max_epochs=300, simplex=True, act="relu", val_adv=False,
                            seed=seed)
@@ -199,9 +200,9 @@ def main():
     dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     torch.cuda.set_device(dev)
 
-    def timed_run(train_ode: bool, steps: int, warmup: int):
+    def timed_run(train_ode: bool, steps: int, warmup: int, solver: str = "rk4"):
         """Build the module, capture (or not) the step, run warmup + timed steps; max over ranks."""
-        mod = build_module(dev, seed=0, train_ode=train_ode)
+        mod = build_module(dev, seed=0, train_ode=train_ode, solver=solver)
         mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
         opt = mod.configure_optimizers(capturable=not args.eager)[0][0]
         params = [p for p in mod.parameters() if p.requires_grad]
@@ -265,11 +266,20 @@ def main():
     elapsed, mod, x, y, health = timed_run(train_ode, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B_PER_RANK * args.steps / elapsed
-    lyap_only = None
+    lyap_only = dopri5_step = None
     if train_ode and not args.no_secondary:
         e2, _, _, _, _ = timed_run(False, args.steps, args.warmup)
         lyap_only = {"images_per_s": round(world * B_PER_RANK * args.steps / e2, 2),
                      "ms_per_step": round(e2 / args.steps * 1e3, 4)}
+        # BASELINE configs[2]: the same train step with the YAML's own train_ode solver (dopri5, tol
+        # 1e-3: cifar_train.yaml:30,32), backprop through the adaptive solve
+        e3, m3, _, _, h3 = timed_run(True, args.steps, args.warmup, solver="dopri5")
+        st3 = m3.last_ode_plan["stats"].cpu().tolist()
+        dopri5_step = {"images_per_s": round(world * B_PER_RANK * args.steps / e3, 2),
+                       "ms_per_step": round(e3 / args.steps * 1e3, 4), "device_status": h3,
+                       "last_solve": {"nfe": st3[0], "n_accept": st3[4], "n_reject": st3[5]},
+                       "workload": "BASELINE configs[2]: the configs[1] step with train_ode_solver dopri5, "
+                                   "train_ode_tol 1e-3 (rtol = atol), direct backprop through the adaptive solve"}
 
     # ---- per-kernel timing of the fused hot path with HIP events (same inputs as a step) ----
     from fiode_amd import _lib as L, ops
@@ -343,6 +353,7 @@ def main():
            "roofline": roofline,
            "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)},
            "lyapunov_only_step": lyap_only,
+           "dopri5_train_step": dopri5_step,
            "device_status": health,
            "runtime_env": {"DEBUG_HIP_FORCE_GRAPH_QUEUES": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES")}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -517,18 +517,28 @@ class LyapunovLearning(nn.Module):
                                "the step's loss is NaN")
 
     def ode_plan(self, batch: int, masks: Optional[torch.Tensor] = None) -> dict:
-        """Solver plan of the train_ode solve (make_solver_params(train_ode_solver, train_ode_tol))."""
+        """Solver plan of the train_ode solve (make_solver_params(train_ode_solver, train_ode_tol),
+        pl_modules.py:24-35): 'rk4' with options.step_size = tol, or 'dopri5' with rtol = atol = tol
+        (cifar_train.yaml:30,32), at most ``train_ode_max_attempts`` adaptive step attempts (the eval
+        capacity of the device solve; torchdiffeq has no cap -- more attempts report status 2 and a
+        NaN loss, see check_device_status)."""
         if self.use_adjoint:
             raise NotImplementedError("odeint_adjoint (SURVEY.md section 8f row 3)")
-        if self.train_ode_solver != "rk4":
-            raise NotImplementedError(f"train_ode with {self.train_ode_solver!r}: the differentiable HIP solve is the "
-                                      "fixed-grid rk4 (BASELINE config 2); adaptive backprop is section 8f row 3")
-        step = make_solver_params("rk4", self.train_ode_tol)["options"]["step_size"]
+        if self.train_ode_solver not in ("rk4", "dopri5"):
+            raise NotImplementedError(f"train_ode with {self.train_ode_solver!r}: the differentiable HIP solves are "
+                                      "'rk4' and 'dopri5'")
         mode = L.FIODE_DROPOUT_PHILOX if self.training else L.FIODE_DROPOUT_OFF
         if masks is not None:
             mode = L.FIODE_DROPOUT_GIVEN
-        cfg = ops.odetrain_config(batch, 0.0, float(self.t_max), float(step), mode, seed=self.seed,
-                                  offset=self._rng_offset if self.rng_counter is None else 0)
+        sp = make_solver_params(self.train_ode_solver, self.train_ode_tol)
+        off = self._rng_offset if self.rng_counter is None else 0
+        if self.train_ode_solver == "rk4":
+            cfg = ops.odetrain_config(batch, 0.0, float(self.t_max), float(sp["options"]["step_size"]), mode,
+                                      seed=self.seed, offset=off)
+        else:
+            cfg = ops.odetrain_config(batch, 0.0, float(self.t_max), 0.0, mode, seed=self.seed, offset=off,
+                                      method="dopri5", rtol=float(sp["rtol"]), atol=float(sp["atol"]),
+                                      max_attempts=int(getattr(self, "train_ode_max_attempts", 64)))
         return dict(dyn=self.dyn_fun.dyn_cfg(), cfg=cfg, masks=masks, offset_dev=self.rng_counter)
 
     def _ode_launch(self, static_state, w, masks=None):

@@ -174,3 +174,35 @@ def test_odetrain_backward_parts_host_checks():
     g.Q2 = None
     assert lib.fiode_odetrain_backward_weights(None, ct.byref(cfg), ct.byref(dyn), ct.byref(w), d, ct.byref(g), d,
                                                big) == 1
+
+
+def test_odetrain_dopri5_shape_on_host():
+    """The dopri5 train_ode solve's host-side shape (no kernel): eval capacity 2 + 6 max_attempts,
+    the dopri5 extras in the saved offsets, invalid tolerances / capacities refused; the module's
+    plan for the YAML's train_ode_solver dopri5 (cifar_train.yaml:30,32) is a dopri5 config with
+    rtol = atol = train_ode_tol."""
+    import ctypes as ct
+    from fiode_amd import _lib, ops
+    lib = _lib.lib()
+    cfg = ops.odetrain_config(128, 0.0, 1.0, 0.0, _lib.FIODE_DROPOUT_PHILOX, method="dopri5", rtol=1e-3, atol=1e-3,
+                              max_attempts=64)
+    assert lib.fiode_odetrain_evals(ct.byref(cfg)) == 2 + 6 * 64
+    rk = ops.odetrain_config(128, 0.0, 1.0, 0.1, _lib.FIODE_DROPOUT_PHILOX)
+    assert lib.fiode_odetrain_evals(ct.byref(rk)) == 40
+    assert lib.fiode_odetrain_workspace_bytes(ct.byref(cfg)) > lib.fiode_odetrain_workspace_bytes(ct.byref(rk))
+    off = (ct.c_int64 * 12)()
+    assert lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)) == 0
+    assert all(off[i] > 0 for i in (9, 10, 11))
+    assert lib.fiode_odetrain_saved_offsets(ct.byref(rk), ct.cast(off, ct.c_void_p)) == 0
+    assert all(off[i] == 0 for i in (9, 10, 11))
+    for bad in (dict(rtol=0.0), dict(max_attempts=0), dict(max_attempts=5000)):
+        kw = dict(rtol=1e-3, atol=1e-3, max_attempts=64)
+        kw.update(bad)
+        c = ops.odetrain_config(128, 0.0, 1.0, 0.0, _lib.FIODE_DROPOUT_PHILOX, method="dopri5", **kw)
+        assert lib.fiode_odetrain_evals(ct.byref(c)) == -1
+        assert lib.fiode_odetrain_workspace_bytes(ct.byref(c)) == 0
+    import bench
+    import torch
+    mod = bench.build_module(torch.device("cpu"), train_ode=True, solver="dopri5")
+    plan = mod.ode_plan(128)
+    assert plan["cfg"].method == _lib.FIODE_ODE_DOPRI5 and plan["cfg"].rtol == plan["cfg"].atol == 1e-3

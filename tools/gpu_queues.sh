@@ -1,10 +1,18 @@
 #!/bin/bash
-# step time vs the hipGraph executor's queue count (one process per setting; not a test)
+# The captured step under several graph-executor queue settings (not a test), one process each,
+# with native backtraces on a host fault (tools/probes/graph_queue_probe.py).
+# usage (via gpurun): bash tools/gpu_queues.sh <tag> [settings...]   ("unset" = the runtime default)
 set -u
-export TMPDIR=/tmp
-O=gpurun_out/queues; mkdir -p $O
-# (6 and 8 make this ROCm runtime segfault: not run; any failure ends the script)
-for Q in ${QS:-3 4 2 5}; do
-  DEBUG_HIP_FORCE_GRAPH_QUEUES=$Q timeout -k 10 200 python tools/ab_step.py 4 default > $O/q$Q.log 2>&1 || { echo "Q=$Q failed"; exit 1; }
-  echo "Q=$Q $(grep '{' $O/q$Q.log | cut -c1-60)"
+TAG=$1; shift
+O=gpurun_out/$TAG; mkdir -p $O
+for Q in "$@"; do
+  if [ "$Q" = unset ]; then
+    timeout -k 10 150 python tools/probes/graph_queue_probe.py 30 > $O/q_$Q.log 2>&1
+  else
+    DEBUG_HIP_FORCE_GRAPH_QUEUES=$Q timeout -k 10 150 python tools/probes/graph_queue_probe.py 30 > $O/q_$Q.log 2>&1
+  fi
+  rc=$?
+  echo "queues=$Q rc=$rc: $(tail -1 $O/q_$Q.log)"
+  if [ $rc -ne 0 ] && [ $rc -ne 139 ] && [ $rc -ne 134 ]; then echo "stopping: rc $rc"; exit 1; fi
+  if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit 1; fi
 done
