@@ -13,6 +13,6 @@ for Q in "$@"; do
   fi
   rc=$?
   echo "queues=$Q rc=$rc: $(tail -1 $O/q_$Q.log)"
-  if [ $rc -ne 0 ] && [ $rc -ne 139 ] && [ $rc -ne 134 ]; then echo "stopping: rc $rc"; exit 1; fi
-  if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit 1; fi
+  # a fault, abort, time limit or any failure ends the call: nothing more runs on the GPU
+  if [ $rc -ne 0 ]; then echo "stopping: rc $rc"; exit 1; fi
 done
