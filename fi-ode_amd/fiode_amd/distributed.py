@@ -6,10 +6,11 @@ whole fan-out on its own images, DDP all-reduces the gradients (bucketed, 25 MB)
 reduces each logged scalar with its own collective.  The path has one real exchange step (the
 gradient mean) and one bookkeeping exchange (the logged means), so here:
 
-* ``GradAllReducer``  -- one persistent flat fp32 bucket holding every trainable gradient
-  (~2.6 M floats = 10.5 MB for the README model: a single RCCL ring all-reduce, well under one
-  xGMI link's latency-bandwidth knee, instead of DDP's per-bucket launches); the views of
-  ``p.grad`` point INTO the bucket, so no pack/unpack copies are made.
+* ``GradAllReducer``  -- one persistent flat fp32 buffer holding every trainable gradient
+  (~2.6 M floats = 10.5 MB for the README model), laid out in the order the backward finalises
+  the gradients and all-reduced in a few contiguous buckets -- inside the captured step, each as
+  soon as its gradients are final, overlapping the rest of the backward (DDP's bucketing); the
+  views of ``p.grad`` point INTO the buffer, so no pack/unpack copies are made.
 * ``MetricReducer``   -- the logged scalars of a step packed into one small tensor, one
   all-reduce (SUM, divided by world) instead of one collective per ``self.log``.
 * ``shard_range``     -- contiguous image shards for certification / validation (no collective
@@ -51,11 +52,25 @@ def shard_range(n: int, rank: int, world: int) -> range:
 
 
 class GradAllReducer:
-    """Mean of the gradients over ranks with ONE all-reduce of one persistent flat bucket.
+    """Mean of the gradients over ranks from one persistent flat bucket, all-reduced in a few
+    contiguous BUCKETS that follow the order in which the backward finalises the gradients (DDP's
+    bucketing, sl_pipeline.py:157-170 via Lightning's DDP strategy).
 
-    After construction ``p.grad`` of every parameter is a view into ``self.flat`` (the optimizer
-    and autograd accumulate into it in place), so ``allreduce()`` is a single collective plus one
-    scale, with no gather/scatter copies.  Parameters are laid out in ``parameters()`` order.
+    ``p.grad`` of every parameter is a view into ``self.flat``.  Two ways to run the collective:
+
+    * ``allreduce()`` -- after the backward (eager, between graph replays; any backend): one
+      all-reduce per bucket, then the 1/world scale;
+    * ``arm(world, stream)`` before the backward and ``finish()`` after it -- a post-accumulate
+      hook per parameter moves each fresh gradient into its bucket view and, once a bucket's last
+      parameter has its gradient, launches that bucket's all-reduce on ``stream`` (ordered after the
+      producing stream), so the collective of the early buckets runs while the rest of the backward
+      does; ``finish()`` launches what is left and joins.  Used by GraphTrainStep with RCCL, where
+      the whole step (collectives included) is one captured graph.
+
+    The bucket layout comes from ``plan_buckets(order, cap_bytes)``: ``order`` = the parameters in
+    the order their gradients became final in a warm-up backward (``record_order``), the flat
+    bucket laid out in that order and cut into buckets of about ``cap_bytes``.  Until then: one
+    bucket in ``params`` order.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None):
@@ -69,27 +84,82 @@ class GradAllReducer:
         self.group = group
         self.numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.numel, dtype=self.params[0].dtype, device=dev)
-        o = 0
-        for p in self.params:
-            n = p.numel()
-            view = self.flat[o:o + n].view_as(p)
+        self._hooks = []
+        self._armed = None
+        self._order_log = None
+        self._layout(list(self.params), [len(self.params)])
+        for p, v in zip(self.params, self.views):
             if p.grad is not None:
-                view.copy_(p.grad)
-            p.grad = view
-            o += n
+                v.copy_(p.grad)
+            p.grad = v
 
+    # ---- layout ------------------------------------------------------------------------------
+    def _layout(self, order, cuts):
+        """Flat bucket in ``order``; bucket k = parameters order[cuts[k-1]:cuts[k]]."""
+        self.order = order
+        self.views = [None] * len(self.params)
+        pos = {id(p): i for i, p in enumerate(self.params)}
+        o = 0
+        starts = []
+        for p in order:
+            starts.append(o)
+            self.views[pos[id(p)]] = self.flat[o:o + p.numel()].view_as(p)
+            o += p.numel()
+        self.buckets = []                 # (lo, hi) flat ranges; members as positions in params
+        self.members = []
+        lo_i = 0
+        for c in cuts:
+            lo = starts[lo_i]
+            hi = starts[c] if c < len(order) else self.numel
+            self.buckets.append((lo, hi))
+            self.members.append([pos[id(p)] for p in order[lo_i:c]])
+            lo_i = c
+        self.bucket_of = [0] * len(self.params)
+        for k, m in enumerate(self.members):
+            for i in m:
+                self.bucket_of[i] = k
+
+    def plan_buckets(self, order: Sequence[torch.nn.Parameter], cap_bytes: int = 4 << 20):
+        """Lay the bucket out in ``order`` (gradients' ready order) and cut it every ~cap_bytes
+        (a parameter never straddles two buckets)."""
+        seen = {id(p) for p in order}
+        order = list(order) + [p for p in self.params if id(p) not in seen]
+        cuts, acc = [], 0
+        for i, p in enumerate(order):
+            acc += p.numel() * p.element_size()
+            if acc >= cap_bytes and i + 1 < len(order):
+                cuts.append(i + 1)
+                acc = 0
+        cuts.append(len(order))
+        grads = [p.grad.detach().clone() if p.grad is not None else None for p in self.params]
+        self._layout(order, cuts)
+        for p, v, g in zip(self.params, self.views, grads):
+            if g is not None:
+                v.copy_(g)
+            else:
+                v.zero_()
+            p.grad = v
+
+    def record_order(self):
+        """Start logging the order in which the next backward finalises the gradients."""
+        self._order_log = []
+        if not self._hooks:
+            for i, p in enumerate(self.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self._on_grad(i)))
+
+    def recorded_order(self) -> List[torch.nn.Parameter]:
+        log, self._order_log = self._order_log or [], None
+        return [self.params[i] for i in log]
+
+    # ---- collectives ------------------------------------------------------------------------------
     def rebind(self):
         """Re-point grads into the bucket (after something replaced p.grad, e.g. set_to_none)."""
-        o = 0
-        for p in self.params:
-            n = p.numel()
-            view = self.flat[o:o + n].view_as(p)
+        for p, v in zip(self.params, self.views):
             if p.grad is None:
-                view.zero_()
-            elif p.grad.data_ptr() != view.data_ptr():
-                view.copy_(p.grad)
-            p.grad = view
-            o += n
+                v.zero_()
+            elif p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+            p.grad = v
 
     def zero_grad(self):
         self.flat.zero_()
@@ -99,27 +169,88 @@ class GradAllReducer:
         None, so AccumulateGrad stole its results instead of adding them into the bucket one kernel
         per parameter) into the bucket with ONE multi-tensor copy, and re-point p.grad at the bucket
         views.  A parameter that received no gradient gets zeros."""
-        views, o = [], 0
-        for p in self.params:
-            n = p.numel()
-            views.append(self.flat[o:o + n].view_as(p))
-            o += n
-        have = [(v, p.grad) for v, p in zip(views, self.params) if p.grad is not None]
+        have = [(v, p.grad) for v, p in zip(self.views, self.params) if p.grad is not None]
         if have:
             torch._foreach_copy_([v for v, _ in have], [g for _, g in have])
-        for v, p in zip(views, self.params):
+        for v, p in zip(self.views, self.params):
             if p.grad is None:
                 v.zero_()
             p.grad = v
         return self.flat
 
-    def allreduce(self, world: Optional[int] = None):
+    def allreduce(self, world: Optional[int] = None, force: bool = False):
         world = dist.get_world_size(self.group) if world is None else world
-        if world > 1:
+        if world > 1 or force:
             self.rebind()
-            dist.all_reduce(self.flat, group=self.group)
+            for lo, hi in self.buckets:
+                dist.all_reduce(self.flat[lo:hi], group=self.group)
             self.flat.div_(world)
         return self.flat
+
+    def arm(self, world: int, stream: torch.cuda.Stream, force: bool = False):
+        """Overlapped all-reduce of the next backward (see the class docstring).  The backward must
+        run with p.grad = None (GraphTrainStep does)."""
+        if not self._hooks:
+            for i, p in enumerate(self.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self._on_grad(i)))
+        self._armed = dict(world=world, stream=stream, force=force, left=[len(m) for m in self.members],
+                           fresh=[None] * len(self.params), done=[False] * len(self.buckets), keep=[])
+
+    def _on_grad(self, i):
+        if self._order_log is not None:
+            self._order_log.append(i)
+        st = self._armed
+        if st is None:
+            return
+        # the gradient was produced on the hook's current stream (autograd runs a node on its
+        # forward's stream, side streams included): the comm stream waits for every one of them
+        st["stream"].wait_stream(torch.cuda.current_stream(st["stream"].device))
+        k = self.bucket_of[i]
+        p = self.params[i]
+        st["fresh"][i] = p.grad
+        st["left"][k] -= 1
+        if st["left"][k] == 0:
+            self._launch(k)
+
+    def _launch(self, k):
+        st = self._armed
+        comm = st["stream"]
+        comm.wait_stream(torch.cuda.current_stream(comm.device))
+        with torch.cuda.stream(comm):
+            pairs = []
+            for i in self.members[k]:
+                g = st["fresh"][i]
+                v = self.views[i]
+                if g is None:
+                    v.zero_()
+                elif g.data_ptr() != v.data_ptr():
+                    pairs.append((v, g))
+                    g.record_stream(comm)         # read on the comm stream: no reuse before that
+                    st["keep"].append(g)
+                self.params[i].grad = v
+            if pairs:
+                torch._foreach_copy_([v for v, _ in pairs], [g for _, g in pairs])
+            lo, hi = self.buckets[k]
+            if st["world"] > 1 or st["force"]:
+                dist.all_reduce(self.flat[lo:hi], group=self.group)
+        st["done"][k] = True
+
+    def finish(self):
+        """Launch the buckets the backward left (parameters without a gradient), join the comm
+        stream, scale by 1/world."""
+        st = self._armed
+        for k in range(len(self.buckets)):
+            if not st["done"][k]:
+                self._launch(k)
+        main = torch.cuda.current_stream(self.flat.device)
+        main.wait_stream(st["stream"])
+        if st["world"] > 1 or st["force"]:
+            self.flat.div_(st["world"])
+        self._armed = None
+        return self.flat
+
+    def grads_in_param_order(self) -> torch.Tensor:
+        return torch.cat([v.reshape(-1) for v in self.views])
 
 
 class MetricReducer:

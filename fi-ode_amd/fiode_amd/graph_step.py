@@ -12,8 +12,13 @@ the Cayley inverses are all device-side), so it is captured once and replayed:
 * ``opt`` graph: the Adam step (``capturable=True``: step counts on the device);
 * maps_ahead: the conv layers' Cayley maps of the NEXT step are computed inside this one (see
   ``_maps_ahead_on``).
-For one rank both are captured into a single graph; for N ranks the RCCL gradient all-reduce
-and the metric reduce run eagerly between the two replays.
+For one rank both are captured into a single graph.  For N ranks over RCCL (comm "graph") too:
+the gradient buffer is laid out in the order the warm-up backward finalised the gradients and
+cut into ~4 MB buckets, and each bucket's all-reduce is captured on a comm stream as soon as its
+last gradient is final (GradAllReducer.arm / finish), so the collectives of the early buckets (the
+dynamics, the head and the 4096 -> 512 CayleyLinear) overlap the rest of the backward (the conv
+stack) -- DDP's bucketed overlap (sl_pipeline.py:157-170), one replay per step.  Over gloo
+(comm "eager": not capturable) the bucket all-reduces run between two replays.
 
 Static inputs: ``step(x, y)`` copies the batch into the captured input buffers.  What the
 captured step bakes in (and ``GraphTrainStep`` checks on every call): the sampler plan of the
@@ -29,13 +34,26 @@ import torch
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
-                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True):
+                 warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
+                 comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
         self.module, self.opt, self.reducer, self.world, self.act = module, optimizer, reducer, world, act
         self.check_every, self.n_replays = int(check_every), 0
         self.piped, self.early = [], False
+        # N ranks: "graph" = the bucket all-reduces captured in the step (RCCL); "eager" = between
+        # replays (gloo, or any backend on request).  force_comm: run the collectives even at
+        # world 1 (the capture path's test on one GPU).
+        self.force_comm = bool(force_comm)
+        multi = reducer is not None and (world > 1 or self.force_comm)
+        if comm is None:
+            import torch.distributed as dist
+            comm = "graph" if (multi and dist.is_initialized() and dist.get_backend() == "nccl") else "eager"
+        if comm not in ("graph", "eager"):
+            raise ValueError(f"comm must be 'graph' or 'eager', got {comm!r}")
+        self.comm = comm if multi else "none"
+        self.comm_stream = torch.cuda.Stream(dev) if self.comm == "graph" else None
         dyn = module.dyn_fun
         if module.global_step < dyn.kappa_length:
             raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
@@ -60,8 +78,12 @@ class GraphTrainStep:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self._fwd_bwd()
+            for it in range(warmup):
+                if it == 0 and multi:
+                    reducer.record_order()          # the order the backward finalises the gradients
+                self._fwd_bwd(bucket_plan=False)
+                if it == 0 and multi:
+                    reducer.plan_buckets(reducer.recorded_order(), bucket_bytes)
                 self._between()
                 self.opt.step()
         torch.cuda.current_stream(dev).wait_stream(side)
@@ -69,22 +91,23 @@ class GraphTrainStep:
         self._restore(snap)
         torch.cuda.synchronize(dev)
 
-        self.single = world == 1
+        self.single = world == 1 and not self.force_comm
         if maps_ahead:
             self._maps_ahead_on()
+        self.one_graph = self.single or self.comm == "graph"
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
             self.loss = self._fwd_bwd()
-            if self.single:
+            if self.one_graph:
                 self.opt.step()
                 self._refresh_late()
         self.g_opt = None
-        if not self.single:
+        if not self.one_graph:
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt):
                 self.opt.step()
                 self._refresh_late()
-        if self.reducer is not None and world > 1:
+        if self.reducer is not None and (world > 1 or self.force_comm):
             views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
                      + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
             if not all(views):
@@ -176,20 +199,27 @@ class GraphTrainStep:
                         v.zero_()        # state created by the warm-up: its initial value (Adam: 0)
             self.module.rng_counter.copy_(counter)
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, bucket_plan: bool = True):
         m = self.module
         for p in self.params:
             p.grad = None
+        overlap = self.comm == "graph" and bucket_plan
+        if overlap:
+            self.reducer.arm(self.world, self.comm_stream, force=self.force_comm)
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         loss.backward()
-        if self.reducer is not None and self.world > 1:
+        if overlap:
+            self.reducer.finish()                 # the last buckets, join the comm stream, 1/world
+        elif self.comm != "none":
             self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)
         return loss
 
-    def _between(self):
-        if self.reducer is not None and self.world > 1:
-            self.reducer.allreduce(self.world)
+    def _between(self, warmup: bool = True):
+        # eager collectives: every warm-up iteration (the captured step has none of its own when
+        # comm is "graph"), and between the two replays when comm is "eager"
+        if self.comm == "eager" or (self.comm == "graph" and warmup):
+            self.reducer.allreduce(self.world, force=self.force_comm)
 
     def step(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None):
         m = self.module
@@ -205,8 +235,8 @@ class GraphTrainStep:
         if y is not None:
             self.static_y.copy_(y, non_blocking=True)
         self.g_fb.replay()
-        if not self.single:
-            self._between()
+        if not self.one_graph:
+            self._between(warmup=False)
             self.g_opt.replay()
         m.global_step += 1
         self.n_replays += 1

@@ -329,9 +329,21 @@ class LyapunovLearning(nn.Module):
             loss = F.nll_loss(torch.log(torch.clamp(net_out, min=1e-12)), y)
         else:
             loss = F.cross_entropy(net_out, y)
-        self.log("validation_loss", loss)
-        self.log("validation_error", error)
-        self.log("validation_adv_error", error)
+        # self.log(..., sync_dist=True) (pl_modules.py:217-219): the mean over ranks, all three
+        # values in one all-reduce (distributed.MetricReducer); a single process logs its own
+        from .distributed import MetricReducer
+        import torch.distributed as dist
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if world > 1:
+            red = MetricReducer(["validation_loss", "validation_error"], loss.device).reduce(
+                {"validation_loss": loss, "validation_error": error}, world)
+            self.log("validation_loss", red["validation_loss"])
+            self.log("validation_error", red["validation_error"])
+            self.log("validation_adv_error", red["validation_error"])
+        else:
+            self.log("validation_loss", loss)
+            self.log("validation_error", error)
+            self.log("validation_adv_error", error)
         return loss
 
     # Lightning-like surface -------------------------------------------------------------------

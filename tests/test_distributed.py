@@ -118,3 +118,106 @@ def test_shard_range_covers_exactly():
         for w in (1, 2, 3, 8):
             seen = [i for r in range(w) for i in shard_range(n, r, w)]
             assert seen == list(range(n))
+
+
+def _bucket_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        import pathlib
+        root = pathlib.Path(__file__).resolve().parents[1]
+        sys.path[:0] = [str(root), str(root / "fi-ode_amd")]
+        from fiode_amd.distributed import GradAllReducer
+        torch.manual_seed(0)
+        params = [torch.nn.Parameter(torch.randn(s)) for s in ((300,), (17, 5), (4096,), (3,), (1000, 2))]
+        red = GradAllReducer(params)
+        g = torch.Generator().manual_seed(10 + rank)
+        grads = [torch.randn(p.shape, generator=g) for p in params]
+        # the ready order of a backward: reversed parameter order; ~4 KB buckets
+        red.plan_buckets(list(reversed(params)), cap_bytes=4096)
+        for p, gr in zip(params, grads):
+            p.grad.copy_(gr)
+        red.allreduce(world)
+        q.put((rank, (len(red.buckets), [p.grad.clone() for p in params], grads,
+                      red.grads_in_param_order().clone())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_is_mean_two_ranks():
+    """GradAllReducer laid out in a ready order and cut into several buckets: after the bucket
+    all-reduces every p.grad (a view into the flat buffer) is the mean of the ranks' gradients."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    nb, g0, raw0, flat0 = out[0]
+    _, g1, raw1, _ = out[1]
+    assert nb >= 3
+    for a, b, r0, r1 in zip(g0, g1, raw0, raw1):
+        torch.testing.assert_close(a, (r0 + r1) / 2, rtol=1e-6, atol=1e-7)
+        assert torch.equal(a, b)
+    assert torch.equal(flat0, torch.cat([g.reshape(-1) for g in g0]))
+
+
+def _val_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        import pathlib
+        root = pathlib.Path(__file__).resolve().parents[1]
+        sys.path[:0] = [str(root), str(root / "fi-ode_amd")]
+        from fiode_amd.lyapunov import LyapunovLearning
+
+        class _Stub(LyapunovLearning):
+            """validation_step's logging with the solve replaced by fixed per-rank outputs (the
+            HIP solve needs a GPU; the sync is what is tested)."""
+            def __init__(self, out):
+                torch.nn.Module.__init__(self)
+                self.simplex, self.logged, self._o = True, {}, out
+
+            def forward(self, x, t_steps=2, return_traj=False):
+                return self._o
+
+        g = torch.Generator().manual_seed(3 + rank)
+        out = torch.softmax(torch.randn(16, 10, generator=g), -1)
+        y = torch.randint(0, 10, (16,), generator=g)
+        m = _Stub(out)
+        m.validation_step((torch.zeros(16, 3, 32, 32), y))
+        local_loss = torch.nn.functional.nll_loss(torch.log(out), y)
+        local_err = (out.argmax(-1) != y).float().mean()
+        q.put((rank, ({k: float(v) for k, v in m.logged.items()}, float(local_loss), float(local_err))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_validation_metrics_synced_two_ranks():
+    """validation_step logs validation_loss / error / adv_error with sync_dist=True
+    (pl_modules.py:217-219): every rank logs the mean over ranks."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_val_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    (l0, a0, e0), (l1, a1, e1) = out[0], out[1]
+    assert l0 == l1
+    assert abs(l0["validation_loss"] - (a0 + a1) / 2) < 1e-6
+    assert abs(l0["validation_error"] - (e0 + e1) / 2) < 1e-6
+    assert l0["validation_adv_error"] == l0["validation_error"]

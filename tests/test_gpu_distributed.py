@@ -70,7 +70,8 @@ def _rank_main(rank, world, port, q):
         red = metrics.reduce({"training_loss": sc[0], "effective_batch_size": sc[1],
                               "mean_active_constraints": sc[2]}, world)
         torch.cuda.synchronize()
-        q.put((rank, dict(bucket=reducer.flat.cpu().numpy().copy(), solo=solo.cpu().numpy(),
+        q.put((rank, dict(bucket=reducer.grads_in_param_order().cpu().numpy().copy(), solo=solo.cpu().numpy(),
+                          nbuckets=len(reducer.buckets), comm=gs.comm,
                           solo_sc=solo_sc.cpu().numpy(), sc=sc.cpu().numpy().copy(),
                           solo_ode=solo_ode.cpu().numpy(), ode=mod.last_ode_plan["stats"].cpu().numpy(),
                           red={k: float(v) for k, v in red.items()})))
@@ -98,6 +99,7 @@ def test_two_rank_graph_step_is_ddp_mean():
         if isinstance(v, Exception):
             raise v
     a, b = out[0], out[1]
+    assert a["comm"] == "eager" and a["nbuckets"] >= 2        # gloo: bucket all-reduces between replays
     assert np.array_equal(a["bucket"], b["bucket"])
     mean = (a["solo"].astype(np.float64) + b["solo"]) / 2
     scale = float(np.abs(mean).max())
@@ -110,3 +112,66 @@ def test_two_rank_graph_step_is_ddp_mean():
     for i, k in enumerate(["training_loss", "effective_batch_size", "mean_active_constraints"]):
         exp = (float(a["sc"][i]) + float(b["sc"][i])) / 2
         assert abs(a["red"][k] - exp) <= 1e-6 * max(1.0, abs(exp)) and a["red"][k] == b["red"][k], k
+
+
+def _world1_main(port, q, comm):
+    """One rank on an RCCL ("nccl") group of size 1 with the collectives forced on: the captured
+    bucketed all-reduce (comm "graph") must give the same losses and parameters, bit for bit, as
+    the single-rank step with the maps refreshed after the optimizer (an all-reduce over one rank
+    and the 1/1 scale are exact)."""
+    import sys
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "fi-ode_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    try:
+        import bench
+        from fiode_amd.distributed import GradAllReducer
+        from fiode_amd.graph_step import GraphTrainStep
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        g = torch.Generator(device="cpu").manual_seed(5)
+        x = torch.rand(64, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (64,), generator=g).to(dev)
+        res = {}
+        for mode in ("ref", comm):
+            mod = bench.build_module(dev, seed=0, train_ode=True)
+            mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+            opt = mod.configure_optimizers(capturable=True)[0][0]
+            if mode == "ref":
+                gs = GraphTrainStep(mod, opt, x, y, warmup=2)
+            else:
+                red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
+                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True)
+                assert gs.comm == comm and len(red.buckets) >= 2
+            losses = [float(gs.step()) for _ in range(3)]
+            torch.cuda.synchronize()
+            res[mode] = (losses, [p.detach().cpu().clone() for p in mod.parameters()])
+        q.put((0, dict(ref=res["ref"], got=res[comm])))
+    except Exception:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((0, RuntimeError(traceback.format_exc())))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["graph", "eager"])
+def test_world1_rccl_bucketed_allreduce_equals_single(comm):
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_main, args=(_free_port(), q, comm))
+    p.start()
+    _, out = q.get(timeout=300)
+    p.join(timeout=60)
+    if isinstance(out, Exception):
+        raise out
+    (l0, p0), (l1, p1) = out["ref"], out["got"]
+    assert l0 == l1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
