@@ -85,7 +85,6 @@ struct LyapArgs {
   float* g_u;          // [B][M]
   float* gu_tiles;     // fused backward: per-(tile, image segment) partial g_u [ntiles][nseg][M] (else null)
   unsigned long long* prof;   // OT_PROFILE builds: per-phase wall-clock ticks summed over waves
-  double* xslabs;      // fused backward, XCD mode: [8][SLAB] per-XCD sums (L2 float64 atomics), else null
   int nseg;            // image segments per 32-row tile (images a tile's rows can span)
   // outputs
   float* scalars;
@@ -197,8 +196,6 @@ __global__ __launch_bounds__(128) void k_static_proj(LyapArgs a) {
 // Per-row preparation: sampler fan-out (h -> h_ws) and the dropout keep words of the 4 mask sets.
 __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a.xslabs)             // the per-XCD sums the backward adds into
-    for (int e = row; e < 8 * SLAB; e += gridDim.x * blockDim.x) a.xslabs[e] = 0.0;
   if (row >= a.N) return;
   if (a.offset_dev) {            // graph replay: the step counter lives in device memory
     const uint64_t o = (((uint64_t)a.rng.off_hi << 32) | a.rng.off_lo) + *a.offset_dev;
@@ -528,39 +525,13 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       LY_T(16);
     }
   }
-  // ---- this workgroup's partial: added into its XCD's float64 sum with L2 atomics (the XCD id
-  // from the hardware register, so every address of a per-XCD sum is touched by one L2 only;
-  // workgroup scope keeps the atomic in that L2: no HBM traffic but the final write-back of
-  // 8 x 154 KB).  The 32 float partials of an element add EXACTLY in float64 unless their
-  // exponents span more than ~29 binades, so the sum -- and the float gradient rounded from it --
-  // does not depend on the order the workgroups arrive in.  Or (FIODE_DETERMINISTIC=1) its own
-  // slab, summed by k_lyap_reduce in a fixed order.
+  // ---- this workgroup's partial: its own fp32 slab (plain stores), summed by k_lyap_reduce in a
+  // fixed order -- bit-reproducible.  (Round 2 added the partials into 8 per-XCD float64 sums with
+  // atomics instead; float atomics execute at the memory side, not in L2 (MI355X_MICROARCH.md,
+  // Global float atomics: ~1.3 TB/s of added bytes), so the 4.9 M adds cost ~20 us more per step
+  // than these 19.7 MB of slab stores and their reduce: k_lyap_bwd 103 -> 83 us.)
   db2 += shfl_xor32(db2);
   db3 += shfl_xor32(db3);
-  if (a.xslabs) {
-    const unsigned xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;     // hwreg(HW_REG_XCC_ID, 0, 4)
-    double* xs = a.xslabs + (size_t)xcd * SLAB;
-    auto add = [](double* p, float v) {
-      __hip_atomic_fetch_add(p, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) add(xs + SLAB_Q2 + (32 * w + acc_row(r, half)) * M + 32 * kb + col, dq2[kb][r]);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = acc_row(r, half);
-      if (i < C) add(xs + SLAB_Q3 + i * M + 32 * w + col, dq3[r]);
-      if (col < C) add(xs + SLAB_Q1 + (32 * w + i) * C + col, dq1[r]);
-    }
-    if (half == 0) {
-      add(xs + SLAB_B2 + 32 * w + col, db2);
-      if (w == 0 && col < C) add(xs + SLAB_B3 + col, db3);
-    }
-    LY_T(17);
-    LY_STAMP(64 + 2048, 1);
-    return;
-  }
   float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
@@ -644,20 +615,7 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
   const int nwg = a.nslab;
   const int n_el_blocks = (SLAB + RED_COLS - 1) / RED_COLS;
   const int n_gu_blocks = (a.B * M + RED_COLS - 1) / RED_COLS;
-  if ((int)blockIdx.x < n_el_blocks && a.xslabs) {     // the 8 per-XCD float64 sums, fixed order
-    const int e = blockIdx.x * RED_COLS + lane;
-    if (wv == 0 && e < SLAB) {
-      double d = 0.0;
-#pragma unroll
-      for (int x = 0; x < 8; ++x) d += a.xslabs[(size_t)x * SLAB + e];
-      const float t = (float)d;
-      if (e < SLAB_Q3) a.grads.Q2[e] = t;
-      else if (e < SLAB_Q1) a.grads.Q3[e - SLAB_Q3] = t;
-      else if (e < SLAB_B2) a.grads.Q1[e - SLAB_Q1] = t;
-      else if (e < SLAB_B1) a.grads.b2[e - SLAB_B2] = t;
-      else if (e >= SLAB_B3 && e < SLAB_B3 + C) a.grads.b3[e - SLAB_B3] = t;
-    }
-  } else if ((int)blockIdx.x < n_el_blocks) {
+  if ((int)blockIdx.x < n_el_blocks) {
     const int e = blockIdx.x * RED_COLS + lane;
     float s = 0.f;
     if (e < SLAB) {
@@ -754,16 +712,7 @@ __global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
 struct WsLayout {
   size_t conv, u, h, ft, kw, tsc, slabs, gut, gu, total;
   int nslab, nseg;
-  bool xcd;                 // per-XCD atomic sums instead of per-workgroup slabs
 };
-// FIODE_DETERMINISTIC=1: the fused backward writes one partial slab per workgroup and the reduce
-// sums them in a fixed float order (bit-reproducible by construction, ~39 MB more HBM traffic per
-// step); default: per-XCD float64 sums by L2 atomics (exact, hence order-free, unless an element's
-// partials span > ~29 binades).
-inline bool deterministic_grads() {
-  const char* e = getenv("FIODE_DETERMINISTIC");
-  return e && *e && *e != '0';
-}
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline void parts_for(int B, int S, int& parts, int& chunk) {
   parts = (256 + B - 1) / B;
@@ -786,7 +735,6 @@ inline WsLayout ws_layout(int B, int S) {
   const size_t ntiles = (N + 31) / 32;
   WsLayout L;
   L.nslab = bwd_grid(N);
-  L.xcd = !deterministic_grads();
   L.nseg = S >= 32 ? 2 : (31 / S + 2 > 32 ? 32 : 31 / S + 2);   // images one 32-row tile can span
   size_t o = 0;
   L.conv = o; o = al(o + 16);
@@ -795,7 +743,7 @@ inline WsLayout ws_layout(int B, int S) {
   L.ft = o; o = al(o + 2 * N * C * 4);
   L.kw = o; o = al(o + 4 * N * 16);
   L.tsc = o; o = al(o + ntiles * 16);
-  L.slabs = o; o = al(o + (size_t)(L.xcd ? 16 : L.nslab) * SLAB * 4);   // XCD mode: 8 float64 sums
+  L.slabs = o; o = al(o + (size_t)L.nslab * SLAB * 4);
   L.gut = o; o = al(o + ntiles * L.nseg * M * 4);
   L.gu = o; o = al(o + (size_t)B * M * 4);
 #ifdef OT_PROFILE
@@ -869,7 +817,6 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.tile_sc = reinterpret_cast<float*>(ws + L.tsc);
   a.slabs = reinterpret_cast<float*>(ws + L.slabs);
   a.nslab = L.nslab;
-  a.xslabs = L.xcd ? reinterpret_cast<double*>(a.slabs) : nullptr;
 #ifdef OT_PROFILE
   a.prof = reinterpret_cast<unsigned long long*>(ws + L.total - (64 + 4096) * 8);
 #endif

@@ -212,12 +212,9 @@ def test_barrier_projection_function_autograd():
     assert np.array_equal(nt.grad.cpu().numpy(), gn) and np.array_equal(lt.grad.cpu().numpy(), gl)
 
 
-def test_fused_backward_partial_modes(monkeypatch):
-    """The fused backward's weight-gradient partials: FIODE_DETERMINISTIC=1 (one slab per workgroup,
-    fixed-order float reduce) is bit-reproducible by construction; the default per-XCD float64
-    L2-atomic sums are exact for partials within ~29 binades of each other, so repeated runs agree
-    bit for bit too, and they agree with the float reduce to summation-order noise (1e-5 of each
-    gradient's max)."""
+def test_fused_backward_is_bit_reproducible():
+    """The fused backward's weight-gradient partials (one fp32 slab per workgroup, summed by
+    k_lyap_reduce in a fixed order) make repeated steps on the same inputs bit-identical."""
     dev = _dev()
     ops, L = _ops()
     P = make_params(seed=77)
@@ -226,17 +223,12 @@ def test_fused_backward_partial_modes(monkeypatch):
     x = torch.randn(B, 10, generator=g).to(dev)
     y = torch.randint(0, 10, (B,), generator=g).to(dev)
     dyn = ops.DynCfg(scale_nominal=True, dropout=0.5)
-    runs = {}
-    for mode, det in (("det_a", "1"), ("det_b", "1"), ("xcd", "0"), ("xcd_b", "0")):
-        monkeypatch.setenv("FIODE_DETERMINISTIC", det)
+    runs = []
+    for _ in range(3):
         sc, gr, _ = ops.lyap_step(x, y, _wt(P, dev), dyn, sample_size=S, n_uniform=204, seed=3, offset=1)
         torch.cuda.synchronize()
-        runs[mode] = (sc.clone(), {k: v.clone() for k, v in gr.items()})
-    for k in runs["det_a"][1]:
-        a, b, c = runs["det_a"][1][k], runs["det_b"][1][k], runs["xcd"][1][k]
-        assert torch.equal(a, b), k
-        assert torch.equal(c, runs["xcd_b"][1][k]), k
-        scale = float(a.abs().max()) + 1e-30
-        assert float((a - c).abs().max()) <= 1e-5 * scale, k
-    assert torch.equal(runs["det_a"][0], runs["det_b"][0])
-    torch.testing.assert_close(runs["det_a"][0], runs["xcd"][0], rtol=1e-6, atol=1e-7)
+        runs.append((sc.clone(), {k: v.clone() for k, v in gr.items()}))
+    for sc, gr in runs[1:]:
+        assert torch.equal(sc, runs[0][0])
+        for k in gr:
+            assert torch.equal(gr[k], runs[0][1][k]), k
