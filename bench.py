@@ -366,14 +366,5 @@ def main():
         dist.destroy_process_group()
 
 
-# The hipGraph executor of this ROCm runs a captured graph's parallel branches on a set of
-# internal streams; 3 of them measured fastest for this step (alternated runs, tools/probes/env_probe.sh:
-# 3: 2.23-2.24 ms, 2: 2.24-2.27, 4: 2.28-2.29, default: 2.32-2.37).  Read when HIP initialises, so
-# it is set here, before main() makes the first torch.cuda call, and only when bench.py runs as
-# the program (importing bench, as the tests do, changes nothing); an explicit setting in the
-# environment wins.  The value in effect is recorded in the JSON line ("runtime_env").
-GRAPH_QUEUES_DEFAULT = "3"
-
 if __name__ == "__main__":
-    os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", GRAPH_QUEUES_DEFAULT)
     main()

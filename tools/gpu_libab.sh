@@ -18,7 +18,7 @@ done
 for r in 1 2; do
   for L in tools/libfiode_ref.so "$@"; do
     n=$(basename $L .so)
-    FIODE_LIB=$PWD/$L DEBUG_HIP_FORCE_GRAPH_QUEUES=3 timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary > $O/bench_${n}_$r.json 2> $O/bench_${n}_$r.err || { echo bench $n failed; exit 1; }
+    FIODE_LIB=$PWD/$L timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary > $O/bench_${n}_$r.json 2> $O/bench_${n}_$r.err || { echo bench $n failed; exit 1; }
     python -c "import json; d=json.load(open('$O/bench_${n}_$r.json')); k=d['roofline']['per_kernel_ms']; print('$n', d['ms_per_step'], 'ot_fwd', k['k_ot_fwd'], 'ot_bwd', k['k_ot_bwd+wgrad'])"
   done
 done
