@@ -233,7 +233,10 @@ def main():
                 last["loss"] = loss
         else:
             from fiode_amd.graph_step import GraphTrainStep
-            gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world)
+            # comm: RCCL collectives captured in the step ("graph", the default over nccl) or eager
+            # between two replays ("eager"); FIODE_COMM overrides (e.g. a runtime that cannot capture)
+            gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world, comm=os.environ.get("FIODE_COMM"))
+            last["comm"] = gstep.comm if world > 1 else None
 
             def step():
                 last["loss"] = gstep.step()           # hipGraph replay (+ eager RCCL between graphs)
@@ -260,6 +263,7 @@ def main():
                   "loss_finite": bool(torch.isfinite(last["loss"]).all())}
         if health["status"] or not health["loss_finite"]:
             raise RuntimeError(f"unhealthy timed run: {health}")
+        health["comm"] = last.get("comm")
         return float(dt.item()), mod, x, y, health
 
     train_ode = args.workload == "rk4"

@@ -94,6 +94,29 @@ class GraphTrainStep:
         self.single = world == 1 and not self.force_comm
         if maps_ahead:
             self._maps_ahead_on()
+        self.comm_fallback = None
+        try:
+            self._capture()
+        except Exception as exc:                   # noqa: BLE001 - rethrown unless it is the comm capture
+            if self.comm != "graph":
+                raise
+            # the collectives could not be captured by this runtime: eager bucket all-reduces
+            # between two graphs instead (the reason is kept in comm_fallback)
+            if self.reducer is not None:
+                self.reducer._armed = None
+            self.comm, self.comm_fallback = "eager", repr(exc)
+            self._capture()
+        if self.reducer is not None and (world > 1 or self.force_comm):
+            views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
+                     + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
+            if not all(views):
+                raise RuntimeError("p.grad does not point into the reducer's bucket after capture")
+        self.scalars = module.last_plan["scalars"]
+        # a float lr is a launch argument baked into the captured optimizer step (a tensor lr is
+        # read on the device: LR schedulers may change it between replays)
+        self._float_lrs = [g["lr"] for g in self.opt.param_groups]
+
+    def _capture(self):
         self.one_graph = self.single or self.comm == "graph"
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
@@ -107,15 +130,6 @@ class GraphTrainStep:
             with torch.cuda.graph(self.g_opt):
                 self.opt.step()
                 self._refresh_late()
-        if self.reducer is not None and (world > 1 or self.force_comm):
-            views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
-                     + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
-            if not all(views):
-                raise RuntimeError("p.grad does not point into the reducer's bucket after capture")
-        self.scalars = module.last_plan["scalars"]
-        # a float lr is a launch argument baked into the captured optimizer step (a tensor lr is
-        # read on the device: LR schedulers may change it between replays)
-        self._float_lrs = [g["lr"] for g in self.opt.param_groups]
 
     # ---- conv maps computed ahead -------------------------------------------------------------
     # Each CayleyConv's spectral map depends only on its own two parameters, and the step's first
