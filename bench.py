@@ -51,7 +51,7 @@ FLOP_ROW = {"k_lyap_fwd": 2 * FLOP_ROW_FWD_PASS,                   # loss pass +
             "k_lyap_bwd": 2 * (128 * 128 + 128 * 10) + FLOP_ROW_FWD_PASS}
 
 
-def build_module(dev, seed=0, train_ode=False, solver="rk4"):
+def build_module(dev, seed=0, train_ode=False, solver="rk4", h_sample=H_SAMPLE):
     from fiode_amd.dynamics import OrthoClassDynProjectSimplexLips
     from fiode_amd.lyapunov import LyapunovLearning, UniformInitFun, DecisionBoundary
     from fiode_amd.models import make_ortho_KWLarge_Concat
@@ -66,7 +66,7 @@ def build_module(dev, seed=0, train_ode=False, solver="rk4"):
     sampler = CompositeSampler((10,), [UniformSimplexSampling(), CorrectConeSampling()])
     sched = CompositeSamplerScheduler([LinearScheduler(-0.02, 1.0, "min", 0.02, 10),
                                        LinearScheduler(0.02, 0.0, "max", 0.98, 10)], [1.0, 1.0])
-    mod = LyapunovLearning(order=1, h_sample_size=H_SAMPLE, h_dist_lim=15.0, sampler=sampler,
+    mod = LyapunovLearning(order=1, h_sample_size=h_sample, h_dist_lim=15.0, sampler=sampler,
                            sampler_scheduler=sched, dynamics=dyn, init_fun=UniformInitFun((10,), backbone),
                            lya_cand=DecisionBoundary(on_simplex=True), t_max=1.0, opt_name="Adam", lr=5e-3,
                            train_ode=train_ode, train_ode_epoch=TRAIN_ODE_EPOCH,

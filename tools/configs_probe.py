@@ -62,4 +62,29 @@ out["fanout_B1024_S1024"] = {"ms": round(ms, 3), "rows": B * S,
                              "tflops": round(148992 * B * S / (ms * 1e-3) / 1e12, 2),
                              "loss": float(sc[0]), "finite": bool(all(torch.isfinite(v).all() for v in g.values()))}
 print(out["fanout_B1024_S1024"], flush=True)
+# config 5 as a whole training step: B=1024 images x S=1024 samples per rank, train_ode with the
+# YAML's dopri5 (tol 1e-3), backbone + Cayley maps + Adam, hipGraph replay
+import bench  # noqa: E402
+from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
+B, S = 1024, 1024
+mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5", h_sample=S)
+opt = mod.configure_optimizers(capturable=True)[0][0]
+gx = torch.Generator(device="cpu").manual_seed(7)
+x = torch.rand(B, 3, 32, 32, generator=gx).to(dev)
+yb = torch.randint(0, 10, (B,), generator=gx).to(dev)
+gs = GraphTrainStep(mod, opt, x, yb, warmup=2)
+for _ in range(2):
+    gs.step()
+torch.cuda.synchronize()
+a, b = ev(), ev(); a.record()
+for _ in range(5):
+    loss = gs.step()
+b.record(); torch.cuda.synchronize()
+ms = a.elapsed_time(b) / 5
+st = mod.last_ode_plan["stats"].cpu().tolist()
+out["train_step_B1024_S1024_dopri5"] = {"ms": round(ms, 3), "images_per_s": round(B / (ms * 1e-3), 1),
+                                        "rows": B * S, "loss_finite": bool(torch.isfinite(loss)),
+                                        "train_ode": {"nfe": st[0], "n_accept": st[4], "n_reject": st[5],
+                                                      "status": st[3]}}
+print(out["train_step_B1024_S1024_dopri5"], flush=True)
 print(json.dumps(out))
