@@ -33,6 +33,12 @@
 namespace {
 using namespace fiode_tile;
 
+typedef float f32x4q __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4q mfma16q(float a, float b, f32x4q c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4q q4_zero() { return f32x4q{0.f, 0.f, 0.f, 0.f}; }
+
 // Phase timing (OT_PROFILE builds, tools/lyap_probe.py): lane 0 of every wave of workgroups 0..7
 // adds the wall-clock ticks (100 MHz) of each phase into prof[i] (a sample: all workgroups' atomics
 // on one word would time their own contention); LY_COUNT(i) counts the sampled waves.
@@ -326,9 +332,13 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   const int K1 = qp_exit_iter(a.conv[1], a.d.max_iter);
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
   const int ntiles = (a.N + 31) / 32;
-  f32x16 dq2[4], dq3 = f16_zero(), dq1 = f16_zero();
+  f32x16 dq2[4];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) dq2[kb] = f16_zero();
+  // dQ3 (10 x 32 block w) and dQ1 (32 x 10 block w) on 16x16x4 tiles: the 10 classes pad to 16,
+  // not 32 (lane l: j = l & 15, q = l >> 4; A[i = j][k = q], B[k = q][j], D[4q + r][j])
+  f32x4q dq3[2] = {q4_zero(), q4_zero()}, dq1[2] = {q4_zero(), q4_zero()};
+  const int j16 = lane & 15, q16 = lane >> 4;
   float db2 = 0.f, db3 = 0.f;
   for (int base = 4 * blockIdx.x; base < ntiles; base += 4 * gridDim.x) {
     // ---------------- phase A: wave w, tile base + w: the row math of the loss and logging passes
@@ -489,10 +499,18 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
         db2 += av;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) dq2[kb] = mfma32(av, st.a1[n][32 * kb + col], dq2[kb]);
-        const float fv = col < C ? st.gf[t][n][col] : 0.f;
+      }
+#pragma unroll 2
+      for (int s = 0; s < 8; ++s) {
+        const int n = 4 * s + q16;
+        const float fv = j16 < C ? st.gf[t][n][j16] : 0.f;
+        const float hv = j16 < C ? st.hh[t][n][j16] : 0.f;
         if (w == 0) db3 += fv;
-        dq3 = mfma32(fv, st.a2[n][32 * w + col], dq3);
-        dq1 = mfma32(st.g1[n][32 * w + col], col < C ? st.hh[t][n][col] : 0.f, dq1);
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          dq3[hb] = mfma16q(fv, st.a2[n][32 * w + 16 * hb + j16], dq3[hb]);
+          dq1[hb] = mfma16q(st.g1[n][32 * w + 16 * hb + j16], hv, dq1[hb]);
+        }
       }
       LY_T(14);
       // this tile's per-image partial of g_u: rows in order, one segment per image (threads 0..127)
@@ -531,6 +549,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   // Global float atomics: ~1.3 TB/s of added bytes), so the 4.9 M adds cost ~20 us more per step
   // than these 19.7 MB of slab stores and their reduce: k_lyap_bwd 103 -> 83 us.)
   db2 += shfl_xor32(db2);
+  db3 += __shfl_xor(db3, 16, 64);
   db3 += shfl_xor32(db3);
   float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
 #pragma unroll
@@ -538,11 +557,13 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) slab[SLAB_Q2 + (32 * w + acc_row(r, half)) * M + 32 * kb + col] = dq2[kb][r];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = acc_row(r, half);
-    if (i < C) slab[SLAB_Q3 + i * M + 32 * w + col] = dq3[r];
-    if (col < C) slab[SLAB_Q1 + (32 * w + i) * C + col] = dq1[r];
-  }
+  for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * q16 + r;
+      if (i < C) slab[SLAB_Q3 + i * M + 32 * w + 16 * hb + j16] = dq3[hb][r];
+      if (j16 < C) slab[SLAB_Q1 + (32 * w + 16 * hb + i) * C + j16] = dq1[hb][r];
+    }
   if (half == 0) {
     slab[SLAB_B2 + 32 * w + col] = db2;
     if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
