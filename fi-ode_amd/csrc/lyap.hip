@@ -290,6 +290,7 @@ struct BwdStage {
   float g1[32][LDQ];    // gz1[n][i]
   float gf[4][32][12];  // gft[n][c] of the round's 4 tiles (phase A)
   float hh[4][32][12];  // h[n][c]
+  uint32_t kw[4][32][8];  // keep words of both dropout layers (phase A loads them behind its QP work)
 };
 constexpr size_t BWD_LDS = (size_t)(M + C) * LDQ * sizeof(float) + sizeof(BwdStage);
 
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
 #pragma unroll
       for (int j = 0; j < C; ++j) gft[j] = 0.f;
       load_row10(hsrc + (size_t)rr * C, h);
+      const uint4 kwa = a.kw[rr], kwb = a.kw[(size_t)a.N + rr];
       if (tile < ntiles) {
         const int label = (int)a.y[rr / a.S];
         float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
@@ -413,6 +415,8 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
           st.gf[w][col][c] = gft[c];
           st.hh[w][col][c] = valid ? h[c] : 0.f;
         }
+        *reinterpret_cast<uint4*>(&st.kw[w][col][0]) = kwa;
+        *reinterpret_cast<uint4*>(&st.kw[w][col][4]) = kwb;
       }
     }
     __syncthreads();
@@ -425,18 +429,17 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       const int row = tile * 32 + col;
       const int rr = row < a.N ? row : a.N - 1;
       const int b = rr / a.S;
-      float h[C];
-      load_row10(hsrc + (size_t)rr * C, h);
-      const uint4 k1 = a.kw[rr], k2 = a.kw[(size_t)a.N + rr];
+      // h and the keep words from phase A's LDS copy (rows past N: h = 0; their gradients are 0)
+      const uint4 k1 = *reinterpret_cast<const uint4*>(&st.kw[t][col][0]);
       const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w};
-      const uint32_t kw2w = w == 0 ? k2.x : (w == 1 ? k2.y : (w == 2 ? k2.z : k2.w));
+      const uint32_t kw2w = st.kw[t][col][4 + w];
       // layer 1 (all units): z1 = u[b] + Q1 h, dropout-ReLU
       f32x16 z1[4];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)b * M, mb, half, z1[mb]);
 #pragma unroll
       for (int s = 0; s < 5; ++s) {
-        const float bs = half ? h[2 * s + 1] : h[2 * s];
+        const float bs = st.hh[t][col][2 * s + half];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) z1[mb] = mfma32(q1[mb][s], bs, z1[mb]);
       }
@@ -568,6 +571,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
     slab[SLAB_B2 + 32 * w + col] = db2;
     if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
   }
+  LY_STAMP(64 + 2048, 1);
 }
 
 // Weight gradients.  Workgroup (image b, part p) reduces rows [b*S + p*chunk, ...) of that image.

@@ -82,6 +82,7 @@ class SpectralConfig(ct.Structure):
 
 
 ABI_VERSION = 2            # FIODE_ABI_VERSION (include/fiode.h)
+FIODE_ODETRAIN_NSAVED = 12  # entries fiode_odetrain_saved_offsets writes
 
 
 class AdamConfig(ct.Structure):

@@ -323,7 +323,7 @@ def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, 
 def odetrain_saved(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> Dict[str, torch.Tensor]:
     """Views of the forward's saved arrays in an odetrain workspace (for checkers)."""
     B, E = int(cfg.batch), odetrain_evals(cfg)
-    off = (ct.c_int64 * 12)()
+    off = (ct.c_int64 * L.FIODE_ODETRAIN_NSAVED)()
     L.check(L.lib().fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)),
             "fiode_odetrain_saved_offsets")
     f = lambda i, n: ws[off[i]:off[i] + 4 * n].view(torch.float32)

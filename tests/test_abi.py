@@ -32,6 +32,10 @@ def test_host_only_entry_points():
     from fiode_amd import _lib
     lib = _lib.lib()
     assert lib.fiode_abi_version() == _lib.ABI_VERSION == 2
+    hdr = (pathlib.Path(__file__).resolve().parents[1] / "include" / "fiode.h").read_text()
+    for name in ("FIODE_ABI_VERSION", "FIODE_ODETRAIN_NSAVED"):
+        val = int(re.search(r"#define %s (\d+)" % name, hdr).group(1))
+        assert val == getattr(_lib, name.replace("FIODE_ABI_", "ABI_")), name
     assert lib.fiode_error_string(2).decode().startswith("unsupported shape")
     cfg = _lib.LyapConfig(128, 256, 204, 1, 2, 2.0, 0, 0)
     dyn = _lib.DynConfig(10, 128, 10, 100.0, 20.0, 0.02, 1, 0.5, 30, 1e-4)
@@ -179,7 +183,7 @@ def test_odetrain_dopri5_shape_on_host():
     rk = ops.odetrain_config(128, 0.0, 1.0, 0.1, _lib.FIODE_DROPOUT_PHILOX)
     assert lib.fiode_odetrain_evals(ct.byref(rk)) == 40
     assert lib.fiode_odetrain_workspace_bytes(ct.byref(cfg)) > lib.fiode_odetrain_workspace_bytes(ct.byref(rk))
-    off = (ct.c_int64 * 12)()
+    off = (ct.c_int64 * _lib.FIODE_ODETRAIN_NSAVED)()
     assert lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)) == 0
     assert all(off[i] > 0 for i in (9, 10, 11))
     assert lib.fiode_odetrain_saved_offsets(ct.byref(rk), ct.cast(off, ct.c_void_p)) == 0

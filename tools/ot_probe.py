@@ -20,7 +20,7 @@ for B, sn in ((128, False), (128, True), (1024, False)):
     off = ct.c_int64 * 8
     # prof array sits after the exchange granules
     lib = L.lib()
-    offs = (ct.c_int64 * 9)()
+    offs = (ct.c_int64 * L.FIODE_ODETRAIN_NSAVED)()
     # xslots offset = gft offset + al(R*C*4)
     lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
     al = lambda v: (v + 255) & ~255

@@ -47,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         E = ops.odetrain_evals(cfg)
         nt = (B + 15) // 16
-        offs = (ct.c_int64 * 9)()
+        offs = (ct.c_int64 * L.FIODE_ODETRAIN_NSAVED)()
         lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
         xs = offs[7] + ((B * E * 10 * 4 + 255) & ~255)
         slots = ws[xs: xs + E * 2 * nt * 8].view(torch.int64).cpu().numpy().astype(np.uint64).reshape(E, 2, nt)

@@ -43,6 +43,9 @@ for name, base, nwg in (("k_lyap_fwd", 64, 512), ("k_lyap_bwd", 64 + 2048, 256))
     print(f"{name}: span {st[:, 1].max() - t0:.1f} us; workgroup start offsets (us) p50 {np.median(st[:, 0] - t0):.1f} "
           f"max {(st[:, 0] - t0).max():.1f}; durations p10/p50/p90/max {np.percentile(dur, 10):.1f} / "
           f"{np.median(dur):.1f} / {np.percentile(dur, 90):.1f} / {dur.max():.1f}")
+    slow = np.argsort(dur)[::-1][:6]
+    print(f"  slowest workgroups (id: start offset, duration us): "
+          + ", ".join(f"{i}: {st[i, 0] - t0:.1f}, {dur[i]:.1f}" for i in slow))
 fw, bw = max(int(prof[6]), 1), max(int(prof[18]), 1)
 us = lambda i, n: prof[i] / n * 0.01
 print(f"k_lyap_fwd ({fw} waves), us per wave: weights {us(0, fw):.2f}  row loads {us(1, fw):.2f}  "
