@@ -21,6 +21,7 @@
 #include "common.h"
 #include "tile.h"
 #include "tile16.h"
+#include "tile4.h"
 #include "wgrad.h"
 #include "dopri5.h"
 #include "../../include/fiode.h"
@@ -28,6 +29,7 @@
 namespace {
 using namespace fiode_tile;
 using namespace fiode_t16;
+using namespace fiode_t4;
 using namespace fiode_dp;
 
 
@@ -309,6 +311,166 @@ __global__ __launch_bounds__(256) void k_ot_fwd(OTArgs a) {
     for (int i = 0; i < C; ++i) y[i] = __builtin_nanf("");
   }
   if (p == 0 && valid && q == 0) store_row10(a.y_out + (size_t)b * C, y);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.stats[0] = 4 * (a.niters - 1);
+    a.stats[1] = a.niters - 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward on 4-row tiles (tile4.h) for B <= 4 * FIODE_OT4_MAX_TILES: the same solve, the same
+// exchanges and saved arrays as k_ot_fwd; per eval every wave issues the 4x4x1 MFMAs of its
+// quarter of the hidden units for 4 samples (77 MFMAs of 8 cycles) instead of the 16x16x4
+// products of 16 samples (78 of 32 cycles), on 4x as many workgroups.  The MLP's sums run in
+// another order than the 16-row kernel's (both within float32 rounding of the oracle's).
+constexpr int FIODE_OT4_MAX_TILES = 256;     // one persistent workgroup per CU at most
+constexpr int OT4_XSTRIDE = 16;              // u64 words per exit granule: one 128-byte line per tile
+struct OtShared4 {
+  Mlp4Shared mlp;
+  float mu_rec[4][64][33];    // [wave][lane][bisection iteration] (padded): every lane its own
+  int K;
+  int Kprev;
+  int dead;
+  int pad;
+};
+
+__device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, int p, int b, bool valid, int lane,
+                         int j, const f32x4& uacc, uint32_t kw1p, uint32_t kw2p, const float (&h)[C], float (&k)[C]) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + e;
+  const bool writer = p == 0 && valid && lane < TR4;     // lane j of wave 0 stores sample j's rows
+#ifdef OT_PROFILE
+  uint64_t t_prev = wall_clock64();
+#endif
+  if (writer) store_row10(a.hs + r * C, h);
+  float lower[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) lower[i] = -a.d.alpha_1 * (expf(a.d.sigma_1 * h[i]) - 1.0f);
+  mlp4_part(w, uacc, h, kw1p, kw2p, a.drop_scale, p, lane, valid ? a.a1 + r * M : nullptr,
+            valid ? a.a2 + r * M : nullptr, sh.mlp);
+  OT_MARK(1);
+  __syncthreads();
+  float ft[C];
+  ft4_sum(sh.mlp, j, ft);
+  float nominal[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    const float upper = a.d.alpha_2 * (1.0f - h[i]);
+    const float span = upper - lower[i];
+    if (a.d.scale_nominal) {
+      const float sig = 1.0f / (1.0f + expf(-ft[i]));
+      nominal[i] = span * sig + lower[i];
+    } else {
+      nominal[i] = ft[i];
+    }
+  }
+  OT_MARK(5);
+  float* rec = &sh.mu_rec[p][lane][0];
+  qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
+            a.xslots + (size_t)e * 2 * gridDim.x * OT4_XSTRIDE, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
+            a.drop_block,
+#ifdef OT_PROFILE
+            a.prof,
+#else
+            nullptr,
+#endif
+            OT4_XSTRIDE);
+  OT_MARK(3);
+  const int K = sh.K;
+  const float mu = sh.mu_rec[p][lane][K];
+#pragma unroll
+  for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);
+  if (writer) {
+    store_row10(a.ftw + r * C, ft);
+    store_row10(a.nomw + r * C, nominal);
+    store_row10(a.loww + r * C, lower);
+    store_row10(a.vw + r * C, k);
+    a.muw[r] = mu;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.stats[2] = K;
+#ifdef OT_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0 && e < 96) a.prof[16 + e] = (unsigned long long)K;
+#endif
+  if (threadIdx.x == 0) sh.Kprev = K;
+  __syncthreads();            // zpart / a1s / mu_rec / K reused by the next eval
+  OT_MARK(4);
+}
+
+__global__ __launch_bounds__(256) void k_ot_fwd4(OTArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  OtShared4& sh = *reinterpret_cast<OtShared4*>(smem);
+  if (threadIdx.x == 0) {
+    sh.Kprev = a.d.max_iter - 1;
+    sh.dead = 0;
+  }
+  const int lane = threadIdx.x & 63, j = lane & 3;
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x * TR4 + j;
+  const bool valid = b < a.B;
+  const int bb = valid ? b : a.B - 1;
+  T4W w;                      // this wave's weight operands, in registers for the whole solve
+  load_t4w(a.Q1, a.Q2, a.Q3, a.b2, a.b3, p, lane, w);
+  // u[b] = U_x x_b + bx + b1 for this tile's rows
+  for (int t = threadIdx.x; t < TR4 * M; t += blockDim.x) {
+    const int rb = blockIdx.x * TR4 + t / M, i = t % M;
+    if (rb < a.B) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < FIODE_X; ++c) s = __fmaf_rn(a.Qx[i * FIODE_X + c], a.x_feat[(size_t)rb * FIODE_X + c], s);
+      a.u[(size_t)rb * M + i] = (s + a.bx[i]) + a.b1[i];
+    }
+  }
+  __syncthreads();
+  const f32x4 uacc = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 32 * p + 4 * ((lane >> 2) & 7));
+  // this part's keep words of eval e (k_ot_masks), prefetched one eval ahead
+  const uint32_t* kwp = a.kw;
+  auto fetch = [&](int e, uint32_t& w1, uint32_t& w2) {
+    if (a.dropout_mode == FIODE_DROPOUT_OFF) {
+      w1 = w2 = 0xFFFFFFFFu;
+      return;
+    }
+    w1 = kwp[(((size_t)e * 2 + 0) * a.B + bb) * 4 + p];
+    w2 = kwp[(((size_t)e * 2 + 1) * a.B + bb) * 4 + p];
+  };
+  uint32_t kc1, kc2, kn1 = 0u, kn2 = 0u;
+  fetch(0, kc1, kc2);
+  float y[C], k1[C], k2[C], k3[C], k4[C], hin[C];
+  load_row10(a.h0 + (size_t)bb * C, y);
+  const float third = 1.0f / 3.0f;
+  const int eN = 4 * (a.niters - 1);
+  for (int it = 0; it + 1 < a.niters; ++it) {
+    float ta, dt;
+    step_times(a, it, ta, dt);
+    const int e0 = 4 * it;
+#define OT4_STAGE(E_, H_, K_)                                                            \
+    {                                                                                    \
+      if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                      \
+      ot_eval4(a, w, sh, (E_), p, b, valid, lane, j, uacc, kc1, kc2, H_, K_);           \
+      kc1 = kn1;                                                                         \
+      kc2 = kn2;                                                                         \
+    }
+    OT4_STAGE(e0, y, k1)
+#pragma unroll
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + (dt * k1[i]) * third;
+    OT4_STAGE(e0 + 1, hin, k2)
+#pragma unroll
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + dt * (k2[i] - k1[i] * third);
+    OT4_STAGE(e0 + 2, hin, k3)
+#pragma unroll
+    for (int i = 0; i < C; ++i) hin[i] = y[i] + dt * ((k1[i] - k2[i]) + k3[i]);
+    OT4_STAGE(e0 + 3, hin, k4)
+#undef OT4_STAGE
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const float dy = (((k1[i] + 3.0f * (k2[i] + k3[i])) + k4[i]) * dt) * 0.125f;
+      y[i] = y[i] + dy;
+    }
+  }
+  if (sh.dead) {              // this tile's QP exits came from a partial AND: make the loss NaN
+#pragma unroll
+    for (int i = 0; i < C; ++i) y[i] = __builtin_nanf("");
+  }
+  if (p == 0 && valid && lane < TR4) store_row10(a.y_out + (size_t)b * C, y);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.stats[0] = 4 * (a.niters - 1);
     a.stats[1] = a.niters - 1;
@@ -1292,8 +1454,8 @@ OtLayout ot_layout(int B, int E, int A = 0) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  const size_t nt = (size_t)(B + TR - 1) / TR;
-  L.xs = o; o += (size_t)E * 2 * nt * 8 + 1024;     // the reduction granules follow: one clear for both
+  const size_t nt = (size_t)(B + TR - 1) / TR, nt4 = (size_t)(B + TR4 - 1) / TR4;   // 16- / 4-row tiles
+  L.xs = o; o += (size_t)E * 2 * nt4 * 8 * OT4_XSTRIDE + 1024;     // the reduction granules follow: one clear for both
   L.xr = o; o += al(A > 0 ? 2 * nt * 2 * OT_XV * 8 : 0);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
@@ -1354,7 +1516,7 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.meta = reinterpret_cast<double*>(ws + L.meta);
   a.imeta = reinterpret_cast<int32_t*>(ws + L.imeta);
 #ifdef OT_PROFILE
-  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + TR - 1) / TR) + 8;
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + TR4 - 1) / TR4) * OT4_XSTRIDE + 8;
 #endif
   return FIODE_OK;
 }
@@ -1420,6 +1582,9 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   FIODE_HIP_CHECK(hipGetLastError());
   if (a.method == FIODE_ODE_DOPRI5) {
     hipLaunchKernelGGL(k_odp_fwd, dim3(ntiles), dim3(256), sizeof(OdpShared), st, a);
+  } else if ((a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES) {
+    // 4-row tiles (tile4.h T4W: weights in registers)
+    hipLaunchKernelGGL(k_ot_fwd4, dim3((a.B + TR4 - 1) / TR4), dim3(256), sizeof(OtShared4), st, a);
   } else {
     // the weights live in registers (tile16.h T16W)
     hipLaunchKernelGGL(k_ot_fwd, dim3(ntiles), dim3(256), sizeof(OtShared), st, a);

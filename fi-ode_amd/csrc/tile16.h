@@ -96,12 +96,13 @@ __device__ __forceinline__ void publish_mask(unsigned long long* slot, unsigned 
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...).
+// one wave: AND of the masks of all tiles for this epoch (lane i reads tiles i, i+64, ...); tile t's
+// granule at slots[t * stride] (stride 16: one 128-byte line per tile, no two publishers on a line).
 // Bounded: after ~0.5 s without every tag (a tile not resident) it records status 4, sets the
 // workgroup's sticky `dead` flag (LDS) -- later exchanges of this workgroup then stop waiting at
 // once -- and returns the partial AND; the caller poisons its outputs (see k_ot_fwd).
 __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int ntiles, unsigned epoch,
-                                                 int32_t* status, int lane, int& dead) {
+                                                 int32_t* status, int lane, int& dead, int stride = 1) {
   uint32_t acc = 0xFFFFFFFFu;
   for (int base = 0; base < ntiles; base += 64) {
     const int t = base + lane;
@@ -110,7 +111,7 @@ __device__ __forceinline__ uint32_t gather_masks(unsigned long long* slots, int 
       bool ok = true;
       unsigned long long x = 0;
       if (t < ntiles) {
-        x = __hip_atomic_load((gu64_t*)(slots + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x = __hip_atomic_load((gu64_t*)(slots + (size_t)t * stride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = (unsigned)(x >> 32) == epoch;
       }
       if (__all(ok)) {
@@ -329,7 +330,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
                                          int kprev, bool valid, int p, int q, int lane, float* mu_rec_row,
                                          unsigned long long* slots, unsigned epoch, int32_t* status, int& shK,
                                          int& dead, int drop_block = -1,
-                                         unsigned long long* prof = nullptr) {
+                                         unsigned long long* prof = nullptr, int stride = 1) {
   const int last = max_iter - 1;
   const int kspec = min(last, kprev + FIODE_KSPEC_MARGIN);
   float lo, hi;
@@ -343,8 +344,9 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   if (p == 0) {
     // drop_block (test hook, FIODE_DEBUG_DROP_PUBLISH): that workgroup never publishes epoch 1,
     // as if it were not resident -- exercises the timeout path
-    if (lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block)) publish_mask(slots + blockIdx.x, epoch, conv);
-    const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane, dead);
+    if (lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block))
+      publish_mask(slots + (size_t)blockIdx.x * stride, epoch, conv);
+    const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane, dead, stride);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
     if (lane == 0) shK = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
@@ -357,8 +359,9 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   if (shK < 0) {                        // block-uniform: every tile saw the same masks
     conv |= qp_bisect_seq(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, true, valid);
     if (p == 0) {
-      if (lane == 0) publish_mask(slots + ntiles + blockIdx.x, epoch, conv);
-      const uint32_t all = gather_masks(slots + ntiles, ntiles, epoch, status, lane, dead);
+      unsigned long long* s2 = slots + (size_t)ntiles * stride;
+      if (lane == 0) publish_mask(s2 + (size_t)blockIdx.x * stride, epoch, conv);
+      const uint32_t all = gather_masks(s2, ntiles, epoch, status, lane, dead, stride);
       if (lane == 0) shK = qp_exit_iter(all, max_iter);
     }
     __syncthreads();

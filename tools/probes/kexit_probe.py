@@ -46,11 +46,12 @@ def main():
         y, st, ws = ops.odetrain_forward(feat, h0, w, dyn, cfg)
         torch.cuda.synchronize()
         E = ops.odetrain_evals(cfg)
-        nt = (B + 15) // 16
+        nt = (B + 3) // 4 if B <= 1024 else (B + 15) // 16   # k_ot_fwd4 tiles (k_ot_fwd beyond)
         offs = (ct.c_int64 * L.FIODE_ODETRAIN_NSAVED)()
         lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
         xs = offs[7] + ((B * E * 10 * 4 + 255) & ~255)
-        slots = ws[xs: xs + E * 2 * nt * 8].view(torch.int64).cpu().numpy().astype(np.uint64).reshape(E, 2, nt)
+        xst = 16 if B <= 1024 else 1    # granule stride of k_ot_fwd4 (one line per tile)
+        slots = ws[xs: xs + E * 2 * nt * xst * 8].view(torch.int64).cpu().numpy().astype(np.uint64).reshape(E, 2, nt, xst)[..., 0]
         kprev = dyn.qp_max_iter - 1
         for e in range(E):
             m0 = (slots[e, 0] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
