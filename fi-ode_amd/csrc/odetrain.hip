@@ -524,8 +524,8 @@ struct VjpW {
 struct VjpRow {
   float nominal[C], sig[C], span[C], es[C];     // es = exp(sigma_1 h)
 };
-template <bool SN>
-__device__ __forceinline__ void vjp_row_math(const OTArgs& a, const VjpIn& in, VjpRow& rw) {
+template <bool SN, class In>
+__device__ __forceinline__ void vjp_row_math(const OTArgs& a, const In& in, VjpRow& rw) {
   // the expressions of barrier_nominal (common.h), branch-free for a compile-time scale_nominal
 #pragma unroll
   for (int i = 0; i < C; ++i) {
@@ -749,6 +749,227 @@ __global__ __launch_bounds__(256) void k_ot_bwd(OTArgs a) {
     for (int i = 0; i < C; ++i) gy[i] = acc[i] + gY[i];
   }
 #undef OT_VJP
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward on 4-row tiles (the rk4 solve for B <= 4 * FIODE_OT4_MAX_TILES): the VJPs of k_ot_bwd
+// with the MFMA products of tile4.h -- wave p owns hidden units 32p .. 32p + 31:
+//   g_z2 = (Q3^T g_ft) [a2 > 0] / (1 - p): K = 10 in two halves (5 steps), halves by permlane32;
+//   g_a1 = Q2^T g_z2 (K = 128 from LDS, halves, 4 accumulators), g_z1 = g_a1 [a1 > 0] / (1 - p);
+//   g_h partial = Q1^T g_z1 over the wave's 32 units (quarters, permlane16 / permlane32);
+// the 4 parts of g_h meet in LDS (double-buffered, one barrier per VJP besides the g_z2 one).
+struct OtBwdShared4 {
+  float gz2s[TR4][M + 4];     // g_z2 of all units [sample][unit] (B operands of Q2^T)
+  float gz1s[TR4][M + 4];     // g_z1 [sample][unit] (each wave reads back its own units)
+  float gpart[2][4][16][4];   // [buffer][part][lane 4 blk + j][reg]: g_h partial of outputs 4 blk + reg
+};
+
+struct VjpIn4 {
+  float h[C], ft[C], v[C], mu;
+  f32x4 a2, a1;               // saved post-activations of units 32p + 4 blk + r (this lane's block)
+};
+
+__device__ __forceinline__ void load_vjp_in4(const OTArgs& a, int p, int e, int b, bool valid, int lane, VjpIn4& in) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + (e < 0 ? 0 : e);
+  load_row10(a.hs + r * C, in.h);
+  load_row10(a.ftw + r * C, in.ft);
+  load_row10(a.vw + r * C, in.v);
+  in.mu = a.muw[r];
+  const int u0 = 32 * p + 4 * ((lane >> 2) & 7);
+  in.a2 = *reinterpret_cast<const f32x4*>(a.a2 + r * M + u0);
+  in.a1 = *reinterpret_cast<const f32x4*>(a.a1 + r * M + u0);
+}
+
+// transposed weight operands of wave p (registers for the whole kernel), i = lane & 3, b = lane >> 2:
+//   q3t[s] = Q3[s + 5 (b >> 3)][32p + 4 (b & 7) + i]         (g_z2, s = 0..4)
+//   q2t[s] = Q2[s + 64 (b >> 3)][32p + 4 (b & 7) + i]        (g_a1, s = 0..63)
+//   q1t[s] = Q1[32p + 8 (b >> 2) + s][4 (b & 3) + i]  (0 for classes >= C; g_h, s = 0..7)
+struct VjpW4 {
+  float q3t[5];
+  float q2t[64];
+  float q1t[8];
+};
+
+template <bool SN>
+__device__ void ot_vjp4(const OTArgs& a, const VjpW4& wv, OtBwdShared4& sh, int buf, int p, int e, int b, bool valid,
+                        int lane, int j, const VjpIn4& in, const VjpRow& rw, const float (&g)[C], float (&gy_out)[C]) {
+  const int bb = valid ? b : a.B - 1;
+  const size_t r = (size_t)bb * a.E + e;
+  const int blk4 = lane >> 2, hi = blk4 >> 3, blk = blk4 & 7;
+#ifdef OT_PROFILE
+  uint64_t t_prev = wall_clock64();
+#endif
+  float g_nom[C], g_low[C], gft[C], ghb[C];
+  float gin[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) gin[i] = valid ? g[i] : 0.f;
+  qp_backward_row(gin, in.v, in.mu, rw.nominal, g_nom, g_low);
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    float g_lo = g_low[i], g_up = 0.f;
+    if constexpr (SN) {
+      gft[i] = ((g_nom[i] * rw.span[i]) * (1.0f - rw.sig[i])) * rw.sig[i];
+      const float g_span = g_nom[i] * rw.sig[i];
+      g_lo = (g_lo + g_nom[i]) - g_span;
+      g_up = g_span;
+    } else {
+      gft[i] = g_nom[i];
+    }
+    ghb[i] = ((g_lo * -a.d.alpha_1) * rw.es[i]) * a.d.sigma_1 + g_up * -a.d.alpha_2;
+  }
+  if (p == 0 && valid && lane < TR4) {
+    store_row10(a.gft + r * C, gft);
+    if (a.dbg_gft) store_row10(a.dbg_gft + r * C, gft);
+  }
+  OT_MARK(10);
+  // g_z2 of units 32p + 4 blk + r
+  f32x4v gz = zero4();
+#pragma unroll
+  for (int s = 0; s < 5; ++s) gz = mfma4(wv.q3t[s], hi ? gft[s + 5] : gft[s], gz);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float v = gz[t] + swap32(gz[t]);
+    gz[t] = in.a2[t] > 0.f ? v * a.drop_scale : 0.f;
+  }
+  if (blk4 < 8) {
+    const f32x4 v = f32x4{gz[0], gz[1], gz[2], gz[3]};
+    *reinterpret_cast<f32x4*>(&sh.gz2s[j][32 * p + 4 * blk]) = v;
+    if (valid) *reinterpret_cast<f32x4*>(a.gz2 + r * M + 32 * p + 4 * blk) = v;
+  }
+  __syncthreads();
+  OT_MARK(11);
+  // g_a1 = Q2^T g_z2 of units 32p + 4 blk + r: K half hi, 4 accumulators
+  f32x4v acc[4] = {zero4(), zero4(), zero4(), zero4()};
+  const float* gzr = &sh.gz2s[j][64 * hi];
+#pragma unroll
+  for (int s = 0; s < 64; s += 4) {
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(gzr + s);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = mfma4(wv.q2t[s + t], bv[t], acc[t]);
+  }
+  f32x4v gb;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float part = (acc[0][t] + acc[1][t]) + (acc[2][t] + acc[3][t]);
+    const float other = swap32(part);
+    const float v = hi ? (other + part) : (part + other);
+    gb[t] = in.a1[t] > 0.f ? v * a.drop_scale : 0.f;
+  }
+  if (blk4 < 8) {
+    const f32x4 v = f32x4{gb[0], gb[1], gb[2], gb[3]};
+    *reinterpret_cast<f32x4*>(&sh.gz1s[j][32 * p + 4 * blk]) = v;       // read back by this wave only
+    if (valid) *reinterpret_cast<f32x4*>(a.gz1 + r * M + 32 * p + 4 * blk) = v;
+  }
+  OT_MARK(12);
+  // g_h partial over the wave's units: outputs 4 (b & 3) + t, units 32p + 8 (b >> 2) + s
+  f32x4v gha = zero4(), ghc = zero4();
+  const float* g1 = &sh.gz1s[j][32 * p + 8 * (blk4 >> 2)];
+  const f32x4 v0 = *reinterpret_cast<const f32x4*>(g1), v1 = *reinterpret_cast<const f32x4*>(g1 + 4);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    gha = mfma4(wv.q1t[t], v0[t], gha);
+    ghc = mfma4(wv.q1t[4 + t], v1[t], ghc);
+  }
+  f32x4v gh;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float x = gha[t] + ghc[t];
+    const float y = x + swap16(x);
+    gh[t] = y + swap32(y);
+  }
+  if (blk4 < 4) *reinterpret_cast<f32x4*>(&sh.gpart[buf][p][lane][0]) = f32x4{gh[0], gh[1], gh[2], gh[3]};
+  OT_MARK(13);
+  __syncthreads();
+  OT_MARK(14);
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    const int ln = 4 * (i >> 2) + j, rg = i & 3;
+    const float ghm = ((sh.gpart[buf][0][ln][rg] + sh.gpart[buf][1][ln][rg]) + sh.gpart[buf][2][ln][rg]) +
+                      sh.gpart[buf][3][ln][rg];
+    gy_out[i] = ghm + ghb[i];
+  }
+  OT_MARK(15);
+}
+
+template <bool SN>
+__global__ __launch_bounds__(256) void k_ot_bwd4(OTArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  OtBwdShared4& sh = *reinterpret_cast<OtBwdShared4*>(smem);
+  const int lane = threadIdx.x & 63, j = lane & 3;
+  const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  VjpW4 wv;
+  {
+    const int bq = lane >> 2, i = lane & 3;
+    const int u = 32 * p + 4 * (bq & 7) + i;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) wv.q3t[s] = a.Q3[(s + 5 * (bq >> 3)) * M + u];
+#pragma unroll
+    for (int s = 0; s < 64; ++s) wv.q2t[s] = a.Q2[(size_t)(s + 64 * (bq >> 3)) * M + u];
+    const int c = 4 * (bq & 3) + i;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wv.q1t[s] = c < C ? a.Q1[(32 * p + 8 * (bq >> 2) + s) * C + c] : 0.f;
+  }
+  const int b = blockIdx.x * TR4 + j;
+  const bool valid = b < a.B;
+  float gy[C];
+  if (valid) load_row10(a.g_y + (size_t)b * C, gy);
+  else
+#pragma unroll
+    for (int i = 0; i < C; ++i) gy[i] = 0.f;
+  const float third = 1.0f / 3.0f;
+  int buf = 0;
+  VjpIn4 cur, nxt;
+  VjpRow crw;
+  load_vjp_in4(a, p, a.E - 1, b, valid, lane, cur);
+#define OT_VJP4(E_, G_)                                                                 \
+  load_vjp_in4(a, p, (E_) - 1, b, valid, lane, nxt);                                    \
+  vjp_row_math<SN>(a, cur, crw);                                                        \
+  ot_vjp4<SN>(a, wv, sh, buf, p, (E_), b, valid, lane, j, cur, crw, G_, gY);          \
+  cur = nxt;                                                                            \
+  buf ^= 1;
+  for (int it = a.niters - 2; it >= 0; --it) {
+    float ta, dt;
+    step_times(a, it, ta, dt);
+    const float c8 = dt * 0.125f, c38 = 3.0f * c8;
+    float gk1[C], gk2[C], gk3[C], gk4[C], acc[C], gY[C];
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      acc[i] = gy[i];
+      gk1[i] = gy[i] * c8;
+      gk2[i] = gy[i] * c38;
+      gk3[i] = gy[i] * c38;
+      gk4[i] = gy[i] * c8;
+    }
+    const int e0 = 4 * it;
+    OT_VJP4(e0 + 3, gk4)
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      const float d = dt * gY[i];
+      gk1[i] += d;
+      gk2[i] -= d;
+      gk3[i] += d;
+    }
+    OT_VJP4(e0 + 2, gk3)
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      const float d = dt * gY[i];
+      gk2[i] += d;
+      gk1[i] -= d * third;
+    }
+    OT_VJP4(e0 + 1, gk2)
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      acc[i] += gY[i];
+      gk1[i] += (dt * gY[i]) * third;
+    }
+    OT_VJP4(e0, gk1)
+#pragma unroll
+    for (int i = 0; i < C; ++i) gy[i] = acc[i] + gY[i];
+  }
+#undef OT_VJP4
 }
 
 // =============================================================================================
@@ -1527,6 +1748,10 @@ hipError_t launch_sweep(const OTArgs& a, hipStream_t st) {
   if (a.method == FIODE_ODE_DOPRI5) {
     if (a.d.scale_nominal) hipLaunchKernelGGL(k_odp_bwd<true>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
     else hipLaunchKernelGGL(k_odp_bwd<false>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
+  } else if ((a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES) {
+    const dim3 grid4((a.B + TR4 - 1) / TR4);
+    if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd4<true>, grid4, dim3(256), sizeof(OtBwdShared4), st, a);
+    else hipLaunchKernelGGL(k_ot_bwd4<false>, grid4, dim3(256), sizeof(OtBwdShared4), st, a);
   } else {
     if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd<true>, grid, dim3(256), sizeof(OtBwdShared), st, a);
     else hipLaunchKernelGGL(k_ot_bwd<false>, grid, dim3(256), sizeof(OtBwdShared), st, a);

@@ -54,12 +54,14 @@ def pmc(path: pathlib.Path, counter: str, pass_dir: str = None):
 # v_mfma_f32_32x32x2_f32 = 64 cycles, v_mfma_f32_16x16x4_f32 = 32 cycles (MI355X_MICROARCH.md).
 #   k_lyap_fwd   (20 + 256 + 64) MFMA32 per 32-row tile per pass x 2 passes x 1,024 tiles
 #   k_lyap_bwd   fused: per tile and wave 20 (layer 1) + 64 (layer-2 block) + 5 (Q3^T) + 64 (Q2^T block)
-#                + 96 (its quarter of dQ2 / dQ3 / dQ1) = 249 MFMA32 x 4 waves x 1,024 tiles
+#                + 64 (its quarter of dQ2) = 217 MFMA32, + 16 MFMA16 (dQ3 / dQ1, round 3) x 4 waves x 1,024 tiles
+#   k_ot_fwd4    (4-row tiles, round 3) 77 v_mfma_f32_4x4x1_16b_f32 (8 cycles) per wave per eval x 4 waves
+#                x 32 tiles x 40 evals
 #   k_lyap_wgrad (the train_ode solve's weight gradients, N = B x 40 evals) 6 MFMA32 per wave per row pair x 4 waves x N / 2
 #   k_ot_fwd     96 MFMA16 per wave per eval x 4 waves x 8 tiles x 40 evals (k_ot_bwd the same)
 EXPECTED_MFMA_SIMD_CYCLES = {
-    "k_lyap_fwd": 340 * 2 * 1024 * 64, "k_lyap_bwd": 249 * 4 * 1024 * 64, "k_lyap_wgrad": 24 * 2560 * 64,
-    "k_ot_fwd": 96 * 4 * 8 * 40 * 32, "k_ot_bwd": 96 * 4 * 8 * 40 * 32}
+    "k_lyap_fwd": 340 * 2 * 1024 * 64, "k_lyap_bwd": (217 * 64 + 16 * 32) * 4 * 1024, "k_lyap_wgrad": 24 * 2560 * 64,
+    "k_ot_fwd": 96 * 4 * 8 * 40 * 32, "k_ot_fwd4": 77 * 4 * 32 * 40 * 8, "k_ot_bwd": 96 * 4 * 8 * 40 * 32}
 N_CU, N_SIMD, N_XCD = 256, 4, 8
 
 
