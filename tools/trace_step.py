@@ -21,7 +21,7 @@ for r in rows[1:]:
     end = max(end, r["e"])
 bursts.append(cur)
 rows = max(bursts, key=len)
-ot = [i for i, r in enumerate(rows) if r["n"] == "k_ot_fwd"]
+ot = [i for i, r in enumerate(rows) if r["n"].startswith("k_ot_fwd")]
 steps = []
 for a, b in zip(ot, ot[1:]):
     seg = rows[a:b]
