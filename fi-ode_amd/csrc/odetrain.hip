@@ -18,6 +18,7 @@
 //   gradients (Q3^T, Q2^T via LDS images, Q1^T via a zero-padded LDS image), writing the per-
 //   (row, eval) activation gradients gft / gz2 / gz1.
 // Weight gradients: the training step's wgrad chain over rows r = b*E + e (wgrad.h).
+#include <type_traits>
 #include "common.h"
 #include "tile.h"
 #include "tile16.h"
@@ -1071,32 +1072,38 @@ __device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& 
   __syncthreads();
 }
 
+template <bool T4>
 struct OdpShared {
-  OtShared ot;
-  float kst[4][7][TR][C];      // [wave][stage][row][c]: the current attempt's k_0..k_6
+  std::conditional_t<T4, OtShared4, OtShared> ot;
+  float kst[4][7][T4 ? TR4 : TR][C];      // [wave][stage][row][c]: the current attempt's k_0..k_6
   double red[OT_XV];
 };
 
 __device__ __forceinline__ double rms_of(double sumsq, double n) { return sqrt(sumsq / n); }
 
+// T4: 4-row tiles (tile4.h MLP, ot_eval4) for B <= 4 * FIODE_OT4_MAX_TILES, else 16-row tiles
+template <bool T4>
 __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  OdpShared& S = *reinterpret_cast<OdpShared*>(smem);
-  OtShared& sh = S.ot;
+  constexpr int TRX = T4 ? TR4 : TR;
+  OdpShared<T4>& S = *reinterpret_cast<OdpShared<T4>*>(smem);
+  auto& sh = S.ot;
   if (threadIdx.x == 0) {
     sh.Kprev = a.d.max_iter - 1;
     sh.dead = 0;
   }
-  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & (TRX - 1);
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b = blockIdx.x * TR + j;
+  const int b = blockIdx.x * TRX + j;
   const bool valid = b < a.B;
-  const bool own = valid && q == 0;            // lanes whose row values count in the batch sums
+  const bool first = T4 ? lane < TR4 : q == 0;   // one lane per row (wave 0's are the row writers)
+  const bool own = valid && first;             // lanes whose row values count in the batch sums
   const int bb = valid ? b : a.B - 1;
-  T16W w;
-  load_t16w(a.Q1, a.Q2, M, a.Q3, M, a.b2, a.b3, p, q, j, w);
-  for (int t = threadIdx.x; t < TR * M; t += blockDim.x) {
-    const int rb = blockIdx.x * TR + t / M, i = t % M;
+  std::conditional_t<T4, T4W, T16W> w;
+  if constexpr (T4) load_t4w(a.Q1, a.Q2, a.Q3, a.b2, a.b3, p, lane, w);
+  else load_t16w(a.Q1, a.Q2, M, a.Q3, M, a.b2, a.b3, p, q, j, w);
+  for (int t = threadIdx.x; t < TRX * M; t += blockDim.x) {
+    const int rb = blockIdx.x * TRX + t / M, i = t % M;
     if (rb < a.B) {
       float s = 0.f;
 #pragma unroll
@@ -1105,13 +1112,19 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
     }
   }
   __syncthreads();
-  f32x4v uacc[8];
+  std::conditional_t<T4, f32x4, f32x4v[8]> uacc;
+  if constexpr (T4) {
+    uacc = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 32 * p + 4 * ((lane >> 2) & 7));
+  } else {
 #pragma unroll
-  for (int hb = 0; hb < 8; ++hb) {
-    const f32x4 uv = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 16 * hb + 4 * q);
-    uacc[hb] = f32x4v{uv[0], uv[1], uv[2], uv[3]};
+    for (int hb = 0; hb < 8; ++hb) {
+      const f32x4 uv = *reinterpret_cast<const f32x4*>(a.u + (size_t)bb * M + 16 * hb + 4 * q);
+      uacc[hb] = f32x4v{uv[0], uv[1], uv[2], uv[3]};
+    }
   }
-  const uint4* kwp = reinterpret_cast<const uint4*>(a.kw);
+  // keep words of eval e: all 4 words of layer 1 and the part's layer-2 word (16-row), or the
+  // part's word of each layer (4-row)
+  const uint32_t* kwp = a.kw;
   auto fetch = [&](int e, uint32_t (&w1)[4], uint32_t& w2) {
     if (a.dropout_mode == FIODE_DROPOUT_OFF) {
 #pragma unroll
@@ -1119,11 +1132,11 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       w2 = 0xFFFFFFFFu;
       return;
     }
-    const uint4 q1 = kwp[((size_t)e * 2 + 0) * a.B + bb];
+    const uint4 q1 = reinterpret_cast<const uint4*>(kwp)[((size_t)e * 2 + 0) * a.B + bb];
     w1[0] = q1.x; w1[1] = q1.y; w1[2] = q1.z; w1[3] = q1.w;
-    w2 = reinterpret_cast<const uint32_t*>(kwp + ((size_t)e * 2 + 1) * a.B + bb)[p];
+    w2 = kwp[(((size_t)e * 2 + 1) * a.B + bb) * 4 + p];
   };
-  float (*ks)[TR][C] = S.kst[p];
+  float (*ks)[TRX][C] = S.kst[p];
   // every lane of the row writes the same values into its wave's copy, so no lane reads another's
   auto kput = [&](int s, const float (&v)[C]) {
 #pragma unroll
@@ -1139,7 +1152,8 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
   auto eval = [&](const float (&h)[C], float (&k)[C]) {
     uint32_t kn1[4] = {0u, 0u, 0u, 0u}, kn2 = 0u;
     if (e + 1 < a.E) fetch(e + 1, kn1, kn2);
-    ot_eval(a, w, sh, e, p, b, valid, lane, q, j, uacc, kc1, kc2, h, k);
+    if constexpr (T4) ot_eval4(a, w, sh, e, p, b, valid, lane, j, uacc, kc1[p], kc2, h, k);
+    else ot_eval(a, w, sh, e, p, b, valid, lane, q, j, uacc, kc1, kc2, h, k);
 #pragma unroll
     for (int t = 0; t < 4; ++t) kc1[t] = kn1[t];
     kc2 = kn2;
@@ -1208,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       break;
     }
     const float dt32 = (float)dt;
-    if (p == 0 && q == 0 && valid) store_row10(a.ys + ((size_t)n * a.B + b) * C, y);
+    if (p == 0 && first && valid) store_row10(a.ys + ((size_t)n * a.B + b) * C, y);
     if (lead) {
       double* lg = a.alog + (size_t)n * ALOG_W;
       lg[ALOG_T] = tcur; lg[ALOG_DT] = dt; lg[ALOG_FIDX] = fidx; lg[ALOG_E0] = e;
@@ -1322,7 +1336,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
 #pragma unroll
     for (int c = 0; c < C; ++c) out[c] = __builtin_nanf("");   // failed solve: the loss turns NaN
   }
-  if (p == 0 && valid && q == 0) store_row10(a.y_out + (size_t)b * C, out);
+  if (p == 0 && valid && first) store_row10(a.y_out + (size_t)b * C, out);
   if (lead) {
     a.stats[0] = e;
     a.stats[1] = nacc;
@@ -1337,43 +1351,57 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
 }
 
 // ---- backward: the reverse sweep of oracle/dopri5_train.py dopri5_adjoint ---------------------
+template <bool T4>
 struct OdpBwdShared {
-  OtBwdShared ot;
-  float gk[4][7][TR][C];       // [wave][stage][row][c]: adjoints of the attempt's k_0..k_6
+  std::conditional_t<T4, OtBwdShared4, OtBwdShared> ot;
+  float gk[4][7][T4 ? TR4 : TR][C];       // [wave][stage][row][c]: adjoints of the attempt's k_0..k_6
   double red[OT_XV];
   int dead;
 };
 
-template <bool SN>
+template <bool SN, bool T4>
 __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  OdpBwdShared& S = *reinterpret_cast<OdpBwdShared*>(smem);
+  constexpr int TRX = T4 ? TR4 : TR;
+  OdpBwdShared<T4>& S = *reinterpret_cast<OdpBwdShared<T4>*>(smem);
   if (threadIdx.x == 0) S.dead = 0;
-  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & (TRX - 1);
   const int p = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  VjpW wv;
+  std::conditional_t<T4, VjpW4, VjpW> wv;
+  float q3t[8][3];                    // 16-row only (VjpW4 holds its own Q3^T operands)
+  if constexpr (T4) {
+    const int bq = lane >> 2, i = lane & 3;
+    const int u = 32 * p + 4 * (bq & 7) + i;
 #pragma unroll
-  for (int o = 0; o < 2; ++o) {
+    for (int s = 0; s < 5; ++s) wv.q3t[s] = a.Q3[(s + 5 * (bq >> 3)) * M + u];
+#pragma unroll
+    for (int s = 0; s < 64; ++s) wv.q2t[s] = a.Q2[(size_t)(s + 64 * (bq >> 3)) * M + u];
+    const int c = 4 * (bq & 3) + i;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wv.q1t[s] = c < C ? a.Q1[(32 * p + 8 * (bq >> 2) + s) * C + c] : 0.f;
+  } else {
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+#pragma unroll
+      for (int hb = 0; hb < 8; ++hb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wv.q2t[o][hb][t] = a.Q2[(16 * hb + 4 * q + t) * M + 16 * (2 * p + o) + j];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wv.q1t[o][t] = j < C ? a.Q1[(16 * (2 * p + o) + 4 * q + t) * C + j] : 0.f;
+    }
 #pragma unroll
     for (int hb = 0; hb < 8; ++hb)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) wv.q2t[o][hb][t] = a.Q2[(16 * hb + 4 * q + t) * M + 16 * (2 * p + o) + j];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) wv.q1t[o][t] = j < C ? a.Q1[(16 * (2 * p + o) + 4 * q + t) * C + j] : 0.f;
+      for (int s = 0; s < 3; ++s) q3t[hb][s] = 4 * s + q < C ? a.Q3[(4 * s + q) * M + 16 * hb + j] : 0.f;
   }
-  float q3t[8][3];
-#pragma unroll
-  for (int hb = 0; hb < 8; ++hb)
-#pragma unroll
-    for (int s = 0; s < 3; ++s) q3t[hb][s] = 4 * s + q < C ? a.Q3[(4 * s + q) * M + 16 * hb + j] : 0.f;
-  const int b = blockIdx.x * TR + j;
+  const int b = blockIdx.x * TRX + j;
   const bool valid = b < a.B;
-  const bool own = valid && q == 0;
+  const bool own = valid && (T4 ? lane < TR4 : q == 0);
   const int bb = valid ? b : a.B - 1;
   const int nfe = a.imeta[0], A = a.imeta[1];
   const bool failed = a.imeta[2] != 0 || A < 1;
   __syncthreads();
-  float (*gks)[TR][C] = S.gk[p];
+  float (*gks)[TRX][C] = S.gk[p];
   auto gadd = [&](int s, const float (&v)[C]) {
 #pragma unroll
     for (int c = 0; c < C; ++c) gks[s][j][c] += v[c];
@@ -1395,17 +1423,25 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   const float rtol = (float)a.rtol, atol = (float)a.atol;
   unsigned rep = 1;
   int buf = 0;
-  VjpIn cur, nxt;
+  std::conditional_t<T4, VjpIn4, VjpIn> cur, nxt;
   VjpRow crw, nrw;
   int ecur = nfe - 1;
-  load_vjp_in(a, p, ecur, b, valid, q, cur);
+  if constexpr (T4) load_vjp_in4(a, p, ecur, b, valid, lane, cur);
+  else load_vjp_in(a, p, ecur, b, valid, q, cur);
   vjp_row_math<SN>(a, cur, crw);
   // evals visited nfe-1, nfe-2, ..., 0 (attempts in reverse, stages 5..0; then evals 1, 0)
   auto vjp = [&](const float (&g)[C], float (&gY)[C]) {
-    load_vjp_in(a, p, ecur - 1, b, valid, q, nxt);
-    ot_vjp<SN>(a, wv, q3t, S.ot, buf, p, ecur, b, valid, lane, q, j, cur, crw, nxt, nrw, g, gY);
-    cur = nxt;
-    crw = nrw;
+    if constexpr (T4) {
+      load_vjp_in4(a, p, ecur - 1, b, valid, lane, nxt);
+      ot_vjp4<SN>(a, wv, S.ot, buf, p, ecur, b, valid, lane, j, cur, crw, g, gY);
+      cur = nxt;
+      vjp_row_math<SN>(a, cur, crw);
+    } else {
+      load_vjp_in(a, p, ecur - 1, b, valid, q, nxt);
+      ot_vjp<SN>(a, wv, q3t, S.ot, buf, p, ecur, b, valid, lane, q, j, cur, crw, nxt, nrw, g, gY);
+      cur = nxt;
+      crw = nrw;
+    }
     buf ^= 1;
     --ecur;
   };
@@ -1677,7 +1713,7 @@ OtLayout ot_layout(int B, int E, int A = 0) {
   L.gft = o; o += al(R * C * 4);
   const size_t nt = (size_t)(B + TR - 1) / TR, nt4 = (size_t)(B + TR4 - 1) / TR4;   // 16- / 4-row tiles
   L.xs = o; o += (size_t)E * 2 * nt4 * 8 * OT4_XSTRIDE + 1024;     // the reduction granules follow: one clear for both
-  L.xr = o; o += al(A > 0 ? 2 * nt * 2 * OT_XV * 8 : 0);
+  L.xr = o; o += al(A > 0 ? 2 * nt4 * 2 * OT_XV * 8 : 0);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
   L.ys = o; o += al((size_t)A * B * C * 4);
@@ -1745,11 +1781,17 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
 // the adjoint sweep (weight operands in registers: VjpW): rk4 k_ot_bwd, dopri5 k_odp_bwd
 hipError_t launch_sweep(const OTArgs& a, hipStream_t st) {
   const dim3 grid((a.B + TR - 1) / TR);
+  const bool t4 = (a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES;
+  const dim3 grid4((a.B + TR4 - 1) / TR4);
   if (a.method == FIODE_ODE_DOPRI5) {
-    if (a.d.scale_nominal) hipLaunchKernelGGL(k_odp_bwd<true>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
-    else hipLaunchKernelGGL(k_odp_bwd<false>, grid, dim3(256), sizeof(OdpBwdShared), st, a);
-  } else if ((a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES) {
-    const dim3 grid4((a.B + TR4 - 1) / TR4);
+    if (t4) {
+      if (a.d.scale_nominal) hipLaunchKernelGGL((k_odp_bwd<true, true>), grid4, dim3(256), sizeof(OdpBwdShared<true>), st, a);
+      else hipLaunchKernelGGL((k_odp_bwd<false, true>), grid4, dim3(256), sizeof(OdpBwdShared<true>), st, a);
+    } else {
+      if (a.d.scale_nominal) hipLaunchKernelGGL((k_odp_bwd<true, false>), grid, dim3(256), sizeof(OdpBwdShared<false>), st, a);
+      else hipLaunchKernelGGL((k_odp_bwd<false, false>), grid, dim3(256), sizeof(OdpBwdShared<false>), st, a);
+    }
+  } else if (t4) {
     if (a.d.scale_nominal) hipLaunchKernelGGL(k_ot_bwd4<true>, grid4, dim3(256), sizeof(OtBwdShared4), st, a);
     else hipLaunchKernelGGL(k_ot_bwd4<false>, grid4, dim3(256), sizeof(OtBwdShared4), st, a);
   } else {
@@ -1806,7 +1848,10 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if (a.method == FIODE_ODE_DOPRI5) {
-    hipLaunchKernelGGL(k_odp_fwd, dim3(ntiles), dim3(256), sizeof(OdpShared), st, a);
+    if ((a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES)
+      hipLaunchKernelGGL(k_odp_fwd<true>, dim3((a.B + TR4 - 1) / TR4), dim3(256), sizeof(OdpShared<true>), st, a);
+    else
+      hipLaunchKernelGGL(k_odp_fwd<false>, dim3(ntiles), dim3(256), sizeof(OdpShared<false>), st, a);
   } else if ((a.B + TR4 - 1) / TR4 <= FIODE_OT4_MAX_TILES) {
     // 4-row tiles (tile4.h T4W: weights in registers)
     hipLaunchKernelGGL(k_ot_fwd4, dim3((a.B + TR4 - 1) / TR4), dim3(256), sizeof(OtShared4), st, a);

@@ -3,8 +3,10 @@ train_ode_solver dopri5, train_ode_tol 1e-3; pl_modules.py:490-500, models.py:23
 backprop, use_adjoint False at pl_modules.py:303) -- fiode_odetrain_forward / _backward with
 method FIODE_ODE_DOPRI5.
 
-* dropout off: the forward takes the eval solve's (fiode_odeint dopri5) steps and reaches its
-  y(t1) bit for bit (same MLP / QP kernels, same controller);
+* dropout off: the forward takes the eval solve's (fiode_odeint dopri5) steps -- same NFE, accept /
+  reject sequence -- and reaches its y(t1) bit for bit on 16-row tiles (B > 1,024: the same MLP / QP
+  kernels), within 1e-4 on 4-row tiles (B <= 1,024: the MLP sums in another order, which moves
+  each QP solution within its bisection resolution);
 * train mode (given dropout masks): every eval's stage input and the output agree with the float64
   restatement oracle/dopri5_train.py run at the device's linearisation points (QP active sets, exit
   mu and accept decisions pinned) -- same NFE and accept / reject sequence;
@@ -44,7 +46,7 @@ def _setup(B, seed, tol, p=0.5, A=64):
     return ops, dev, P, x, h0, cfg, masks, w
 
 
-@pytest.mark.parametrize("B,seed,sn", [(64, 1, False), (128, 2, True)])
+@pytest.mark.parametrize("B,seed,sn", [(64, 1, False), (128, 2, True), (1040, 3, False)])
 def test_dropout_off_equals_eval_solve(B, seed, sn):
     ops, dev, P, x, h0, cfg, _, w = _setup(B, seed, 1e-3, p=0.0)
     dyn = ops.DynCfg(scale_nominal=sn, dropout=0.0)
@@ -56,7 +58,10 @@ def test_dropout_off_equals_eval_solve(B, seed, sn):
     s, e = st.cpu().numpy(), est.cpu().numpy()
     assert s[3] == 0 and e[3] == 0, (s, e)
     assert (s[0], s[4], s[5]) == (e[0], e[1], e[2]), (s, e)
-    assert torch.equal(y, sol[-1])
+    if B > 1024:              # 16-row tiles: the eval solve's MLP and QP kernels
+        assert torch.equal(y, sol[-1])
+    else:                     # 4-row tiles (tile4.h): the same solve, MLP sums in another order
+        assert float((y - sol[-1]).abs().max()) <= 1e-4     # QP bisection resolution (tol 1e-4)
 
 
 def _pins(ops, ws, cfg, st, B):
