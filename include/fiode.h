@@ -213,7 +213,9 @@ FIODE_API size_t fiode_odetrain_workspace_bytes(const fiode_odetrain_config* cfg
 /* y_out [B][C] = y(t1); stats (device int32[8]): nfe, accepted steps, last QP exit iteration, status
  * (0 ok, 2 attempt capacity exhausted, 3 dt underflow, 4 a cross-workgroup exchange timed out), and
  * for dopri5 n_accept, n_reject, attempts.  offset_dev: optional device addend of the Philox offset
- * (graph replay). */
+ * (graph replay).  The forward is one persistent workgroup per tile whose workgroups exchange the
+ * batch-global QP exits, so all of them must be resident at once: 4-row tiles up to B = 1,024
+ * (ceil(B / 4) workgroups), 16-row tiles beyond (ceil(B / 16), B <= FIODE_ODE_MAX_BATCH). */
 FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* cfg, const fiode_dyn_config* dyn,
                                      const fiode_dyn_weights* w, const float* x_feat, const float* h0,
                                      const uint8_t* masks, const uint64_t* offset_dev, float* y_out,
