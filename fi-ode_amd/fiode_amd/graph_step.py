@@ -118,8 +118,11 @@ class GraphTrainStep:
 
     def _capture(self):
         self.one_graph = self.single or self.comm == "graph"
+        # capture_error_mode "thread_local": the process group's watchdog thread polls its events
+        # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it
+        # ("operation not permitted when stream is capturing" -> the watchdog terminates the process)
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
+        with torch.cuda.graph(self.g_fb, capture_error_mode="thread_local"):
             self.loss = self._fwd_bwd()
             if self.one_graph:
                 self.opt.step()
@@ -127,7 +130,7 @@ class GraphTrainStep:
         self.g_opt = None
         if not self.one_graph:
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt):
+            with torch.cuda.graph(self.g_opt, capture_error_mode="thread_local"):
                 self.opt.step()
                 self._refresh_late()
 

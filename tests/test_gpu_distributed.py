@@ -167,7 +167,15 @@ def test_world1_rccl_bucketed_allreduce_equals_single(comm):
     q = ctx.Queue()
     p = ctx.Process(target=_world1_main, args=(_free_port(), q, comm))
     p.start()
-    _, out = q.get(timeout=300)
+    import queue
+    out = None
+    for _ in range(100):                   # a child that dies (e.g. aborted by a runtime error) fails fast
+        try:
+            _, out = q.get(timeout=1.0)
+            break
+        except queue.Empty:
+            assert p.is_alive() or not q.empty(), f"RCCL child exited with code {p.exitcode}"
+    assert out is not None, "RCCL child produced no result in 100 s"
     p.join(timeout=60)
     if isinstance(out, Exception):
         raise out
