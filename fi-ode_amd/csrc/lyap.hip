@@ -341,7 +341,17 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   f32x4q dq3[2] = {q4_zero(), q4_zero()}, dq1[2] = {q4_zero(), q4_zero()};
   const int j16 = lane & 15, q16 = lane >> 4;
   float db2 = 0.f, db3 = 0.f;
+  // u[b] rows of the layer-1 accumulators, loaded one tile ahead (the global-load latency of the
+  // first tile hides behind phase A, of tile t + 1 behind tile t's MFMA work)
+  f32x16 un[4];
+  auto load_u = [&](int tile) {
+    const int row = tile * 32 + col;
+    const int b = (row < a.N ? row : a.N - 1) / a.S;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)b * M, mb, half, un[mb]);
+  };
   for (int base = 4 * blockIdx.x; base < ntiles; base += 4 * gridDim.x) {
+    load_u(base);
     // ---------------- phase A: wave w, tile base + w: the row math of the loss and logging passes
     {
       const int tile = base + w;
@@ -426,17 +436,13 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
     for (int t = 0; t < 4; ++t) {
       const int tile = base + t;
       if (tile >= ntiles) break;                   // block-uniform
-      const int row = tile * 32 + col;
-      const int rr = row < a.N ? row : a.N - 1;
-      const int b = rr / a.S;
       // h and the keep words from phase A's LDS copy (rows past N: h = 0; their gradients are 0)
       const uint4 k1 = *reinterpret_cast<const uint4*>(&st.kw[t][col][0]);
       const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w};
       const uint32_t kw2w = st.kw[t][col][4 + w];
       // layer 1 (all units): z1 = u[b] + Q1 h, dropout-ReLU
-      f32x16 z1[4];
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) load_acc_rows(a.u + (size_t)b * M, mb, half, z1[mb]);
+      f32x16 z1[4] = {un[0], un[1], un[2], un[3]};
+      if (t + 1 < 4 && tile + 1 < ntiles) load_u(tile + 1);
 #pragma unroll
       for (int s = 0; s < 5; ++s) {
         const float bs = st.hh[t][col][2 * s + half];
@@ -456,14 +462,21 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) z2[4 * g + e] = b2w[g][e];
+      // the LDS operands of step kk + 1 are read before the MFMAs of step kk (software pipeline: the
+      // compiler otherwise waits on every read right before its MFMA -- one wave per SIMD, nothing
+      // else hides the ~100-cycle LDS latency)
+      {
+        const float* q2row = Q2s + (32 * w + col) * LDQ + 4 * half;
+        f32x4 q = *reinterpret_cast<const f32x4*>(q2row);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+        for (int kk = 0; kk < 16; ++kk) {                // kk = 4 kb + g
+          const f32x4 qn = kk + 1 < 16 ? *reinterpret_cast<const f32x4*>(q2row + 32 * ((kk + 1) >> 2) + 8 * ((kk + 1) & 3))
+                                       : q;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(Q2s + (32 * w + col) * LDQ + 32 * kb + 8 * g + 4 * half);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) z2 = mfma32(q[e], z1[kb][4 * g + e], z2);
+          for (int e = 0; e < 4; ++e) z2 = mfma32(q[e], z1[kk >> 2][4 * (kk & 3) + e], z2);
+          q = qn;
         }
+      }
       dropout_relu(z2, kw2w, half, a.drop_scale);
       // g_a2^T block w = Q3^T g_ft^T ; g_z2 = g_a2 [a2 > 0] * scale
       f32x16 ga = f16_zero();
@@ -479,15 +492,28 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       LY_T(11);
       // g_a1^T block w = Q2^T g_z2^T: A = Q2[32kb + 8g + 4half + e][32w + col], B = g_z2[n = col][32kb + 8g + 4half + e]
       f32x16 gb = f16_zero();
+      {
+        auto ld = [&](int kk, float (&qa)[4], f32x4& gz) {   // kk = 4 kb + g
+          const int k0 = 32 * (kk >> 2) + 8 * (kk & 3) + 4 * half;
+          gz = *reinterpret_cast<const f32x4*>(&st.g2[col][k0]);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+          for (int e = 0; e < 4; ++e) qa[e] = Q2s[(k0 + e) * LDQ + 32 * w + col];
+        };
+        float qa[4];
+        f32x4 gz;
+        ld(0, qa, gz);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 gz = *reinterpret_cast<const f32x4*>(&st.g2[col][32 * kb + 8 * g + 4 * half]);
+        for (int kk = 0; kk < 16; ++kk) {
+          float qn[4] = {0.f, 0.f, 0.f, 0.f};
+          f32x4 gn = gz;
+          if (kk + 1 < 16) ld(kk + 1, qn, gn);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            gb = mfma32(Q2s[(32 * kb + 8 * g + 4 * half + e) * LDQ + 32 * w + col], gz[e], gb);
+          for (int e = 0; e < 4; ++e) gb = mfma32(qa[e], gz[e], gb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) qa[e] = qn[e];
+          gz = gn;
         }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) gb[r] = z1w[r] > 0.f ? gb[r] * a.drop_scale : 0.f;
       store_acc_rows(&st.g1[col][0], w, half, gb);
@@ -495,24 +521,54 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       __syncthreads();
       LY_T(13);
       // weight gradients of this tile: wave w's quarter
-#pragma unroll 4
-      for (int s = 0; s < 16; ++s) {
-        const int n = 2 * s + half;
-        const float av = st.g2[n][32 * w + col];
-        db2 += av;
+      {
+        float av = st.g2[half][32 * w + col], bv[4];
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) dq2[kb] = mfma32(av, st.a1[n][32 * kb + col], dq2[kb]);
+        for (int kb = 0; kb < 4; ++kb) bv[kb] = st.a1[half][32 * kb + col];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int n1 = 2 * (s + 1) + half;
+          float avn = av, bvn[4] = {bv[0], bv[1], bv[2], bv[3]};
+          if (s + 1 < 16) {
+            avn = st.g2[n1][32 * w + col];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) bvn[kb] = st.a1[n1][32 * kb + col];
+          }
+          db2 += av;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) dq2[kb] = mfma32(av, bv[kb], dq2[kb]);
+          av = avn;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) bv[kb] = bvn[kb];
+        }
       }
-#pragma unroll 2
-      for (int s = 0; s < 8; ++s) {
-        const int n = 4 * s + q16;
-        const float fv = j16 < C ? st.gf[t][n][j16] : 0.f;
-        const float hv = j16 < C ? st.hh[t][n][j16] : 0.f;
-        if (w == 0) db3 += fv;
+      {
+        // operands of step s + 1 read ahead of step s's MFMAs (as above)
+        float o[6], on[6];
+        auto ld = [&](int s, float (&v)[6]) {
+          const int n = 4 * s + q16;
+          v[0] = j16 < C ? st.gf[t][n][j16] : 0.f;
+          v[1] = j16 < C ? st.hh[t][n][j16] : 0.f;
 #pragma unroll
-        for (int hb = 0; hb < 2; ++hb) {
-          dq3[hb] = mfma16q(fv, st.a2[n][32 * w + 16 * hb + j16], dq3[hb]);
-          dq1[hb] = mfma16q(st.g1[n][32 * w + 16 * hb + j16], hv, dq1[hb]);
+          for (int hb = 0; hb < 2; ++hb) {
+            v[2 + hb] = st.a2[n][32 * w + 16 * hb + j16];
+            v[4 + hb] = st.g1[n][32 * w + 16 * hb + j16];
+          }
+        };
+        ld(0, o);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+          for (int e = 0; e < 6; ++e) on[e] = o[e];
+          if (s + 1 < 8) ld(s + 1, on);
+          if (w == 0) db3 += o[0];
+#pragma unroll
+          for (int hb = 0; hb < 2; ++hb) {
+            dq3[hb] = mfma16q(o[0], o[2 + hb], dq3[hb]);
+            dq1[hb] = mfma16q(o[4 + hb], o[1], dq1[hb]);
+          }
+#pragma unroll
+          for (int e = 0; e < 6; ++e) o[e] = on[e];
         }
       }
       LY_T(14);

@@ -12,5 +12,6 @@ import json, sys
 O, R = sys.argv[1], int(sys.argv[2])
 for k in ("base", "new"):
     v = [json.loads(open(f"{O}/{k}_{i}.json").read().strip().splitlines()[-1]) for i in range(1, R + 1)]
-    print(k, [d["ms_per_step"] for d in v], "k_ot_fwd", [d["roofline"]["per_kernel_ms"]["k_ot_fwd"] for d in v])
+    print(k, [d["ms_per_step"] for d in v])
+    for d in v: print("   ", d["roofline"]["per_kernel_ms"])
 PY
