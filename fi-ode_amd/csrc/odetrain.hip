@@ -842,13 +842,7 @@ __device__ void ot_vjp4(const OTArgs& a, const VjpW4& wv, OtBwdShared4& sh, int 
   OT_MARK(11);
   // g_a1 = Q2^T g_z2 of units 32p + 4 blk + r: K half hi, 4 accumulators
   f32x4v acc[4] = {zero4(), zero4(), zero4(), zero4()};
-  const float* gzr = &sh.gz2s[j][64 * hi];
-#pragma unroll
-  for (int s = 0; s < 64; s += 4) {
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(gzr + s);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = mfma4(wv.q2t[s + t], bv[t], acc[t]);
-  }
+  k128_half(&sh.gz2s[j][64 * hi], wv.q2t, acc);
   f32x4v gb;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {

@@ -94,6 +94,25 @@ __device__ __forceinline__ void dropout_relu4(f32x4v& z, uint32_t w, int blk, fl
   }
 }
 
+// acc[t] += sum_s q[4s + t] * src[4s + t] over one K half (64 values of the lane's sample in LDS):
+// the 16 B operands are read KD k-steps ahead of their MFMAs -- one step of 4 MFMAs (~34 cycles)
+// does not cover a ds_read_b128's latency, and the compiler's own schedule reads one step ahead
+// (the scheduling barriers keep it from sinking the reads back next to their MFMAs)
+__device__ __forceinline__ void k128_half(const float* src, const float (&q)[64], f32x4v (&acc)[4]) {
+  constexpr int KD = 8;
+  f32x4 bv[16];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) bv[s] = *reinterpret_cast<const f32x4*>(src + 4 * s);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + KD < 16) bv[s + KD] = *reinterpret_cast<const f32x4*>(src + 4 * (s + KD));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = mfma4(q[4 * s + t], bv[s][t], acc[t]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // The MLP of one 4-row tile for hidden part p: uacc = u[sample][32p + 4 (b & 7) + r] (this lane's
 // sample, accumulator order); h: the lane's sample input; kw1p / kw2p: the part's keep words of the
 // two dropout layers.  a1row / a2row (nullable): the sample's saved rows (lanes b < 8 store their
@@ -118,13 +137,7 @@ __device__ __forceinline__ void mlp4_part(const T4W& w, const f32x4& uacc, const
   __syncthreads();
   // layer 2: units 32p + 4 blk + r, K half hi (a1 of units 64 hi + s), 4 accumulators (s mod 4)
   f32x4v acc[4] = {zero4(), zero4(), zero4(), zero4()};
-  const float* a1 = &sh.a1s[j][64 * hi];
-#pragma unroll
-  for (int s = 0; s < 64; s += 4) {
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(a1 + s);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = mfma4(w.q2[s + t], bv[t], acc[t]);
-  }
+  k128_half(&sh.a1s[j][64 * hi], w.q2, acc);
   f32x4v z2;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
