@@ -204,6 +204,15 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
     __syncthreads();
     tile_gemm(sA, sB, w, i, q, acc, -1.0f);
   } else {
+    // X_ij (the second product's accumulator) is loaded with the operands, so its global-load
+    // latency hides behind the first product instead of following it
+    f4v xij[4];
+    if (!piv_r) {
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xij[bj][r] = X[(int64_t)(ib + 16 * w + 4 * q + r) * np + jb + 16 * bj + i];
+    }
     tile_load(sA, P, PB, false);              // R_Kj = P X_Kj
     tile_load(sB, X + (int64_t)k0 * np + jb, np, true);
     if (!piv_r) tile_load(sX, X + (int64_t)ib * np + k0, np, false);
@@ -216,9 +225,7 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
         *reinterpret_cast<f4v*>(&sB[16 * bj + i][16 * w + 4 * q]) = acc[bj];
       __syncthreads();
 #pragma unroll
-      for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[bj][r] = X[(int64_t)(ib + 16 * w + 4 * q + r) * np + jb + 16 * bj + i];
+      for (int bj = 0; bj < 4; ++bj) acc[bj] = xij[bj];
       tile_gemm(sX, sB, w, i, q, acc, -1.0f);
     }
   }

@@ -26,18 +26,18 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4v mfma(float a, float b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
-// the value of this lane's column in lane row qk (rows of 16 lanes), for a compile-time qk
+// the value of this lane's column in lane row QK (rows of 16 lanes), for a compile-time QK: one
+// v_permlane16_swap gives every row pair the value of its row with QK's bit 0, one
+// v_permlane32_swap carries it to the other pair; selects only (per-lane masks, no exec branches)
 template <int QK>
 __device__ __forceinline__ float from_row(float v, int q) {
   const uint32_t u = __float_as_uint(v);
   const auto s16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
   const uint32_t x1 = (q & 1) ? s16[0] : s16[1];                // row q ^ 1
-  const auto s32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  const uint32_t x2 = (q & 2) ? s32[0] : s32[1];                // row q ^ 2
-  const auto s32b = __builtin_amdgcn_permlane32_swap(x1, x1, false, false);
-  const uint32_t x3 = (q & 2) ? s32b[0] : s32b[1];              // row q ^ 3
-  const int d = q ^ QK;
-  return __uint_as_float(d == 0 ? u : (d == 1 ? x1 : (d == 2 ? x2 : x3)));
+  const uint32_t y = ((q & 1) == (QK & 1)) ? u : x1;            // row (q & 2) | (QK & 1)
+  const auto s32 = __builtin_amdgcn_permlane32_swap(y, y, false, false);
+  const uint32_t y2 = (q & 2) ? s32[0] : s32[1];                // y of row q ^ 2
+  return __uint_as_float(((q & 2) == (QK & 2)) ? y : y2);
 }
 
 template <int K>
@@ -47,7 +47,8 @@ __device__ __forceinline__ float newbcast(float v) {             // lane K of th
 
 // In-register Gauss-Jordan of one 16 x 16 block held by one wave: lane (c = lane & 15, q = lane >> 4)
 // holds x[r] = B[4q + r][c].  Pivot k: column entries of my rows B[4q + r][k] by row_newbcast:k,
-// the pivot row entry B[k][c] from lane row k >> 2, the pivot from lane k.
+// the pivot row entry B[k][c] from lane row k >> 2, the pivot B[k][k] by row_newbcast:k of that
+// (every row holds the pivot row after from_row: no readlane / SGPR round trip on the chain).
 template <int K>
 __device__ __forceinline__ void gj16_step(float (&x)[4], int c, int q) {
   constexpr int QK = K >> 2, RK = K & 3;
@@ -55,7 +56,7 @@ __device__ __forceinline__ void gj16_step(float (&x)[4], int c, int q) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) colv[r] = newbcast<K>(x[r]);
   const float rowv = from_row<QK>(x[RK], q);
-  const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rowv), K));
+  const float piv = newbcast<K>(rowv);
   const float p = __builtin_amdgcn_rcpf(piv);
   const float rp = rowv * p;
   const bool is_col = c == K;

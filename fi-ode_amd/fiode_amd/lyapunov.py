@@ -445,8 +445,10 @@ class LyapunovLearning(nn.Module):
             bb = self.init_coordinates.param_map
             target = bb[-1] if isinstance(bb, torch.nn.Sequential) else bb
 
-            def hook(i, _t=target):
-                if i == -1:
+            at = getattr(self, "_prefetch_at", -1)      # tools/ab_step.py probes later capture points
+
+            def hook(i, _t=target, _at=at):
+                if i == _at:
                     _t.after_conv_hook = None
                     self._in_input_hook = True
                     try:

@@ -58,6 +58,14 @@ def unfused_loss(m):
     m.fused_ode_loss = False
 
 
+def pf_conv0(m):
+    m._prefetch_at = 0        # map prefetch captured after conv layer 0 instead of before it
+
+
+def pf_conv1(m):
+    m._prefetch_at = 1
+
+
 def ode_on_main(m):
     m.ode_side_stream = False
 
@@ -67,7 +75,8 @@ def seed1000(m):
 
 
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
-       "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000}
+       "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
+       "pf_conv1": pf_conv1}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
