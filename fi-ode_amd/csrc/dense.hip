@@ -77,6 +77,36 @@ __global__ void __launch_bounds__(NT) k_dense_finish(DArgs a, const float* __res
   }
 }
 
+// Wide maps (cin > cout): Q[o][c] = 2 inv[c][o] - [c == o] for c < k reads inv transposed, so Q is
+// written in 32 x 32 tiles with the inv tile staged through LDS (both sides coalesced); the
+// columns c >= k read P row-major along c.  grid (cin / 32, cout / 32, batch).
+__global__ void __launch_bounds__(NT) k_dense_finish_wide(DArgs a, const float* __restrict__ inv,
+                                                          const float* __restrict__ P, float* __restrict__ Q) {
+  __shared__ float t[32][33];
+  const int b = blockIdx.z, k = a.k, o0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int x = threadIdx.x & 31, y0 = threadIdx.x >> 5;        // 8 rows of 32 per pass
+  float* Qb = Q + (int64_t)b * a.cout * a.cin;
+  if (c0 < k) {                                                  // (k % 32 == 0: whole tile inside)
+    const float* ib = inv + (int64_t)b * k * k;
+#pragma unroll
+    for (int y = y0; y < 32; y += 8) t[y][x] = ib[(int64_t)(c0 + y) * k + o0 + x];   // t[c][o]
+    __syncthreads();
+#pragma unroll
+    for (int y = y0; y < 32; y += 8) {
+      float q = 2.0f * t[x][y];                                  // inv[c0 + x][o0 + y]
+      if (c0 + x == o0 + y) q -= 1.0f;
+      Qb[(int64_t)(o0 + y) * a.cin + c0 + x] = q;
+    }
+  } else {
+    const float s = a.alpha[b] / a.nrm[b];
+    const int RV = a.R - k;
+    const float* Pb = P + (int64_t)b * RV * k;
+#pragma unroll
+    for (int y = y0; y < 32; y += 8)
+      Qb[(int64_t)(o0 + y) * a.cin + c0 + x] = -2.0f * s * Pb[(int64_t)(o0 + y) * RV + (c0 + x - k)];
+  }
+}
+
 __global__ void __launch_bounds__(NT) k_dense_ginv(DArgs a, const float* __restrict__ Gq, const float* __restrict__ A,
                                                    float* __restrict__ Ginv) {
   const int b = blockIdx.y, k = a.k;
@@ -138,8 +168,50 @@ __global__ void __launch_bounds__(NT) k_dense_gv(DArgs a, const float* __restric
   }
 }
 
+// k_dense_gv with float4 rows (cin % 4 == 0, k % 4 == 0): block x walks rows x, x + DPARTS, ...
+// and a row's float4 columns in order -- no per-element division, every access 16 bytes wide
+__global__ void __launch_bounds__(NT) k_dense_gv4(DArgs a, const float* __restrict__ P1, const float* __restrict__ P2,
+                                                  float* __restrict__ gX, float* __restrict__ dpart) {
+  __shared__ float red[NT / 64];
+  const int b = blockIdx.y, k = a.k, n = a.cout * a.cin, RV = a.R - k, c4n = a.cin >> 2;
+  const float s = a.alpha[b] / a.nrm[b];
+  const float* Wb = a.W + (int64_t)b * n;
+  const float* P1b = P1 ? P1 + (int64_t)b * RV * k : nullptr;
+  const float* P2b = P2 ? P2 + (int64_t)b * RV * k : nullptr;
+  float* gXb = gX + (int64_t)b * n;
+  float d = 0.f;
+  for (int o = blockIdx.x; o < a.cout; o += DPARTS) {
+    for (int c4 = threadIdx.x; c4 < c4n; c4 += NT) {
+      const int c = 4 * c4;
+      const int r = a.wide ? c : o;                 // the 4 columns share r < k or r >= k
+      const int64_t idx = (int64_t)o * a.cin + c;
+      f32x4 g;
+      if (r < k) {
+        g = *reinterpret_cast<const f32x4*>(gXb + idx);
+      } else {
+        const int64_t pi = a.wide ? (int64_t)o * RV + (c - k) : (int64_t)(o - k) * k + c;
+        const f32x4 p1 = *reinterpret_cast<const f32x4*>(P1b + pi), p2 = *reinterpret_cast<const f32x4*>(P2b + pi);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = s * p1[e] - 2.0f * p2[e];
+        *reinterpret_cast<f32x4*>(gXb + idx) = g;
+      }
+      const f32x4 w = *reinterpret_cast<const f32x4*>(Wb + idx);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d = fmaf(g[e], w[e], d);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int q = 0; q < NT / 64; ++q) t += red[q];
+    dpart[b * DPARTS + blockIdx.x] = t;
+  }
+}
+
 __global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restrict__ gX, const float* __restrict__ dpart,
-                                                 float* __restrict__ gW, float* __restrict__ galpha) {
+                                                 float* __restrict__ gW, float* __restrict__ galpha, int vec) {
   __shared__ float sD;
   const int b = blockIdx.y;
   if (threadIdx.x < 64) {                     // fixed-order sum of the D partials
@@ -156,7 +228,18 @@ __global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restric
   const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
   const float* gXb = gX + (int64_t)b * a.cout * a.cin;
   float* gWb = gW + (int64_t)b * a.cout * a.cin;
-  for (int idx = blockIdx.x * NT + threadIdx.x; idx < a.cout * a.cin; idx += gridDim.x * NT)
+  const int ne = a.cout * a.cin;
+  if (vec) {                                  // float4: ne % 4 == 0 and 16-byte aligned matrices (host check)
+    for (int i4 = blockIdx.x * NT + threadIdx.x; i4 < (ne >> 2); i4 += gridDim.x * NT) {
+      const f32x4 g = reinterpret_cast<const f32x4*>(gXb)[i4], w = reinterpret_cast<const f32x4*>(Wb)[i4];
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = s * g[e] - cw * w[e];
+      reinterpret_cast<f32x4*>(gWb)[i4] = o;
+    }
+    return;
+  }
+  for (int idx = blockIdx.x * NT + threadIdx.x; idx < ne; idx += gridDim.x * NT)
     gWb[idx] = s * gXb[idx] - cw * Wb[idx];
 }
 
@@ -208,8 +291,12 @@ extern "C" int fiode_dense_cayley_finish(void* stream, const fiode_dense_config*
   if (!alpha || !nrm || !inv || !Q || (a.R > a.k && !P)) return FIODE_EINVAL;
   a.alpha = alpha;
   a.nrm = nrm;
-  hipLaunchKernelGGL(k_dense_finish, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, (hipStream_t)stream, a,
-                     inv, P, Q);
+  if (a.wide && a.cout % 32 == 0 && a.cin % 32 == 0)
+    hipLaunchKernelGGL(k_dense_finish_wide, dim3(a.cin / 32, a.cout / 32, batch), dim3(NT), 0, (hipStream_t)stream, a,
+                       inv, P, Q);
+  else
+    hipLaunchKernelGGL(k_dense_finish, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, (hipStream_t)stream, a,
+                       inv, P, Q);
   DENSE_RET();
 }
 
@@ -254,8 +341,14 @@ extern "C" int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* c
   a.nrm = nrm;
   hipStream_t st = (hipStream_t)stream;
   float* dpart = (float*)workspace;
-  hipLaunchKernelGGL(k_dense_gv, dim3(DPARTS, batch), dim3(NT), 0, st, a, P1, P2, gX, dpart);
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const bool vec = a.cin % 4 == 0 && a.k % 4 == 0 && al16(W) && al16(gX) && al16(gW) && (!P1 || al16(P1)) &&
+                   (!P2 || al16(P2));
+  if (vec)
+    hipLaunchKernelGGL(k_dense_gv4, dim3(DPARTS, batch), dim3(NT), 0, st, a, P1, P2, gX, dpart);
+  else
+    hipLaunchKernelGGL(k_dense_gv, dim3(DPARTS, batch), dim3(NT), 0, st, a, P1, P2, gX, dpart);
   hipLaunchKernelGGL(k_dense_gw, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, st, a, (const float*)gX, dpart,
-                     gW, galpha);
+                     gW, galpha, vec ? 1 : 0);
   DENSE_RET();
 }
