@@ -335,8 +335,14 @@ struct OtShared4 {
   int pad;
 };
 
+// end_barrier: the trailing workgroup barrier, which k_ot_fwd4 leaves out -- every LDS word this
+// eval reads is either the lane's own (mu_rec) or is next written only behind a barrier of the next
+// eval that every wave reaches after its last read here: a1s / zpart behind the next layer-1
+// barrier, K / Kprev by lane 0 of wave 0 behind it too, a2s by the owning wave only.  The dopri5
+// solve keeps it (its caller shares the workgroup's LDS between evals).
 __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, int p, int b, bool valid, int lane,
-                         int j, const f32x4& uacc, uint32_t kw1p, uint32_t kw2p, const float (&h)[C], float (&k)[C]) {
+                         int j, const f32x4& uacc, uint32_t kw1p, uint32_t kw2p, const float (&h)[C], float (&k)[C],
+                         bool end_barrier = true) {
   const int bb = valid ? b : a.B - 1;
   const size_t r = (size_t)bb * a.E + e;
   const bool writer = p == 0 && valid && lane < TR4;     // lane j of wave 0 stores sample j's rows
@@ -393,7 +399,7 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
   if (blockIdx.x == 0 && threadIdx.x == 0 && e < 96) a.prof[16 + e] = (unsigned long long)K;
 #endif
   if (threadIdx.x == 0) sh.Kprev = K;
-  __syncthreads();            // zpart / a1s / mu_rec / K reused by the next eval
+  if (end_barrier) __syncthreads();            // (uniform)
   OT_MARK(4);
 }
 
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(256) void k_ot_fwd4(OTArgs a) {
 #define OT4_STAGE(E_, H_, K_)                                                            \
     {                                                                                    \
       if ((E_) + 1 < eN) fetch((E_) + 1, kn1, kn2);                                      \
-      ot_eval4(a, w, sh, (E_), p, b, valid, lane, j, uacc, kc1, kc2, H_, K_);           \
+      ot_eval4(a, w, sh, (E_), p, b, valid, lane, j, uacc, kc1, kc2, H_, K_, false);    \
       kc1 = kn1;                                                                         \
       kc2 = kn2;                                                                         \
     }
