@@ -373,7 +373,7 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
   }
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][lane][0];
-  qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
+  const int K = qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
             a.xslots + (size_t)e * 2 * gridDim.x * OT4_XSTRIDE, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
             a.drop_block,
 #ifdef OT_PROFILE
@@ -381,9 +381,8 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
 #else
             nullptr,
 #endif
-            OT4_XSTRIDE);
+            OT4_XSTRIDE, gridDim.x <= 64);
   OT_MARK(3);
-  const int K = sh.K;
   const float mu = sh.mu_rec[p][lane][K];
 #pragma unroll
   for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);

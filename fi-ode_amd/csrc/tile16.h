@@ -326,11 +326,16 @@ __device__ __forceinline__ void ft16_sum(const float (*zpart)[64][4], int j, flo
 // mask in granule slot slots[blockIdx] (epoch), gather all tiles; only if no iteration <= kspec
 // converged everywhere, resume to max_iter - 1 and exchange again in slots[ntiles + ..].  Called
 // by all 4 waves (identical rows); wave 0 exchanges; shK is an LDS int.  Returns K (uniform).
+// allg (callers pass it for grids of <= 64 tiles, one granule per lane): every wave gathers the
+// granules itself and returns K from its own registers (the rows are replicated over the waves, so
+// all compute the same masks and the same K): no workgroup barrier and no LDS round trip for K;
+// wave 0 still publishes, shK is left untouched.  With more tiles the 4x polling costs more than
+// the barrier (B = 1024: exchange wait 2.35 -> 2.83 us per eval), so those keep the broadcast.
 __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&nominal)[C], float tol, int max_iter,
                                          int kprev, bool valid, int p, int q, int lane, float* mu_rec_row,
                                          unsigned long long* slots, unsigned epoch, int32_t* status, int& shK,
                                          int& dead, int drop_block = -1,
-                                         unsigned long long* prof = nullptr, int stride = 1) {
+                                         unsigned long long* prof = nullptr, int stride = 1, bool allg = false) {
   const int last = max_iter - 1;
   const int kspec = min(last, kprev + FIODE_KSPEC_MARGIN);
   float lo, hi;
@@ -341,32 +346,41 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   const uint64_t t1 = prof ? wall_clock64() : 0;
   if (pr) atomicAdd(prof + 6, (unsigned long long)(t1 - t0));
   const int ntiles = gridDim.x;
-  if (p == 0) {
+  int kw = 0;
+  if (allg || p == 0) {
     // drop_block (test hook, FIODE_DEBUG_DROP_PUBLISH): that workgroup never publishes epoch 1,
     // as if it were not resident -- exercises the timeout path
-    if (lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block))
+    if (p == 0 && lane == 0 && !(epoch == 1u && (int)blockIdx.x == drop_block))
       publish_mask(slots + (size_t)blockIdx.x * stride, epoch, conv);
     const uint32_t all = gather_masks(slots, ntiles, epoch, status, lane, dead, stride);
     const uint32_t lowm = kspec >= 31 ? 0xFFFFFFFFu : ((1u << (kspec + 1)) - 1u);
     const uint32_t bits = all & lowm;
-    if (lane == 0) shK = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
+    kw = bits ? (__ffs((int)bits) - 1) : (kspec >= last ? last : -1);
+    if (!allg && lane == 0) shK = kw;
   }
-  __syncthreads();
+  if (!allg) {                          // (uniform)
+    __syncthreads();
+    kw = shK;
+  }
   if (pr) {
     atomicAdd(prof + 7, (unsigned long long)(wall_clock64() - t1));
-    if (shK < 0) atomicAdd(prof + 8, 1ull);
+    if (kw < 0) atomicAdd(prof + 8, 1ull);
   }
-  if (shK < 0) {                        // block-uniform: every tile saw the same masks
+  if (kw < 0) {                         // block-uniform: every tile saw the same masks
     conv |= qp_bisect_seq(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, true, valid);
-    if (p == 0) {
+    if (allg || p == 0) {
       unsigned long long* s2 = slots + (size_t)ntiles * stride;
-      if (lane == 0) publish_mask(s2 + (size_t)blockIdx.x * stride, epoch, conv);
+      if (p == 0 && lane == 0) publish_mask(s2 + (size_t)blockIdx.x * stride, epoch, conv);
       const uint32_t all = gather_masks(s2, ntiles, epoch, status, lane, dead, stride);
-      if (lane == 0) shK = qp_exit_iter(all, max_iter);
+      kw = qp_exit_iter(all, max_iter);
+      if (!allg && lane == 0) shK = kw;
     }
-    __syncthreads();
+    if (!allg) {
+      __syncthreads();
+      kw = shK;
+    }
   }
-  return shK;
+  return kw;
 }
 
 }  // namespace fiode_t16
