@@ -66,6 +66,15 @@ def pf_conv1(m):
     m._prefetch_at = 1
 
 
+RESTORE = []      # module-level switches a variant flips for its own capture only
+
+
+def dense_bwd_side(m):
+    from fiode_amd import cayley as CY
+    CY.DENSE_BWD_ON_MAIN = False  # each dense map's backward on its forward's (prefetch) stream
+    RESTORE.append(lambda: setattr(CY, "DENSE_BWD_ON_MAIN", True))
+
+
 def ode_on_main(m):
     m.ode_side_stream = False
 
@@ -76,11 +85,15 @@ def seed1000(m):
 
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
-       "pf_conv1": pf_conv1}
+       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
-steps = {k: make(f) for k, f in VARIANTS.items()}
+steps = {}
+for k, f in VARIANTS.items():
+    steps[k] = make(f)          # captured in GraphTrainStep.__init__
+    while RESTORE:
+        RESTORE.pop()()
 times = {k: [] for k in VARIANTS}
 for r in range(rounds):
     for k, gs in steps.items():
