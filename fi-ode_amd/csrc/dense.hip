@@ -243,6 +243,74 @@ __global__ void __launch_bounds__(NT) k_dense_gw(DArgs a, const float* __restric
     gWb[idx] = s * gXb[idx] - cw * Wb[idx];
 }
 
+// C[b] = op(A[b]) op(B[b]) for n x n matrices (n % 64 == 0), op = transpose when TA / TB: the
+// dense maps' backward chain GMn = inv^T (Ginv inv^T), two dependent 512^3 products that the
+// library runs as 16 workgroups of 128 x 128 tiles (~14 us each).  Here 32 x 32 output tiles
+// (256 workgroups at n = 512), the 4 waves split K (n / 4 each) on v_mfma_f32_16x16x4_f32 with
+// operands straight from L2 (16-byte loads along k where the layout allows, 64-byte rows
+// otherwise), the 4 partials summed in LDS in a fixed order (tools/probes/sgemm_probe.hip).
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(256) k_dense_gemm(int n, const float* __restrict__ A, const float* __restrict__ B,
+                                                    float* __restrict__ C) {
+  __shared__ float red[4][32][33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int tm = blockIdx.y * 32, tn = blockIdx.x * 32;
+  const int64_t mo = (int64_t)blockIdx.z * n * n;
+  A += mo;
+  B += mo;
+  C += mo;
+  const int ks = n >> 2, k0 = w * ks;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // chunk of 16 k: step s uses k = kb + s, kb = k0 + 16 kc + 4 q at lane q
+  for (int kc = 0; kc < ks / 16; ++kc) {
+    const int kb = k0 + 16 * kc + 4 * q;
+    f32x4 av[2], bv[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int m = tm + 16 * x + i;
+      if (TA) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) av[x][s] = A[(int64_t)(kb + s) * n + m];
+      } else {
+        av[x] = *reinterpret_cast<const f32x4*>(A + (int64_t)m * n + kb);
+      }
+    }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int c = tn + 16 * y + i;
+      if (TB) {
+        bv[y] = *reinterpret_cast<const f32x4*>(B + (int64_t)c * n + kb);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[y][s] = B[(int64_t)(kb + s) * n + c];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[x][s], bv[y][s], acc[x][y], 0, 0, 0);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][16 * x + 4 * q + r][16 * y + i] = acc[x][y][r];   // D[4q + r][i]
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    const int r = e >> 5, c = e & 31;
+    C[(int64_t)(tm + r) * n + tn + c] = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
+  }
+}
+
 int mk(const fiode_dense_config* cfg, DArgs& a, int& batch) {
   if (!cfg || cfg->batch < 1 || cfg->cout < 1 || cfg->cin < 1) return FIODE_EINVAL;
   a = DArgs{};
@@ -350,5 +418,19 @@ extern "C" int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* c
     hipLaunchKernelGGL(k_dense_gv, dim3(DPARTS, batch), dim3(NT), 0, st, a, P1, P2, gX, dpart);
   hipLaunchKernelGGL(k_dense_gw, grid_for((int64_t)a.cout * a.cin, batch), dim3(NT), 0, st, a, (const float*)gX, dpart,
                      gW, galpha, vec ? 1 : 0);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_gemm(void* stream, int32_t batch, int32_t n, int32_t trans_a, int32_t trans_b,
+                                const float* A, const float* B, float* C) {
+  if (batch < 1 || batch > 65535 || n < 64 || !A || !B || !C) return FIODE_EINVAL;
+  if (n % 64 != 0) return FIODE_ESHAPE;
+  if ((((uintptr_t)A | (uintptr_t)B) & 15u) != 0) return FIODE_ESHAPE;   // 16-byte operand loads
+  const dim3 grid((unsigned)(n / 32), (unsigned)(n / 32), (unsigned)batch);
+  hipStream_t st = (hipStream_t)stream;
+  if (trans_a && trans_b) hipLaunchKernelGGL((k_dense_gemm<true, true>), grid, dim3(256), 0, st, n, A, B, C);
+  else if (trans_a) hipLaunchKernelGGL((k_dense_gemm<true, false>), grid, dim3(256), 0, st, n, A, B, C);
+  else if (trans_b) hipLaunchKernelGGL((k_dense_gemm<false, true>), grid, dim3(256), 0, st, n, A, B, C);
+  else hipLaunchKernelGGL((k_dense_gemm<false, false>), grid, dim3(256), 0, st, n, A, B, C);
   DENSE_RET();
 }

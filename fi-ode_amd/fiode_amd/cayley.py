@@ -196,7 +196,15 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
                                         ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
     ih = inv.mT
-    GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
+    if DENSE_GEMM and k % 64 == 0 and inv.is_contiguous() and inv.data_ptr() % 16 == 0 and Ginv.data_ptr() % 16 == 0:
+        # GMn = inv^T (Ginv inv^T) by fiode_dense_gemm (256 workgroups at k = 512; the library's
+        # 128 x 128 tiles leave 240 CUs idle on this latency-bound chain)
+        T = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
+        GMn = torch.empty_like(T)
+        L.check(lib.fiode_dense_gemm(st, b, k, 0, 1, Ginv.data_ptr(), inv.data_ptr(), T.data_ptr()), "fiode_dense_gemm")
+        L.check(lib.fiode_dense_gemm(st, b, k, 1, 0, inv.data_ptr(), T.data_ptr(), GMn.data_ptr()), "fiode_dense_gemm")
+    else:
+        GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
     gX = torch.empty_like(Wb)                    # W layout
     H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
@@ -339,6 +347,7 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
 # in the interleaved A/B (tools/ab_step.py); the spectral maps' is slower there (2.35 ms).
 SPECTRAL_BWD_ON_MAIN = False
 DENSE_BWD_ON_MAIN = True
+DENSE_GEMM = True          # GMn by fiode_dense_gemm (tools/ab_step.py `lib_gmn` measures the library form)
 SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 

@@ -357,6 +357,12 @@ FIODE_API size_t fiode_dense_cayley_workspace_bytes(const fiode_dense_config* cf
 FIODE_API int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
                                       const float* nrm, const float* P1, const float* P2, float* gX, float* gW,
                                       float* galpha, void* workspace, size_t workspace_bytes);
+/* C[b] = op(A[b]) op(B[b]) for a batch of n x n row-major float matrices (op = transpose when
+ * trans_a / trans_b), n % 64 == 0, A and B 16-byte aligned (FIODE_ESHAPE otherwise): the two
+ * dependent k x k products of the dense maps' backward, GMn = inv^T (Ginv inv^T) (cayley.py
+ * _dense_backward; the reference's autograd through torch.inverse, classification.py:282-293). */
+FIODE_API int fiode_dense_gemm(void* stream, int32_t batch, int32_t n, int32_t trans_a, int32_t trans_b,
+                               const float* A, const float* B, float* C);
 
 /* ---- spectral convolution transforms on spatial-major activations [n][n][C][B] (CayleyConv
  * forward_hwcb; fiode_amd/cayley.py).  Spectrum layout [f][C][B] complex64, f = ka (n/2+1) + kb. */

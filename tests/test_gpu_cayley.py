@@ -456,3 +456,27 @@ def test_conditional_block_inverse_skip_flag():
     skip.zero_()
     ops.block_inverse(M, out=out, skip=skip)
     assert torch.equal(out, exact)
+
+
+@pytest.mark.parametrize("n,batch", [(64, 1), (128, 2), (512, 1)])
+def test_dense_gemm_matches_float64(n, batch):
+    """fiode_dense_gemm (the dense maps' backward products, dense.hip) = float64 matmul for every
+    transpose combination, within 2e-5 of the result's max (fp32 sums over K = n)."""
+    import ctypes as ct
+    from fiode_amd import ops, _lib as L
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(n + batch)
+    A = torch.randn(batch, n, n, generator=g).to(dev)
+    B = torch.randn(batch, n, n, generator=g).to(dev)
+    for ta in (0, 1):
+        for tb in (0, 1):
+            C = torch.empty_like(A)
+            L.check(L.lib().fiode_dense_gemm(ops._stream(dev), batch, n, ta, tb, A.data_ptr(), B.data_ptr(),
+                                             C.data_ptr()), "fiode_dense_gemm")
+            a, b = A.double(), B.double()
+            ref = (a.mT if ta else a) @ (b.mT if tb else b)
+            err = float((C.double() - ref).abs().max())
+            assert err <= 2e-5 * float(ref.abs().max()), (ta, tb, err)
+    assert L.lib().fiode_dense_gemm(ops._stream(dev), 1, 96, 0, 0, A.data_ptr(), B.data_ptr(), A.data_ptr()) == \
+        2      # FIODE_ESHAPE (include/fiode.h)
+

@@ -75,6 +75,12 @@ def dense_bwd_side(m):
     RESTORE.append(lambda: setattr(CY, "DENSE_BWD_ON_MAIN", True))
 
 
+def lib_gmn(m):
+    from fiode_amd import cayley as CY
+    CY.DENSE_GEMM = False         # the dense maps' GMn products by the library GEMM
+    RESTORE.append(lambda: setattr(CY, "DENSE_GEMM", True))
+
+
 def ode_on_main(m):
     m.ode_side_stream = False
 
@@ -85,7 +91,7 @@ def seed1000(m):
 
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
-       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side}
+       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
