@@ -175,6 +175,48 @@ def load_pmc(kernel: str) -> dict:
             "lds_bank_conflict_frac": k.get("lds_bank_conflict_frac"), "pmc_source": d.get("_source")}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """``--gpus N`` (N > 1) without a launcher around us: start N rank processes as CHILDREN
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) -- the reference's
+    ``Trainer(gpus=N, accelerator='ddp')`` spawns its ranks the same way (sl_pipeline.py:157-170).
+    Called before this process touches the GPU (no exec: the parent waits and relays).  Rank 0's
+    JSON line is checked (n_gpus == N, parallelism dpN) and re-printed; anything else on the ranks'
+    stdout goes to stderr.  Returns the exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py")] + argv
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, cwd=str(ROOT))
+    lines = []
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            lines.append(s)
+        else:
+            print(line, end="", file=sys.stderr, flush=True)
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: rank processes exited with {rc}", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    rec = json.loads(lines[0])
+    if rec.get("n_gpus") != n or rec.get("config", {}).get("parallelism") != f"dp{n}":
+        print(f"bench.py: refusing a line with n_gpus={rec.get('n_gpus')} for --gpus {n}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,9 +230,15 @@ def main():
                     help="rk4: BASELINE configs[1] (Lyapunov loss + differentiable RK4 train_ode solve); "
                          "lyap: the Lyapunov-only step")
     ap.add_argument("--no-secondary", action="store_true", help="skip the Lyapunov-only companion measurement")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs[3] (certification) and configs[4] (B=1024 x S=1024) companion lines")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: the line would misreport n_gpus")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -200,15 +248,16 @@ def main():
     dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     torch.cuda.set_device(dev)
 
-    def timed_run(train_ode: bool, steps: int, warmup: int, solver: str = "rk4"):
+    def timed_run(train_ode: bool, steps: int, warmup: int, solver: str = "rk4", batch: int = B_PER_RANK,
+                  h_sample: int = H_SAMPLE):
         """Build the module, capture (or not) the step, run warmup + timed steps; max over ranks."""
-        mod = build_module(dev, seed=0, train_ode=train_ode, solver=solver)
+        mod = build_module(dev, seed=0, train_ode=train_ode, solver=solver, h_sample=h_sample)
         mod.seed = 1000 + rank                      # each rank draws its own samples / dropout masks
         opt = mod.configure_optimizers(capturable=not args.eager)[0][0]
         params = [p for p in mod.parameters() if p.requires_grad]
         g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-        x = torch.rand(B_PER_RANK, 3, 32, 32, generator=g).to(dev)
-        y = torch.randint(0, 10, (B_PER_RANK,), generator=g).to(dev)
+        x = torch.rand(batch, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (batch,), generator=g).to(dev)
         from fiode_amd.distributed import GradAllReducer, MetricReducer, broadcast_parameters
         broadcast_parameters(mod)                   # DDP's construction-time broadcast
         reducer = GradAllReducer(params) if world > 1 else None   # p.grad = views into one flat bucket
@@ -223,7 +272,7 @@ def main():
         if args.eager:
             def step():
                 opt.zero_grad(set_to_none=False)
-                loss = mod.compute_loss(x, y, B_PER_RANK, "relu")
+                loss = mod.compute_loss(x, y, batch, "relu")
                 loss.backward()
                 if world > 1:
                     reducer.allreduce(world)          # one RCCL all-reduce of the whole gradient
@@ -260,11 +309,50 @@ def main():
         # health of the timed run, read after the timed region: the sticky status of the persistent
         # train_ode solve (a timed-out QP-exit exchange poisons the loss with NaN) and the last loss
         health = {"status": int(mod.device_status()) if hasattr(mod, "device_status") else 0,
-                  "loss_finite": bool(torch.isfinite(last["loss"]).all())}
-        if health["status"] or not health["loss_finite"]:
+                  "loss_finite": bool(torch.isfinite(last["loss"]).all()),
+                  "skipped_steps": gstep.skipped_steps() if not args.eager else 0}
+        if health["status"] or not health["loss_finite"] or health["skipped_steps"]:
             raise RuntimeError(f"unhealthy timed run: {health}")
         health["comm"] = last.get("comm")
         return float(dt.item()), mod, x, y, health
+
+    def certify_companion(n_img: int = 2):
+        """BASELINE configs[3]: certify_lipschitz (certify_lipschitz.py:97-143) of this rank's images on
+        the T=40 decision-boundary grid (G = 41,320,837 rows, resident in HBM, built once), 10
+        batches + the 7-row tail, the QP exit per batch; images sharded over the ranks (each rank
+        certifies n_img images, the count all-reduce is outside the timed region)."""
+        from fiode_amd import ops
+        from fiode_amd.certify import certify_lipschitz
+        grid = ops.certify_grid(40, device=dev)
+        G = int(grid.shape[0])
+        cmod = build_module(dev, seed=0, train_ode=False)
+        g = torch.Generator(device="cpu").manual_seed(4321 + rank)
+        xs = torch.rand(n_img + 1, 3, 32, 32, generator=g).to(dev)
+        ys = torch.randint(0, 10, (n_img + 1,), generator=g).to(dev)
+        certify_lipschitz(cmod, xs, ys, T=40, grid=grid, indices=[0])        # warm-up image
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = certify_lipschitz(cmod, xs, ys, T=40, grid=grid, indices=range(1, n_img + 1))
+        torch.cuda.synchronize()
+        dtc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.barrier()
+            dist.all_reduce(dtc, op=dist.ReduceOp.MAX)
+        ms = float(dtc.item()) / n_img * 1e3
+        flop = FLOP_ROW_FWD_PASS * G                 # one MLP per grid row (the QP pass reuses it)
+        tf = flop / (ms * 1e-3) / 1e12
+        del grid
+        torch.cuda.empty_cache()
+        return {"ms_per_image": round(ms, 3), "images_per_s": round(world * n_img / (n_img * ms * 1e-3), 3),
+                "grid_rows": G, "grid_rows_per_s": round(world * G / (ms * 1e-3), 1),
+                "mlp_tflops": round(tf, 3), "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "images_per_rank": n_img,
+                "max_violation": [round(v, 4) for v in res.max_violations],
+                "workload": "BASELINE configs[3]: certify_lipschitz on the T=40 decision-boundary grid, one image "
+                            "at a time (backbone + grid forward + QP per batch + violation max), images "
+                            f"sharded over {world} rank(s); TFLOP/s = 37,888 FLOP x G over the whole per-image "
+                            "time (all four kernels)"}
 
     train_ode = args.workload == "rk4"
     elapsed, mod, x, y, health = timed_run(train_ode, args.steps, args.warmup)
@@ -284,6 +372,22 @@ def main():
                        "last_solve": {"nfe": st3[0], "n_accept": st3[4], "n_reject": st3[5]},
                        "workload": "BASELINE configs[2]: the configs[1] step with train_ode_solver dopri5, "
                                    "train_ode_tol 1e-3 (rtol = atol), direct backprop through the adaptive solve"}
+    certify_line = large_batch = None
+    if not args.no_configs:
+        certify_line = certify_companion()
+        # BASELINE configs[4]: B=1024 images x h_sample 1024 per rank, train_ode dopri5 (tol 1e-3),
+        # backbone + Cayley maps + Adam, DDP over the ranks (the same bucketed all-reduce)
+        k4 = max(1, min(args.steps, 10))
+        e4, m4, _, _, h4 = timed_run(True, k4, 2, solver="dopri5", batch=1024, h_sample=1024)
+        st4 = m4.last_ode_plan["stats"].cpu().tolist()
+        large_batch = {"images_per_s": round(world * 1024 * k4 / e4, 2), "ms_per_step": round(e4 / k4 * 1e3, 4),
+                       "steps": k4, "rows_per_rank": 1024 * 1024, "device_status": h4,
+                       "last_solve": {"nfe": st4[0], "n_accept": st4[4], "n_reject": st4[5]},
+                       "workload": "BASELINE configs[4]: train step at B=1024 x h_sample 1024 per rank (S1=819 "
+                                   "uniform + 205 correct-cone rows/image), train_ode dopri5 tol 1e-3, "
+                                   f"KWLarge-Cayley backbone + Adam, dp{world}"}
+        del m4
+        torch.cuda.empty_cache()
 
     # ---- per-kernel timing of the fused hot path with HIP events (same inputs as a step) ----
     from fiode_amd import _lib as L, ops
@@ -360,6 +464,10 @@ def main():
            "hot_path": {"ms": round(hot_ms, 4), "images_per_s": round(world * B_PER_RANK / (hot_ms * 1e-3), 1)},
            "lyapunov_only_step": lyap_only,
            "dopri5_train_step": dopri5_step,
+           "certify_T40": certify_line,
+           "large_batch_step": large_batch,
+           "process_group": {"backend": dist.get_backend() if world > 1 else None, "world_size":
+                             dist.get_world_size() if world > 1 else 1},
            "device_status": health,
            "runtime_env": {"DEBUG_HIP_FORCE_GRAPH_QUEUES": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES")}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

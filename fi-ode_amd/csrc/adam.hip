@@ -11,6 +11,10 @@
 //   p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // t is the tensor's step count AFTER this step's increment, read from the device (capturable) or
 // given by the host.
+// Step guard (fiode_step_guard): a step whose train_ode solve failed (status word) or whose loss is
+// not finite -- or, on N ranks, any rank's such step (the guard slot of the all-reduced gradient
+// bucket) -- leaves p, m, v and the step counts as they were, like torch.cuda.amp's found_inf skip
+// but decided on the device; k_adam_steps counts the skipped steps in a sticky word.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -40,7 +44,30 @@ struct AdamArgs {
   const float* t_dev[MAXT];     // per-tensor step count on the device (capturable Adam)
   const void* lr_dev;          // device learning rate (tensor lr) or null
   int lr_dev_is_double;
+  fiode_step_guard guard;      // all-null: no guard
 };
+
+__device__ __forceinline__ bool guard_skip(const fiode_step_guard& g) {
+  bool bad = false;
+  if (g.flag) bad = bad || !(*g.flag == 0.f);            // nonzero or NaN
+  if (g.loss) bad = bad || !isfinite(*g.loss);
+#pragma unroll
+  for (int i = 0; i < FIODE_GUARD_MAX_STATUS; ++i)
+    if (g.status[i]) bad = bad || *g.status[i] != 0;
+  return bad;
+}
+
+// the step counts of a guarded step: +1 unless the guard skips it (then the sticky count +1)
+__global__ __launch_bounds__(64) void k_adam_steps(const AdamArgs a) {
+  const bool skip = guard_skip(a.guard);
+  for (int t = threadIdx.x; t < a.n; t += blockDim.x)
+    if (!skip && a.t_dev[t]) *const_cast<float*>(a.t_dev[t]) += 1.0f;
+  if (threadIdx.x == 0 && skip && a.guard.skipped) *a.guard.skipped += 1;
+}
+
+__global__ void k_guard_flag(const fiode_step_guard g, float* out) {
+  if (threadIdx.x == 0) out[0] = guard_skip(g) ? 1.0f : 0.0f;
+}
 
 struct Coef {
   float lr, b1, omb1, b2, omb2, eps, wd, step_size, bc2_sqrt;
@@ -60,6 +87,7 @@ __device__ __forceinline__ void adam_elem(const Coef& c, float& p, float g, floa
 }
 
 __global__ __launch_bounds__(NT) void k_adam(const AdamArgs a) {
+  if (guard_skip(a.guard)) return;
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < a.n && a.blk0[t + 1] <= b) ++t;
@@ -111,7 +139,7 @@ __global__ __launch_bounds__(NT) void k_adam(const AdamArgs a) {
 
 extern "C" int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float* const* params,
                                const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
-                               const int64_t* numel, const float* const* step) {
+                               const int64_t* numel, float* const* step, const fiode_step_guard* guard) {
   if (!cfg || cfg->n_tensors < 0 || cfg->n_tensors > MAXT) return FIODE_EINVAL;
   if (cfg->n_tensors == 0) return FIODE_OK;
   if (!params || !grads || !exp_avg || !exp_avg_sq || !numel) return FIODE_EINVAL;
@@ -127,6 +155,8 @@ extern "C" int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float
   a.step_h = cfg->step;
   a.lr_dev = cfg->lr_dev;
   a.lr_dev_is_double = cfg->lr_dev_is_double != 0;
+  if (guard) a.guard = *guard;
+  if (cfg->increment_steps && !step) return FIODE_EINVAL;
   int64_t blocks = 0;
   for (int i = 0; i < a.n; ++i) {
     if (numel[i] < 0 || (numel[i] > 0 && (!params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i])))
@@ -140,7 +170,22 @@ extern "C" int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float
   }
   a.blk0[a.n] = (int)blocks;
   if (blocks == 0) return FIODE_OK;
+  if (cfg->increment_steps) {
+    hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+    const hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return FIODE_EHIP + (int)e0;
+  }
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_step_guard_flag(void* stream, const fiode_step_guard* guard, float* flag_out) {
+  if (!guard || !flag_out) return FIODE_EINVAL;
+  fiode_step_guard g = *guard;
+  g.flag = nullptr;
+  g.skipped = nullptr;
+  hipLaunchKernelGGL(k_guard_flag, dim3(1), dim3(64), 0, (hipStream_t)stream, g, flag_out);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

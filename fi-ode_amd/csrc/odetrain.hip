@@ -34,9 +34,19 @@ using namespace fiode_t4;
 using namespace fiode_dp;
 
 
+// Ring of exit-exchange granule sets: eval e publishes into set e % OT_XRING with tag e + 1.  A tile
+// publishes eval e + 2 only after every tile published e + 1, and every tile publishes e + 1 only
+// after all its waves finished reading eval e's granules (the next eval's layer-1 barrier), so a
+// set is never overwritten while it is read; 4 sets leave a margin.  The cleared region no longer
+// grows with the eval count (dopri5: the attempt capacity).
+constexpr int OT_XRING = 4;
+
 struct OTArgs {
   int B, E, niters;
   int nslots;               // u64 words of xslots zeroed by k_ot_masks before the forward
+  int kw_lazy;              // dopri5, Philox p = 0.5: the forward draws each eval's keep words itself
+                            // (and stores them for the backward) instead of k_ot_masks drawing the
+                            // whole eval capacity up front
   float t0, t1, hstep;
   int dropout_mode, bit_mode;
   uint32_t thr8;
@@ -68,7 +78,8 @@ struct OTArgs {
   float* gz2;               // [B][E][M]
   float* gz1;               // [B][E][M]
   float* gft;               // [B][E][C]
-  unsigned long long* xslots;  // [E][2 phases][ntiles] {epoch, mask} granules of the QP exit exchange
+  unsigned long long* xslots;  // [OT_XRING][2 phases][ntiles] {epoch, mask} granules of the QP exit exchange
+                               // (eval e uses ring slot e % OT_XRING, tagged e + 1)
   uint32_t* kw;                // [E][2][B] uint4 dropout keep words
 #ifdef OT_PROFILE
   unsigned long long* prof;    // [9] wall-clock ticks per phase (workgroup 0, lane 0); [16 + e] eval e's exit K
@@ -180,7 +191,7 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][lane][0];
   qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
-            a.xslots + (size_t)e * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
+            a.xslots + (size_t)(e % OT_XRING) * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
             a.drop_block,
 #ifdef OT_PROFILE
             a.prof
@@ -216,7 +227,8 @@ __global__ __launch_bounds__(256) void k_ot_masks(OTArgs a) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q < a.nslots) a.xslots[q] = 0ull;
   if (q < 8) a.stats[q] = 0;
-  if (a.dropout_mode == FIODE_DROPOUT_OFF || q >= a.E * a.B) return;
+  if (q < 8) a.imeta[q] = 0;       // the solve's status word (saved [12]) and the dopri5 counters
+  if (a.dropout_mode == FIODE_DROPOUT_OFF || a.kw_lazy || q >= a.E * a.B) return;
   const int e = q / a.B, b = q - e * a.B;
   const Rng rng = rng_of(a);
 #pragma unroll
@@ -374,7 +386,8 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
   OT_MARK(5);
   float* rec = &sh.mu_rec[p][lane][0];
   const int K = qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
-            a.xslots + (size_t)e * 2 * gridDim.x * OT4_XSTRIDE, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
+            a.xslots + (size_t)(e % OT_XRING) * 2 * gridDim.x * OT4_XSTRIDE, (unsigned)e + 1u, a.stats + 3, sh.K,
+            sh.dead,
             a.drop_block,
 #ifdef OT_PROFILE
             a.prof,
@@ -1060,9 +1073,12 @@ __device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& 
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) acc[v] += __shfl_xor(acc[v], o, 64);
     }
+    // a timed-out exchange summed only the granules that arrived: NaN, so everything computed from
+    // it (y_out in the forward; g_dt and every stage adjoint upstream of it in the backward) is
+    // poisoned instead of silently wrong
     if (lane == 0)
 #pragma unroll
-      for (int v = 0; v < NV; ++v) red[v] = acc[v];
+      for (int v = 0; v < NV; ++v) red[v] = dead ? __builtin_nan("") : acc[v];
   }
   ++ep;
   __syncthreads();
@@ -1124,11 +1140,23 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
   // keep words of eval e: all 4 words of layer 1 and the part's layer-2 word (16-row), or the
   // part's word of each layer (4-row)
   const uint32_t* kwp = a.kw;
+  const Rng krng = rng_of(a);
   auto fetch = [&](int e, uint32_t (&w1)[4], uint32_t& w2) {
     if (a.dropout_mode == FIODE_DROPOUT_OFF) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) w1[t] = 0xFFFFFFFFu;
       w2 = 0xFFFFFFFFu;
+      return;
+    }
+    if (a.kw_lazy) {          // the draws k_ot_masks would make (same stream, index, offset)
+      const uint4 r0 = krng.draw((uint32_t)bb, RNG_STREAM_ODE_DROP + ((uint32_t)e << 5));
+      const uint4 r1 = krng.draw((uint32_t)bb, RNG_STREAM_ODE_DROP + ((uint32_t)e << 5) + (1u << 4));
+      w1[0] = r0.x; w1[1] = r0.y; w1[2] = r0.z; w1[3] = r0.w;
+      w2 = p == 0 ? r1.x : p == 1 ? r1.y : p == 2 ? r1.z : r1.w;
+      if (p == 0 && first && valid && e < a.E) {      // saved for the backward and the weight chain
+        reinterpret_cast<uint4*>(a.kw)[((size_t)e * 2 + 0) * a.B + b] = r0;
+        reinterpret_cast<uint4*>(a.kw)[((size_t)e * 2 + 1) * a.B + b] = r1;
+      }
       return;
     }
     const uint4 q1 = reinterpret_cast<const uint4*>(kwp)[((size_t)e * 2 + 0) * a.B + bb];
@@ -1346,6 +1374,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
     a.imeta[0] = e;
     a.imeta[1] = n;
     a.imeta[2] = status ? status : (sh.dead ? 4 : 0);
+    a.imeta[3] = (int32_t)rep;       // next unused reduction epoch: the backward continues from it
   }
 }
 
@@ -1420,7 +1449,13 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
     for (int c = 0; c < C; ++c) gout[c] = __builtin_nanf("");     // a failed forward: NaN gradients
   const double NBC = (double)a.B * C;
   const float rtol = (float)a.rtol, atol = (float)a.atol;
-  unsigned rep = 1;
+  // the reduction granules still hold the forward's last tags (and a previous sweep's on the same
+  // workspace): continue the epoch sequence where the last user of the workspace left it, so no
+  // stale granule can carry a current tag.  Every workgroup reads imeta[3] before its first
+  // exchange; workgroup 0 advances it only after its last exchange, which no workgroup passes
+  // before all have published theirs.
+  unsigned rep = (unsigned)a.imeta[3];
+  if (rep == 0u) rep = 1u;
   int buf = 0;
   std::conditional_t<T4, VjpIn4, VjpIn> cur, nxt;
   VjpRow crw, nrw;
@@ -1657,6 +1692,7 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   float gy0[C];
   vjp(gf0, gy0);                     // eval 0: f0 = f(y0)
   (void)gy0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.imeta[3] = (int32_t)rep;
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1710,8 +1746,8 @@ OtLayout ot_layout(int B, int E, int A = 0) {
   L.gz2 = o; o += al(R * M * 4);
   L.gz1 = o; o += al(R * M * 4);
   L.gft = o; o += al(R * C * 4);
-  const size_t nt = (size_t)(B + TR - 1) / TR, nt4 = (size_t)(B + TR4 - 1) / TR4;   // 16- / 4-row tiles
-  L.xs = o; o += (size_t)E * 2 * nt4 * 8 * OT4_XSTRIDE + 1024;     // the reduction granules follow: one clear for both
+  const size_t nt4 = (size_t)(B + TR4 - 1) / TR4;     // 4-row tiles (>= the 16-row kernel's tiles)
+  L.xs = o; o += (size_t)OT_XRING * 2 * nt4 * 8 * OT4_XSTRIDE + 1024;   // the reduction granules follow: one clear for both
   L.xr = o; o += al(A > 0 ? 2 * nt4 * 2 * OT_XV * 8 : 0);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
   L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
@@ -1772,7 +1808,7 @@ int fill_args(OTArgs& a, const fiode_odetrain_config* cfg, const fiode_dyn_confi
   a.meta = reinterpret_cast<double*>(ws + L.meta);
   a.imeta = reinterpret_cast<int32_t*>(ws + L.imeta);
 #ifdef OT_PROFILE
-  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)a.E * 2 * ((a.B + TR4 - 1) / TR4) * OT4_XSTRIDE + 8;
+  a.prof = reinterpret_cast<unsigned long long*>(ws + L.xs) + (size_t)OT_XRING * 2 * ((a.B + TR4 - 1) / TR4) * OT4_XSTRIDE + 8;
 #endif
   return FIODE_OK;
 }
@@ -1821,7 +1857,7 @@ extern "C" int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, in
   if (solve_shape(cfg, E, A, n) < 0) return FIODE_EINVAL;
   const OtLayout L = ot_layout(cfg->batch, E, A);
   const size_t o[FIODE_ODETRAIN_NSAVED] = {L.hs, L.ftw, L.vw, L.muw, L.nomw, L.a1, L.a2, L.gft, L.loww,
-                                           A ? L.ys : 0, A ? L.alog : 0, A ? L.meta : 0};
+                                           A ? L.ys : 0, A ? L.alog : 0, A ? L.meta : 0, L.imeta + 2 * 4, L.kw};
   for (int i = 0; i < FIODE_ODETRAIN_NSAVED; ++i) offsets[i] = (int64_t)o[i];
   return FIODE_OK;
 }
@@ -1843,7 +1879,8 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   // draws the dropout keep words when dropout is on
   const OtLayout L = ot_layout(a.B, a.E, a.A);
   a.nslots = (int)((L.kw - L.xs) / 8);
-  const int nthreads = a.nslots > a.E * a.B ? a.nslots : a.E * a.B;
+  a.kw_lazy = a.method == FIODE_ODE_DOPRI5 && a.dropout_mode == FIODE_DROPOUT_PHILOX && a.bit_mode;
+  const int nthreads = (a.kw_lazy || a.nslots > a.E * a.B) ? a.nslots : a.E * a.B;
   hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if (a.method == FIODE_ODE_DOPRI5) {

@@ -62,6 +62,7 @@ FIODE_ODE_RK4, FIODE_ODE_DOPRI5 = 0, 1
 FIODE_DTYPE_F32, FIODE_DTYPE_C64 = 0, 1
 FIODE_INV_MAX_N = 128
 FIODE_ODE_MAX_BATCH = 4096          # fiode_odetrain_*
+FIODE_ODETRAIN_MAX_ATTEMPTS = 1024  # fiode_odetrain_config.max_attempts
 FIODE_ODEINT_MAX_BATCH = 65536      # fiode_odeint (tile-parallel eval-mode solve)
 FIODE_SMALL_CAYLEY_MAX_K, FIODE_SMALL_CAYLEY_MAX_RK = 16, 8192
 
@@ -81,12 +82,20 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
-ABI_VERSION = 2            # FIODE_ABI_VERSION (include/fiode.h)
-FIODE_ODETRAIN_NSAVED = 12  # entries fiode_odetrain_saved_offsets writes
+ABI_VERSION = 3            # FIODE_ABI_VERSION (include/fiode.h)
+FIODE_ODETRAIN_NSAVED = 14  # entries fiode_odetrain_saved_offsets writes
+FIODE_GUARD_MAX_STATUS = 4
+
+
+class StepGuard(ct.Structure):
+    """fiode_step_guard: device pointers (nullable) whose values decide whether a step is applied."""
+    _fields_ = [("flag", ct.c_void_p), ("loss", ct.c_void_p), ("status", ct.c_void_p * FIODE_GUARD_MAX_STATUS),
+                ("skipped", ct.c_void_p)]
 
 
 class AdamConfig(ct.Structure):
-    _fields_ = [("n_tensors", ct.c_int32), ("decoupled", ct.c_int32), ("maximize", ct.c_int32), ("pad_", ct.c_int32),
+    _fields_ = [("n_tensors", ct.c_int32), ("decoupled", ct.c_int32), ("maximize", ct.c_int32),
+                ("increment_steps", ct.c_int32),
                 ("lr", ct.c_double), ("beta1", ct.c_double), ("beta2", ct.c_double), ("eps", ct.c_double),
                 ("weight_decay", ct.c_double), ("step", ct.c_double), ("lr_dev", ct.c_void_p),
                 ("lr_dev_is_double", ct.c_int32), ("pad2_", ct.c_int32)]
@@ -175,7 +184,9 @@ def _load():
                                                      ct.c_size_t]),
         "fiode_spectral_cayley_backward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp, _vp,
                                                       _vp, ct.c_size_t]),
-        "fiode_adam_step": (ct.c_int, [_vp, ct.POINTER(AdamConfig), _vp, _vp, _vp, _vp, _vp, _vp]),
+        "fiode_adam_step": (ct.c_int, [_vp, ct.POINTER(AdamConfig), _vp, _vp, _vp, _vp, _vp, _vp,
+                                       ct.POINTER(StepGuard)]),
+        "fiode_step_guard_flag": (ct.c_int, [_vp, ct.POINTER(StepGuard), _vp]),
         "fiode_error_string": (ct.c_char_p, [ct.c_int]),
         "fiode_abi_version": (ct.c_int, []),
     }

@@ -83,7 +83,12 @@ class GradAllReducer:
             raise ValueError(f"GradAllReducer: mixed parameter dtypes {dtypes}")
         self.group = group
         self.numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(self.numel, dtype=self.params[0].dtype, device=dev)
+        # one float past the gradients: the step-guard slot (this rank's skip verdict, written just
+        # before the last bucket's all-reduce; summed with the gradients, so any rank's bad step --
+        # failed solve, non-finite loss -- makes every rank skip the optimizer step together)
+        self.flat = torch.zeros(self.numel + 1, dtype=self.params[0].dtype, device=dev)
+        self.guard_slot = self.flat[self.numel:]
+        self.guard_writer = None          # callable(slot): launches the verdict kernel, or None
         self._hooks = []
         self._armed = None
         self._order_log = None
@@ -110,7 +115,7 @@ class GradAllReducer:
         lo_i = 0
         for c in cuts:
             lo = starts[lo_i]
-            hi = starts[c] if c < len(order) else self.numel
+            hi = starts[c] if c < len(order) else self.numel + 1     # the last bucket carries the slot
             self.buckets.append((lo, hi))
             self.members.append([pos[id(p)] for p in order[lo_i:c]])
             lo_i = c
@@ -176,16 +181,18 @@ class GradAllReducer:
             if p.grad is None:
                 v.zero_()
             p.grad = v
-        return self.flat
+        return self.flat[:self.numel]
 
     def allreduce(self, world: Optional[int] = None, force: bool = False):
         world = dist.get_world_size(self.group) if world is None else world
         if world > 1 or force:
             self.rebind()
+            if self.guard_writer is not None:
+                self.guard_writer(self.guard_slot)
             for lo, hi in self.buckets:
                 dist.all_reduce(self.flat[lo:hi], group=self.group)
             self.flat.div_(world)
-        return self.flat
+        return self.flat[:self.numel]
 
     def arm(self, world: int, stream: torch.cuda.Stream, force: bool = False):
         """Overlapped all-reduce of the next backward (see the class docstring).  The backward must
@@ -230,6 +237,10 @@ class GradAllReducer:
                 self.params[i].grad = v
             if pairs:
                 torch._foreach_copy_([v for v, _ in pairs], [g for _, g in pairs])
+            if k == len(self.buckets) - 1 and self.guard_writer is not None:
+                # the last bucket's gradients are final, so everything upstream of them (the loss,
+                # the train_ode solve forward and backward) has run: its verdict is final too
+                self.guard_writer(self.guard_slot)
             lo, hi = self.buckets[k]
             if st["world"] > 1 or st["force"]:
                 dist.all_reduce(self.flat[lo:hi], group=self.group)
@@ -247,9 +258,10 @@ class GradAllReducer:
         if st["world"] > 1 or st["force"]:
             self.flat.div_(st["world"])
         self._armed = None
-        return self.flat
+        return self.flat[:self.numel]
 
     def grads_in_param_order(self) -> torch.Tensor:
+        """The gradients (not the guard slot) in ``params`` order."""
         return torch.cat([v.reshape(-1) for v in self.views])
 
 

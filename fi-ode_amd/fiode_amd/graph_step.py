@@ -20,6 +20,13 @@ dynamics, the head and the 4096 -> 512 CayleyLinear) overlap the rest of the bac
 stack) -- DDP's bucketed overlap (sl_pipeline.py:157-170), one replay per step.  Over gloo
 (comm "eager": not capturable) the bucket all-reduces run between two replays.
 
+Step guard: the optimizer kernel (FiodeAdam) skips the update on the device -- p, m, v and the
+step counts untouched, one more in the sticky ``skipped`` word -- when this step's train_ode solve
+failed (its status words: attempt capacity exhausted, an exchange timed out) or its loss is not
+finite; on N ranks each rank's verdict rides in the all-reduced gradient bucket's guard slot, so
+all ranks skip together.  ``check_status()`` (every ``check_every`` replays and on demand) raises
+once a step was skipped.  (torch.amp's found_inf skip, without a host sync.)
+
 Static inputs: ``step(x, y)`` copies the batch into the captured input buffers.  What the
 captured step bakes in (and ``GraphTrainStep`` checks on every call): the sampler plan of the
 current epoch (S1/S2 split, ``scale_nominal``), kappa (needs ``global_step >= kappa_length``),
@@ -35,7 +42,8 @@ import torch
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
-                 comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False):
+                 comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False,
+                 guard: bool = True):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
@@ -63,6 +71,8 @@ class GraphTrainStep:
         if module.rng_counter is None:
             module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.params = [p for p in module.parameters() if p.requires_grad]
+        self.skipped = torch.zeros(1, dtype=torch.int32, device=dev)     # sticky count of guarded skips
+        self._guard_ok = guard and hasattr(optimizer, "guard")          # FiodeAdam / FiodeAdamW
         # Grads are set to None before every backward, so autograd hands its result tensors over
         # (no zero fills, no per-parameter accumulate adds); inside the graph they come from the
         # graph's private pool at fixed addresses.  N ranks: one multi-tensor copy then moves them
@@ -89,6 +99,7 @@ class GraphTrainStep:
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         self._restore(snap)
+        self.skipped.zero_()
         torch.cuda.synchronize(dev)
 
         self.single = world == 1 and not self.force_comm
@@ -224,6 +235,7 @@ class GraphTrainStep:
         if overlap:
             self.reducer.arm(self.world, self.comm_stream, force=self.force_comm)
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
+        self._arm_guard(loss)
         loss.backward()
         if overlap:
             self.reducer.finish()                 # the last buckets, join the comm stream, 1/world
@@ -231,6 +243,24 @@ class GraphTrainStep:
             self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)
         return loss
+
+    def _arm_guard(self, loss):
+        """Point the optimizer's step guard at this step's loss and solve status words (they are new
+        tensors in every eager iteration; fixed graph-pool tensors inside the capture)."""
+        if not self._guard_ok:
+            return
+        from .optim import StepGuard
+        status = self.module.status_words() if hasattr(self.module, "status_words") else []
+        lo = loss.detach().reshape(1)
+        mine = StepGuard(loss=lo if lo.dtype == torch.float32 else None, status=status)
+        if self.comm != "none":
+            # N ranks: this rank's verdict goes into the bucket's guard slot (written right before
+            # the last bucket's all-reduce); the optimizer reads the summed slot
+            self.reducer.guard_writer = mine.write_flag
+            self.opt.guard = StepGuard(flag=self.reducer.guard_slot, skipped=self.skipped)
+        else:
+            mine.skipped = self.skipped
+            self.opt.guard = mine
 
     def _between(self, warmup: bool = True):
         # eager collectives: every warm-up iteration (the captured step has none of its own when
@@ -261,8 +291,19 @@ class GraphTrainStep:
             self.check_status()
         return self.loss
 
+    def skipped_steps(self) -> int:
+        """Replayed steps whose optimizer update the guard skipped (one host read)."""
+        return int(self.skipped.item())
+
     def check_status(self) -> None:
-        """Raise if a persistent solve of the replayed step timed out on a cross-workgroup exchange
-        (sticky device status; one host read, every ``check_every`` replays and on demand)."""
+        """Raise if a replayed step was skipped by the guard (a failed train_ode solve or a
+        non-finite loss, on any rank) or the last solve reports a failure (one or two host reads,
+        every ``check_every`` replays and on demand)."""
+        n = self.skipped_steps()
+        if n:
+            st = self.module.device_status() if hasattr(self.module, "device_status") else 0
+            raise RuntimeError(f"{n} training step(s) skipped by the step guard (failed train_ode solve or "
+                               f"non-finite loss; last solve status {st}): parameters and optimizer state "
+                               "are those of the last good step")
         if hasattr(self.module, "check_device_status"):
             self.module.check_device_status()

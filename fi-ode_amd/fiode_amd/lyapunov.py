@@ -65,6 +65,7 @@ class ODETrainFn(torch.autograd.Function):
         y, stats, ws = ops.odetrain_forward(xf, h0.detach().float().contiguous(), w, plan["dyn"], plan["cfg"],
                                             masks=plan.get("masks"), offset_dev=plan.get("offset_dev"))
         plan["stats"] = stats
+        plan["status_word"] = ops.odetrain_status_word(ws, plan["cfg"])
         ctx.plan, ctx.w, ctx.xf, ctx.ws = plan, w, xf, ws
         from . import cayley as _cy
         ctx.step_stream = _cy.STEP_STREAM
@@ -178,6 +179,7 @@ class LyapODELossFn(torch.autograd.Function):
             res = pre[0]
         y_hat, stats, ws = res
         oplan["stats"] = stats
+        oplan["status_word"] = ops.odetrain_status_word(ws, oplan["cfg"])
         B = y_hat.shape[0]
         total = torch.empty((), dtype=torch.float32, device=y_hat.device)
         loss_ode = torch.empty((), dtype=torch.float32, device=y_hat.device)
@@ -516,26 +518,35 @@ class LyapunovLearning(nn.Module):
             return self._ode_loss(loss, y_hat, y)
         return loss
 
-    def device_status(self) -> int:
-        """Sticky status of the last train_ode solve (fiode_odetrain_forward stats[3]): 0 ok, 4 = a
-        workgroup's QP-exit exchange timed out (its rows of y_hat were poisoned with NaN).  One host
-        read: call it every few hundred steps or at the epoch end, not per step."""
+    def status_words(self) -> list:
+        """Device int32 [1] status words of the last train_ode solve (forward stats[3]; the dopri5
+        solve's forward + backward word): what a step guard reads (optim.StepGuard)."""
         plan = getattr(self, "last_ode_plan", None)
-        st = plan.get("stats") if plan else None
-        return int(st[3]) if st is not None else 0
+        if not plan or not (self.train_ode and self.current_epoch > self.train_ode_epoch):
+            return []
+        return [t for t in (plan["stats"][3:4] if plan.get("stats") is not None else None,
+                            plan.get("status_word")) if t is not None]
+
+    def device_status(self) -> int:
+        """Status of the last train_ode solve: 0 ok, 2 = the dopri5 attempt capacity was exhausted,
+        3 = dt underflow, 4 = a workgroup's cross-workgroup exchange timed out (its outputs were
+        poisoned with NaN).  One host read: call it every few hundred steps or at the epoch end."""
+        return max([int(t[0]) for t in self.status_words()] or [0])
 
     def check_device_status(self) -> None:
         status = self.device_status()
         if status:
-            raise RuntimeError(f"train_ode solve: cross-workgroup QP-exit exchange timed out (status {status}); "
-                               "the step's loss is NaN")
+            what = {2: "the dopri5 attempt capacity (train_ode_max_attempts) was exhausted",
+                    3: "dt underflow"}.get(status, "a cross-workgroup exchange timed out")
+            raise RuntimeError(f"train_ode solve failed (status {status}: {what}); the step's loss is NaN")
 
     def ode_plan(self, batch: int, masks: Optional[torch.Tensor] = None) -> dict:
         """Solver plan of the train_ode solve (make_solver_params(train_ode_solver, train_ode_tol),
         pl_modules.py:24-35): 'rk4' with options.step_size = tol, or 'dopri5' with rtol = atol = tol
-        (cifar_train.yaml:30,32), at most ``train_ode_max_attempts`` adaptive step attempts (the eval
-        capacity of the device solve; torchdiffeq has no cap -- more attempts report status 2 and a
-        NaN loss, see check_device_status)."""
+        (cifar_train.yaml:30,32), at most ``ode_attempt_capacity(batch)`` adaptive step attempts (the eval
+        capacity of the device solve: ``train_ode_max_attempts`` or what 4 GiB of workspace holds;
+        torchdiffeq has no cap -- more attempts report status 2 and a NaN loss, which the step guard
+        keeps away from the parameters; see check_device_status)."""
         if self.use_adjoint:
             raise NotImplementedError("odeint_adjoint (SURVEY.md section 8f row 3)")
         if self.train_ode_solver not in ("rk4", "dopri5"):
@@ -552,8 +563,19 @@ class LyapunovLearning(nn.Module):
         else:
             cfg = ops.odetrain_config(batch, 0.0, float(self.t_max), 0.0, mode, seed=self.seed, offset=off,
                                       method="dopri5", rtol=float(sp["rtol"]), atol=float(sp["atol"]),
-                                      max_attempts=int(getattr(self, "train_ode_max_attempts", 64)))
+                                      max_attempts=self.ode_attempt_capacity(batch))
         return dict(dyn=self.dyn_fun.dyn_cfg(), cfg=cfg, masks=masks, offset_dev=self.rng_counter)
+
+    def ode_attempt_capacity(self, batch: int) -> int:
+        """``train_ode_max_attempts`` if set, else the capacity 4 GiB of workspace holds
+        (ops.odetrain_default_attempts; cached per batch size)."""
+        cap = getattr(self, "train_ode_max_attempts", None)
+        if cap:
+            return int(cap)
+        cache = self.__dict__.setdefault("_attempt_cap", {})
+        if batch not in cache:
+            cache[batch] = ops.odetrain_default_attempts(batch)
+        return cache[batch]
 
     def _ode_launch(self, static_state, w, masks=None):
         """The train_ode solve (pl_modules.py:490-493).  The reference re-runs the backbone inside

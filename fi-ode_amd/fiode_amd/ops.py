@@ -280,6 +280,24 @@ def odetrain_config(B: int, t0: float, t1: float, step_size: float, dropout_mode
                             float(t0), float(t1), float(step_size), m, int(max_attempts), float(rtol), float(atol))
 
 
+ODETRAIN_ATTEMPT_BUDGET = 4 << 30       # bytes of dopri5 workspace the default attempt capacity may use
+
+
+def odetrain_default_attempts(B: int, budget_bytes: int = ODETRAIN_ATTEMPT_BUDGET) -> int:
+    """Attempt capacity of the differentiable dopri5 solve when the caller sets none: as many
+    attempts as ``budget_bytes`` of workspace hold (each attempt saves 6 evals' stage inputs,
+    activations and QP state for the backward), capped at FIODE_ODETRAIN_MAX_ATTEMPTS.  torchdiffeq's
+    loop is uncapped (max_num_steps 2**31 - 1); exhausting the capacity is status 2 (stated
+    deviation).  At B = 128 this is the maximum, 1,024 attempts (~1.9 GB); at
+    B = 1,024, ~280 (configs[4]'s solve takes ~35)."""
+    lib = L.lib()
+    w = [lib.fiode_odetrain_workspace_bytes(ct.byref(odetrain_config(B, 0.0, 1.0, 0.0, L.FIODE_DROPOUT_OFF,
+                                                                      method="dopri5", max_attempts=a)))
+         for a in (1, 2)]
+    per = max(1, w[1] - w[0])
+    return int(max(64, min(L.FIODE_ODETRAIN_MAX_ATTEMPTS, (budget_bytes - w[0]) // per + 1)))
+
+
 def odetrain_evals(cfg: L.OdeTrainConfig) -> int:
     E = L.lib().fiode_odetrain_evals(ct.byref(cfg))
     if E < 0:
@@ -330,13 +348,24 @@ def odetrain_saved(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> Dict[str, torch.T
     R = B * E
     out = dict(h=f(0, R * C).view(B, E, C), ftilde=f(1, R * C).view(B, E, C), v=f(2, R * C).view(B, E, C),
                mu=f(3, R).view(B, E), nominal=f(4, R * C).view(B, E, C), a1=f(5, R * M).view(B, E, M),
-               a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C), lower=f(8, R * C).view(B, E, C))
+               a2=f(6, R * M).view(B, E, M), gft=f(7, R * C).view(B, E, C), lower=f(8, R * C).view(B, E, C),
+               status=ws[off[12]:off[12] + 4].view(torch.int32),
+               keep_words=ws[off[13]:off[13] + E * 2 * B * 16].view(torch.int32).view(E, 2, B, 4))
     if cfg.method == L.FIODE_ODE_DOPRI5:
         A = int(cfg.max_attempts)
         out["ys"] = f(9, A * B * C).view(A, B, C)
         out["attempts"] = ws[off[10]:off[10] + 8 * 8 * A].view(torch.float64).view(A, 8)
         out["init"] = ws[off[11]:off[11] + 8 * 16].view(torch.float64)
     return out
+
+
+def odetrain_status_word(ws: torch.Tensor, cfg: L.OdeTrainConfig) -> torch.Tensor:
+    """int32 [1] view of the solve's status word in an odetrain workspace (saved entry 12: dopri5
+    forward + backward status, 0 ok; rk4 keeps it 0 -- its forward status is stats[3])."""
+    off = (ct.c_int64 * L.FIODE_ODETRAIN_NSAVED)()
+    L.check(L.lib().fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(off, ct.c_void_p)),
+            "fiode_odetrain_saved_offsets")
+    return ws[off[12]:off[12] + 4].view(torch.int32)
 
 
 def odetrain_backward(g_y: torch.Tensor, x_feat: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,

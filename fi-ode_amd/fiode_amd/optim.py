@@ -13,6 +13,12 @@ lr is a launch argument, baked into a captured graph (GraphTrainStep refuses to 
 changed).  Groups the kernel does not cover (CPU or non-float32 parameters, amsgrad,
 differentiable, more than FIODE_ADAM_MAX_TENSORS tensors, a tensor lr off the parameters' device)
 go through torch's own Adam.step unchanged.
+
+Step guard (``opt.guard = StepGuard(...)``): the kernel reads, on the device, whether this step
+may touch the parameters -- the train_ode solve's status words, the loss's finiteness, or (N
+ranks) the guard slot of the all-reduced gradient bucket -- and otherwise leaves p, m, v and the
+device step counts as they were, counting the skipped step in a sticky device word (torch.amp's
+found_inf skip, decided without a host sync; GraphTrainStep arms it).
 """
 from __future__ import annotations
 
@@ -69,8 +75,38 @@ def _kernel_ok_params(opt, params: List[torch.Tensor]) -> bool:
     return not ids
 
 
+class StepGuard:
+    """Device-side skip condition of an optimizer step (include/fiode.h fiode_step_guard): skip when
+    ``flag`` (float32 [1]) is nonzero or NaN, ``loss`` is not finite, or any ``status`` word (int32
+    [1]) is nonzero; ``skipped`` (int32 [1]) counts the skipped steps.  Keeps the tensors alive."""
+
+    def __init__(self, flag=None, loss=None, status=(), skipped=None):
+        status = [t for t in status if t is not None]
+        if len(status) > L.FIODE_GUARD_MAX_STATUS:
+            raise ValueError(f"at most {L.FIODE_GUARD_MAX_STATUS} status words")
+        for t, dt in [(flag, torch.float32), (loss, torch.float32), (skipped, torch.int32)] + \
+                [(t, torch.int32) for t in status]:
+            if t is not None and (t.dtype != dt or not t.is_cuda or t.numel() < 1):
+                raise ValueError(f"StepGuard: expected a {dt} device tensor, got {t.dtype} on {t.device}")
+        self.flag, self.loss, self.status, self.skipped = flag, loss, status, skipped
+
+    def to_c(self, count: bool = True) -> "L.StepGuard":
+        ptr = lambda t: None if t is None else t.data_ptr()
+        st = (ct.c_void_p * L.FIODE_GUARD_MAX_STATUS)(*([t.data_ptr() for t in self.status] +
+                                                         [None] * (L.FIODE_GUARD_MAX_STATUS - len(self.status))))
+        return L.StepGuard(ptr(self.flag), ptr(self.loss), st, ptr(self.skipped) if count else None)
+
+    def write_flag(self, out: torch.Tensor) -> None:
+        """out[0] = 1.0 if this rank's loss / status words say skip, else 0.0 (fiode_step_guard_flag),
+        on the current stream -- the value that goes into the all-reduced guard slot."""
+        g = self.to_c(count=False)
+        L.check(L.lib().fiode_step_guard_flag(_stream(out.device), ct.byref(g), out.data_ptr()),
+                "fiode_step_guard_flag")
+
+
 class _KernelStepMixin:
     _decoupled = False
+    guard = None          # StepGuard or None
 
     def _done_set(self) -> set:
         d = self.__dict__.get("_fiode_done")
@@ -99,7 +135,7 @@ class _KernelStepMixin:
                     raise RuntimeError("FiodeAdam.step_params: parameters not covered by the kernel")
                 pw, grads, m, v, mx, steps = [], [], [], [], [], []
                 self._init_group({**group, "params": params}, pw, grads, m, v, mx, steps)
-                if not self._launch(group, pw, grads, m, v, steps):
+                if not self._launch(group, pw, grads, m, v, steps, count_skip=False):
                     raise RuntimeError("FiodeAdam.step_params: the parameters' step counts differ")
             finally:
                 for (p, _), g0 in zip(sel, saved):
@@ -113,6 +149,7 @@ class _KernelStepMixin:
             with torch.enable_grad():
                 loss = closure()
         fallback = []
+        counted = False
         done = self._done_set()
         for group in self.param_groups:
             params = [p for p in group["params"] if p.grad is not None and id(p) not in done]
@@ -125,7 +162,9 @@ class _KernelStepMixin:
                 continue
             pw, grads, m, v, mx, steps = [], [], [], [], [], []
             self._init_group({**group, "params": params}, pw, grads, m, v, mx, steps)   # torch's lazy state creation
-            if not self._launch(group, pw, grads, m, v, steps):
+            if self._launch(group, pw, grads, m, v, steps, count_skip=not counted):
+                counted = True              # a skipped step is counted once, not once per group
+            else:
                 if done:
                     raise RuntimeError("FiodeAdam: host step counts after step_params are not supported")
                 fallback.append(group)
@@ -139,13 +178,15 @@ class _KernelStepMixin:
                 self.param_groups = kept
         return loss
 
-    def _launch(self, group, pw, grads, m, v, steps) -> bool:
+    def _launch(self, group, pw, grads, m, v, steps, count_skip: bool = True) -> bool:
         """The kernel update of one group's tensors; False (nothing done) when the host step counts
-        cannot take it (mixed placement or counts: torch's path)."""
+        cannot take it (mixed placement or counts: torch's path).  Device step counts are
+        incremented by the library (guarded: a skipped step leaves them)."""
         n = len(pw)
         on_dev = [s.device.type == "cuda" for s in steps]
         if all(on_dev):
-            torch._foreach_add_(steps, 1)
+            if any(s.dtype != torch.float32 for s in steps):
+                return False
             host_step = 0.0
         else:
             if torch.cuda.is_current_stream_capturing():
@@ -160,17 +201,19 @@ class _KernelStepMixin:
         lr = group["lr"]
         lr_t = lr if torch.is_tensor(lr) else None
         cfg = L.AdamConfig(n, int(bool(group.get("decoupled_weight_decay", self._decoupled))),
-                           int(group["maximize"]), 0, 0.0 if lr_t is not None else float(lr), float(beta1),
+                           int(group["maximize"]), int(all(on_dev)), 0.0 if lr_t is not None else float(lr),
+                           float(beta1),
                            float(beta2), float(group["eps"]), float(group["weight_decay"]), host_step,
                            lr_t.data_ptr() if lr_t is not None else None,
                            int(lr_t is not None and lr_t.dtype == torch.float64), 0)
         arr = ct.c_void_p * n
         step_ptrs = arr(*[s.data_ptr() for s in steps]) if all(on_dev) else None
+        guard = self.guard.to_c(count=count_skip) if self.guard is not None else None
         L.check(L.lib().fiode_adam_step(
             _stream(pw[0].device), ct.byref(cfg), arr(*[t.data_ptr() for t in pw]),
             arr(*[t.data_ptr() for t in grads]), arr(*[t.data_ptr() for t in m]),
-            arr(*[t.data_ptr() for t in v]), (ct.c_int64 * n)(*[t.numel() for t in pw]), step_ptrs),
-            "fiode_adam_step")
+            arr(*[t.data_ptr() for t in v]), (ct.c_int64 * n)(*[t.numel() for t in pw]), step_ptrs,
+            ct.byref(guard) if guard is not None else None), "fiode_adam_step")
         return True
 
 

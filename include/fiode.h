@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FIODE_ABI_VERSION 2
+#define FIODE_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define FIODE_API __attribute__((visibility("default")))
@@ -226,8 +226,11 @@ FIODE_API int fiode_odetrain_forward(void* stream, const fiode_odetrain_config* 
  * [B][E][M], [7] dL/d mlp output [B][E][C] (after the backward), [8] QP lower bound [B][E][C];
  * dopri5 only (else 0): [9] y_n of every attempt [A][B][C] float, [10] the attempt log [A][8]
  * double (t_n, dt_n, error ratio, accepted, eval of k_0, eval of stage 0), [11] the initial step
- * [16] double (d0, d1, d2, h0, h1, clamp0, clamp1, dt0, rms(f1 - f0)).  Row (b, e) = b*E + e. */
-#define FIODE_ODETRAIN_NSAVED 12
+ * [16] double (d0, d1, d2, h0, h1, clamp0, clamp1, dt0, rms(f1 - f0)), [12] the solve's int32
+ * status word (rk4: always 0, its status is stats[3]; dopri5: 0 ok; 2 attempt capacity exhausted; 3 dt underflow; 4 a cross-workgroup exchange of
+ * the forward or the backward timed out -- the outputs are NaN then), [13] the dropout keep words uint32 [E][2][B][4] (bit t of word q =
+ * keep hidden unit 32 q + t; the evals the solve made).  Row (b, e) = b*E + e. */
+#define FIODE_ODETRAIN_NSAVED 14
 FIODE_API int fiode_odetrain_saved_offsets(const fiode_odetrain_config* cfg, int64_t* offsets);
 /* Given g_y = dL/dy(t1) [B][C]: all weight gradients and dL/dx_feat (overwritten).  Must follow
  * fiode_odetrain_forward on the same workspace.  dbg_gft: optional [B][E][C] dL/d mlp output. */
@@ -407,17 +410,38 @@ FIODE_API int fiode_spectral_cayley_backward(void* stream, const fiode_spectral_
 /* ---- optimizer step (pl_modules.py:97-147 configure_optimizers -> torch.optim.Adam / AdamW;
  * fiode_amd/optim.py FiodeAdam): one launch updates every parameter tensor (adam.hip).  The host
  * arrays hold n_tensors device pointers each; tensors are contiguous float32 of numel[i] elements.
- * step: host array of device pointers to each tensor's step count after this step's increment
- * (capturable Adam; an entry or the array may be NULL: cfg->step is used).  lr_dev (may be NULL):
+ * step: host array of device pointers to each tensor's step count (capturable Adam; an entry or
+ * the array may be NULL: cfg->step is used), incremented by this call when cfg->increment_steps
+ * (one small kernel ahead of the update, skipped with it), else already incremented by the caller.
+ * guard (nullable): see fiode_step_guard.  lr_dev (may be NULL):
  * a device scalar holding the learning rate (torch's tensor lr, which LR schedulers update in
  * place; float32, or float64 when lr_dev_is_double): read by the kernel at run time, so a captured
  * step follows schedule changes; else cfg->lr (a value baked into a captured launch). */
 #define FIODE_ADAM_MAX_TENSORS 64
+/* Step guard (AMP's found_inf, without a host sync): a training step whose solve failed or whose
+ * loss is not finite must not reach the parameters.  Every non-NULL source is read on the device:
+ *   flag      nonzero or NaN = skip (e.g. the guard slot of the all-reduced gradient bucket, where
+ *             fiode_step_guard_flag wrote this rank's verdict: any rank's bad step skips on all);
+ *   loss      non-finite = skip;
+ *   status[i] nonzero = skip (solve status words: fiode_odetrain_forward stats[3], saved [12]).
+ * A skipped update leaves p, m, v and the step counts untouched; `skipped` (nullable) counts the
+ * skipped steps (sticky, for the host to read now and then). */
+#define FIODE_GUARD_MAX_STATUS 4
+typedef struct fiode_step_guard {
+  const float* flag;
+  const float* loss;
+  const int32_t* status[FIODE_GUARD_MAX_STATUS];
+  int32_t* skipped;
+} fiode_step_guard;
+/* flag_out[0] = 1 if the guard's sources (loss, status words; `flag` ignored) say skip, else 0. */
+FIODE_API int fiode_step_guard_flag(void* stream, const fiode_step_guard* guard, float* flag_out);
+
 typedef struct fiode_adam_config {
   int32_t n_tensors;
   int32_t decoupled;     /* AdamW: p -= lr wd p before the moments (else g += wd p)             */
   int32_t maximize;
-  int32_t pad_;
+  int32_t increment_steps;  /* 1: the device step counts are incremented here (guarded), before
+                               the update reads them; 0: the caller already incremented them   */
   /* hyper-parameters as the host holds them (Python floats): 1 - beta, the bias corrections and
    * lr / (1 - beta1^t) are formed in double, then rounded to the fp32 the update runs in */
   double lr, beta1, beta2, eps, weight_decay;
@@ -428,7 +452,7 @@ typedef struct fiode_adam_config {
 } fiode_adam_config;
 FIODE_API int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float* const* params,
                               const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
-                              const int64_t* numel, const float* const* step);
+                              const int64_t* numel, float* const* step, const fiode_step_guard* guard);
 
 FIODE_API const char* fiode_error_string(int code);
 FIODE_API int fiode_abi_version(void);

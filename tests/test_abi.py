@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from fiode_amd import _lib
     lib = _lib.lib()
-    assert lib.fiode_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.fiode_abi_version() == _lib.ABI_VERSION == 3
     hdr = (pathlib.Path(__file__).resolve().parents[1] / "include" / "fiode.h").read_text()
     for name in ("FIODE_ABI_VERSION", "FIODE_ODETRAIN_NSAVED"):
         val = int(re.search(r"#define %s (\d+)" % name, hdr).group(1))
@@ -121,12 +121,18 @@ def test_adam_step_host_checks():
     cfg = L.AdamConfig(2, 0, 0, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0)
     arr = ct.c_void_p * 2
     one = arr(1, 2)
-    assert lib.fiode_adam_step(None, ct.byref(cfg), one, one, one, one, (ct.c_int64 * 2)(5, -1), None) == 1
-    assert lib.fiode_adam_step(None, ct.byref(cfg), arr(1, None), one, one, one, (ct.c_int64 * 2)(5, 3), None) == 1
+    assert lib.fiode_adam_step(None, ct.byref(cfg), one, one, one, one, (ct.c_int64 * 2)(5, -1), None, None) == 1
+    assert lib.fiode_adam_step(None, ct.byref(cfg), arr(1, None), one, one, one, (ct.c_int64 * 2)(5, 3), None, None) == 1
     cfg.n_tensors = 65
-    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None) == 1
+    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None, None) == 1
     cfg.n_tensors = 0
-    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None) == 0
+    assert lib.fiode_adam_step(None, ct.byref(cfg), None, None, None, None, None, None, None) == 0
+    # the library increments the step counts only through a step-pointer table
+    cfg.n_tensors, cfg.increment_steps = 2, 1
+    assert lib.fiode_adam_step(None, ct.byref(cfg), one, one, one, one, (ct.c_int64 * 2)(5, 3), None, None) == 1
+    g = L.StepGuard()
+    assert lib.fiode_step_guard_flag(None, None, None) == 1
+    assert lib.fiode_step_guard_flag(None, ct.byref(g), None) == 1
 
 
 def test_fiode_adam_cpu_params_use_torch_step():

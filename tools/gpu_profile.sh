@@ -14,7 +14,7 @@ timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo
 cat $O/bench.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
-    python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $O/trace.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
+    python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-configs > $O/trace.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
 timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 PMC_MFMA=""
 for C in SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE; do
@@ -25,6 +25,6 @@ for PASS in FETCH_SIZE WRITE_SIZE MFMA; do
   if [ "$PASS" = MFMA ]; then CS="$PMC_MFMA"; else CS="$PASS"; fi
   [ -z "$CS" ] && continue
   timeout -s KILL 120 rocprofv3 --pmc $CS --output-format csv -d $O/pmc_$PASS -o run -- \
-      python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --prof-reps 2 > $O/pmc_$PASS.log 2>&1 || { echo "pmc $PASS failed rc=$?"; exit 1; }
+      python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --no-configs --prof-reps 2 > $O/pmc_$PASS.log 2>&1 || { echo "pmc $PASS failed rc=$?"; exit 1; }
 done
 echo done
