@@ -152,11 +152,14 @@ __device__ __forceinline__ void and_by_batch(const CertArgs& a, int batch, bool 
   }
 }
 
-__global__ __launch_bounds__(256) void k_cert_fwd(CertArgs a) {
+// Two workgroups per CU (LDS: the Q2 image + Q3's C rows, 72.9 KB each; <= 256 registers): the
+// two waves of a SIMD run many tiles each and drift apart, so one wave's QP / barrier VALU work
+// overlaps the other's MFMAs (one resident workgroup per CU left the matrix pipe idle during them).
+__global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
-  load_weight_images(a.Q2, a.Q3, Q2s, Q3s);
+  load_weight_images(a.Q2, a.Q3, Q2s, Q3s, C);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];
@@ -335,8 +338,13 @@ extern "C" int fiode_certify(void* stream, const fiode_certify_config* cfg, cons
   FIODE_HIP_CHECK(hipGetLastError());
   const uint32_t ntiles = (a.G + 31) / 32;
   uint32_t blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(k_cert_fwd, dim3(blocks), dim3(256), (size_t)(M + 32) * LDQ * sizeof(float), st, a);
+  // persistent: two workgroups per CU, each loading the weight images once
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 256;
+  const uint32_t cap = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(k_cert_fwd, dim3(blocks), dim3(256), (size_t)(M + C) * LDQ * sizeof(float), st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_cert_final, dim3((a.G + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());

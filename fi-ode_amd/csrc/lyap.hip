@@ -229,7 +229,10 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
 // (LDS 72.9 KB each, <= 256 registers): one wave's QP (VALU) overlaps another's MFMA on every
 // SIMD.  Per wave: layers 1-3, ft -> HBM, the QP to max_iter - 1 for its convergence bits, AND-ed
 // per pass into one word (the batch-global exit, barrier_projection.py:247-249).
-__global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
+#ifndef FWD_WAVES
+#define FWD_WAVES 4           // waves per workgroup: FWD_WAVES / 2 tiles x 2 passes
+#endif
+__global__ __launch_bounds__(64 * FWD_WAVES, 8 / FWD_WAVES) void k_lyap_fwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   LY_T0();
   LY_COUNT(6);
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void k_lyap_fwd(LyapArgs a) {
     for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
   const int ntiles = (a.N + 31) / 32;
   const int pass = wave & 1;
-  for (int tile = 2 * blockIdx.x + (wave >> 1); tile < ntiles; tile += 2 * gridDim.x) {
+  for (int tile = (FWD_WAVES / 2) * blockIdx.x + (wave >> 1); tile < ntiles; tile += (FWD_WAVES / 2) * gridDim.x) {
     const int row = tile * 32 + col;
     const bool valid = row < a.N;
     const int rr = valid ? row : a.N - 1;
@@ -921,7 +924,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
     return 0;
   };
   const int ntiles = (a.N + 31) / 32;
-  const int fwd_blocks = (ntiles + 1) / 2;                // 2 tiles x 2 passes per workgroup
+  const int fwd_blocks = (ntiles + FWD_WAVES / 2 - 1) / (FWD_WAVES / 2);   // FWD_WAVES / 2 tiles x 2 passes per workgroup
   const size_t lds_fwd = (size_t)(M + C) * LDQ * sizeof(float);
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);
@@ -930,7 +933,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   hipLaunchKernelGGL(k_lyap_prep, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
-  hipLaunchKernelGGL(k_lyap_fwd, dim3(fwd_blocks), dim3(256), lds_fwd, st, a);
+  hipLaunchKernelGGL(k_lyap_fwd, dim3(fwd_blocks), dim3(64 * FWD_WAVES), lds_fwd, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_lyap_bwd, dim3(L.nslab), dim3(256), BWD_LDS, st, a);

@@ -39,11 +39,14 @@ from typing import Optional
 import torch
 
 
+SPLIT_DEFAULT = True          # one rank: the three-graph split step (see GraphTrainStep._split_backbone)
+
+
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
                  comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False,
-                 guard: bool = True):
+                 guard: bool = True, split: Optional[bool] = None):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
@@ -79,6 +82,16 @@ class GraphTrainStep:
         # into the reducer's flat bucket (GradAllReducer.gather) and p.grad points at the bucket
         # views, which the RCCL all-reduce and the optimizer graph use.
         self.persistent = False
+        self.single = world == 1 and not self.force_comm
+        from .optim import _KernelStepMixin
+        if split is None:
+            split = SPLIT_DEFAULT
+        once = getattr(module, "ode_reuse_features", True) or not getattr(module, "train_ode", False)
+        self.split = bool(split and self.single and maps_ahead and once and isinstance(optimizer, _KernelStepMixin)
+                          and self._split_backbone() is not None and getattr(module.dyn_fun, "cayley", False))
+        self.stores, self.d_params, self.split_cap = [], [], {}
+        if self.split:
+            warmup = max(int(warmup), 2)
 
         # Warm-up iterations (lazy optimizer state, library handles, workspaces) run real updates on
         # the constructor's batch; the reference's Lightning loop makes no such updates, so the
@@ -89,6 +102,13 @@ class GraphTrainStep:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for it in range(warmup):
+                if self.split and it == 1:
+                    self._split_on()                # after one plain iteration (input sizes, alphas)
+                if self.split and it >= 1:
+                    self._phase1()
+                    self._phase_d()
+                    self._phase2()
+                    continue
                 if it == 0 and multi:
                     reducer.record_order()          # the order the backward finalises the gradients
                 self._fwd_bwd(bucket_plan=False)
@@ -102,8 +122,10 @@ class GraphTrainStep:
         self.skipped.zero_()
         torch.cuda.synchronize(dev)
 
-        self.single = world == 1 and not self.force_comm
-        if maps_ahead:
+        if self.split:
+            self.refresh_maps()                     # the stores hold maps of the warm-up's parameters
+            torch.cuda.synchronize(dev)
+        elif maps_ahead:
             self._maps_ahead_on()
         self.comm_fallback = None
         try:
@@ -128,6 +150,8 @@ class GraphTrainStep:
         self._float_lrs = [g["lr"] for g in self.opt.param_groups]
 
     def _capture(self):
+        if self.split:
+            return self._capture_split()
         self.one_graph = self.single or self.comm == "graph"
         # capture_error_mode "thread_local": the process group's watchdog thread polls its events
         # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it
@@ -187,12 +211,138 @@ class GraphTrainStep:
         checkpoint or any update outside the replays)."""
         for c in self.piped:
             c.refresh_map()
+        for st in self.stores:
+            st.refresh()
 
     def close(self) -> None:
         """Back to maps computed at the start of each step (eager training of the same module)."""
         for c in self.piped:
             c.pipeline_off()
         self.piped = []
+        if self.split:
+            from .cayley import CayleyLinear
+            for mod in self.module.modules():
+                if isinstance(mod, CayleyLinear):
+                    mod.pipeline_off()
+            if hasattr(self.module.dyn_fun, "pipeline_off"):
+                self.module.dyn_fun.pipeline_off()
+            bb = self._split_backbone()
+            if bb is not None:
+                bb.split_capture = None
+            self.stores = []
+
+    # ---- the split step ----------------------------------------------------------------------
+    # One replay = three graphs.  F1 (stream s0): the forward through the maps computed ahead, the
+    # fused loss, and the backward down to the conv stack's output (a leaf there), the dense /
+    # small maps' outputs Q (leaves: MapStore) and the head / dynamics biases.  Then, concurrently:
+    # D (stream s1): each dense / small Cayley map's backward from dL/dQ, the Adam update of the
+    # head and dynamics parameters, and their maps for the next step (MapStore.refresh); F2 (s0):
+    # the conv stack's backward from dL/d(conv output) with the conv layers' early Adam updates and
+    # next maps (the maps-ahead hooks), then Adam for the rest (conv biases).  The next F1 waits
+    # for both.  Same kernels on the same values as the one-graph step (bit-identical losses and
+    # parameters, tests/test_gpu_graph.py); what changes is that the ~0.3 ms chain of the dense
+    # maps' backward + update + next forward (latency-bound panel inverses, small GEMMs) runs on
+    # its own stream beside the conv backward instead of before / after it on the step's queue.
+    def _split_backbone(self):
+        from .models import KWLargeConcat
+        root = getattr(self.module, "init_coordinates", None)
+        if root is None:
+            return None
+        for mod in root.modules():
+            if isinstance(mod, KWLargeConcat):
+                return mod
+        return None
+
+    def _split_on(self):
+        from .cayley import CayleyConv, CayleyLinear
+        self._maps_ahead_on()
+        if not self.early:
+            raise RuntimeError("split step: the conv layers' early updates are unavailable")
+        bb = self._split_backbone()
+        bb.split_capture = self.split_cap
+        dyn = self.module.dyn_fun
+        stores, d_params = [], []
+        for mod in bb.modules():
+            if isinstance(mod, CayleyLinear):
+                if not mod.pipeline_on():
+                    raise RuntimeError("split step: a CayleyLinear map cannot be stored")
+                stores.append(mod._mstore)
+                d_params += [mod.weight, mod.alpha] + ([mod.bias] if mod.bias is not None else [])
+        dstores = dyn.pipeline_on() if hasattr(dyn, "pipeline_on") else []
+        if not dstores:
+            raise RuntimeError("split step: the dynamics maps cannot be stored")
+        stores += dstores
+        for st in dstores:
+            d_params += st.params if st.params is not None else [st.weight_fn(), st.alpha_fn()]
+        d_params += [lin.bias for lin in (dyn.hidden_to_mlp, dyn.U_x, dyn.mlp_to_mlp, dyn.mlp_to_hidden)
+                     if lin.bias is not None]
+        conv = [p for c in bb.modules() if isinstance(c, CayleyConv) for p in c.parameters()]
+        ids = {id(p) for p in d_params} | {id(p) for p in conv}
+        if len({id(p) for p in d_params}) != len(d_params) or any(id(p) not in ids for p in self.params):
+            raise RuntimeError("split step: parameters outside the conv stack, head and dynamics")
+        self.stores, self.d_params = stores, d_params
+        self.d_biases = [p for p in d_params if not any(p is q for st in stores
+                                                        for q in (st.params or [st.weight_fn(), st.alpha_fn()]))]
+        dev = self.static_x.device
+        self.s0, self.s1 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.ev1, self.ev_d = torch.cuda.Event(), torch.cuda.Event()
+
+    def _phase1(self):
+        m = self.module
+        for p in self.params:
+            p.grad = None
+        for st in self.stores:
+            st.Q.grad = None
+        self.split_cap.clear()
+        loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
+        if "h_leaf" not in self.split_cap:
+            raise RuntimeError("split step: the backbone did not stop at its conv output")
+        self._arm_guard(loss)
+        loss.backward()
+        m.rng_counter.add_(1)
+        return loss
+
+    def _phase_d(self):
+        pairs = []
+        for st in self.stores:
+            pairs += st.param_grads()
+        for b in self.d_biases:
+            pairs.append((b, b.grad if b.grad is not None else torch.zeros_like(b)))
+        self.opt.step_params(pairs)
+        for st in self.stores:
+            st.refresh()
+
+    def _phase2(self):
+        sp = self.split_cap
+        torch.autograd.backward(sp["h_conv"], sp["h_leaf"].grad)
+        self.opt.step()
+
+    def _capture_split(self):
+        self.one_graph = False
+        self.g_fb = self.g_opt = None
+        self.g1, self.gd, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g1, stream=self.s0, capture_error_mode="thread_local"):
+            self.loss = self._phase1()
+        with torch.cuda.graph(self.gd, stream=self.s1, capture_error_mode="thread_local"):
+            self._phase_d()
+        with torch.cuda.graph(self.g2, stream=self.s0, capture_error_mode="thread_local"):
+            self._phase2()
+
+    def _replay_split(self):
+        cur = torch.cuda.current_stream(self.static_x.device)
+        self.s0.wait_stream(cur)
+        with torch.cuda.stream(self.s0):
+            self.s0.wait_event(self.ev_d)           # the previous step's head / dynamics maps
+            self.g1.replay()
+            self.ev1.record(self.s0)
+        with torch.cuda.stream(self.s1):
+            self.s1.wait_event(self.ev1)
+            self.gd.replay()
+            self.ev_d.record(self.s1)
+        with torch.cuda.stream(self.s0):
+            self.g2.replay()
+        cur.wait_stream(self.s0)
+        cur.wait_event(self.ev_d)
 
     def _snapshot(self):
         """Copies of what a warm-up iteration changes: parameters, optimizer state (None where a
@@ -281,6 +431,13 @@ class GraphTrainStep:
             self.static_x.copy_(x, non_blocking=True)
         if y is not None:
             self.static_y.copy_(y, non_blocking=True)
+        if self.split:
+            self._replay_split()
+            m.global_step += 1
+            self.n_replays += 1
+            if self.check_every > 0 and self.n_replays % self.check_every == 0:
+                self.check_status()
+            return self.loss
         self.g_fb.replay()
         if not self.one_graph:
             self._between(warmup=False)
