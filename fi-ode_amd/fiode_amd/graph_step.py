@@ -87,8 +87,11 @@ class GraphTrainStep:
         if split is None:
             split = SPLIT_DEFAULT
         once = getattr(module, "ode_reuse_features", True) or not getattr(module, "train_ode", False)
-        self.split = bool(split and self.single and maps_ahead and once and isinstance(optimizer, _KernelStepMixin)
-                          and self._split_backbone() is not None and getattr(module.dyn_fun, "cayley", False))
+        # split: one rank, or N ranks whose collectives are captured (RCCL): each half all-reduces
+        # its own gradients on its own stream and process group
+        self.split = bool(split and (self.single or self.comm == "graph") and maps_ahead and once
+                          and isinstance(optimizer, _KernelStepMixin) and self._split_backbone() is not None
+                          and getattr(module.dyn_fun, "cayley", False))
         self.stores, self.d_params, self.split_cap = [], [], {}
         if self.split:
             warmup = max(int(warmup), 2)
@@ -131,7 +134,7 @@ class GraphTrainStep:
         try:
             self._capture()
         except Exception as exc:                   # noqa: BLE001 - rethrown unless it is the comm capture
-            if self.comm != "graph":
+            if self.comm != "graph" or self.split:
                 raise
             # the collectives could not be captured by this runtime: eager bucket all-reduces
             # between two graphs instead (the reason is kept in comm_fallback)
@@ -139,7 +142,7 @@ class GraphTrainStep:
                 self.reducer._armed = None
             self.comm, self.comm_fallback = "eager", repr(exc)
             self._capture()
-        if self.reducer is not None and (world > 1 or self.force_comm):
+        if self.reducer is not None and (world > 1 or self.force_comm) and not self.split:
             views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
                      + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
             if not all(views):
@@ -256,7 +259,7 @@ class GraphTrainStep:
     def _split_on(self):
         from .cayley import CayleyConv, CayleyLinear
         self._maps_ahead_on()
-        if not self.early:
+        if self.single and not self.early:
             raise RuntimeError("split step: the conv layers' early updates are unavailable")
         bb = self._split_backbone()
         bb.split_capture = self.split_cap
@@ -286,6 +289,47 @@ class GraphTrainStep:
         dev = self.static_x.device
         self.s0, self.s1 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         self.ev1, self.ev_d = torch.cuda.Event(), torch.cuda.Event()
+        self.c_params = [p for p in self.params if id(p) not in {id(q) for q in d_params}]
+        if self.comm == "graph":
+            # N ranks: one flat gradient buffer per half (+ its guard slot), all-reduced on its
+            # own stream; the D half on a second process group (= a second RCCL communicator)
+            import torch.distributed as dist
+            self.pg_d = dist.new_group(backend="nccl")
+            self.flat_d, self.view_d = self._flat(d_params)
+            self.flat_c, self.view_c = self._flat(self.c_params)
+
+    def _flat(self, params):
+        n = sum(p.numel() for p in params)
+        flat = torch.zeros(n + 1, dtype=params[0].dtype, device=params[0].device)
+        views, o = {}, 0
+        for p in params:
+            views[id(p)] = flat[o:o + p.numel()].view_as(p)
+            o += p.numel()
+        return flat, views
+
+    def _reduce_half(self, flat, views, pairs, group):
+        """N ranks: this half's gradients into its flat buffer + this rank's guard verdict in the
+        slot, one all-reduce (captured), the mean; returns the pairs on the bucket views."""
+        import torch.distributed as dist
+        torch._foreach_copy_([views[id(p)] for p, _ in pairs], [g for _, g in pairs])
+        if self._mine is not None:
+            self._mine.write_flag(flat[-1:])
+        dist.all_reduce(flat, group=group)
+        flat.div_(self.world)
+        out = [(p, views[id(p)]) for p, _ in pairs]
+        for p, v in out:
+            p.grad = v
+        return out
+
+    def _set_guard(self, slot=None, count=True):
+        if not self._guard_ok:
+            return
+        from .optim import StepGuard
+        if slot is None:
+            g = self._mine
+            self.opt.guard = StepGuard(loss=g.loss, status=g.status, skipped=self.skipped if count else None)
+        else:
+            self.opt.guard = StepGuard(flag=slot, skipped=self.skipped if count else None)
 
     def _phase1(self):
         m = self.module
@@ -297,7 +341,12 @@ class GraphTrainStep:
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         if "h_leaf" not in self.split_cap:
             raise RuntimeError("split step: the backbone did not stop at its conv output")
-        self._arm_guard(loss)
+        self._mine = None
+        if self._guard_ok:
+            from .optim import StepGuard
+            lo = loss.detach().reshape(1)
+            self._mine = StepGuard(loss=lo if lo.dtype == torch.float32 else None,
+                                   status=m.status_words() if hasattr(m, "status_words") else [])
         loss.backward()
         m.rng_counter.add_(1)
         return loss
@@ -308,6 +357,13 @@ class GraphTrainStep:
             pairs += st.param_grads()
         for b in self.d_biases:
             pairs.append((b, b.grad if b.grad is not None else torch.zeros_like(b)))
+        if self.comm == "graph":
+            pairs = self._reduce_half(self.flat_d, self.view_d, pairs, self.pg_d)
+            self._set_guard(self.flat_d[-1:], count=False)
+        else:
+            for p, g in pairs:
+                p.grad = g                  # as after the one-graph step: p.grad = this step's gradient
+            self._set_guard(count=False)
         self.opt.step_params(pairs)
         for st in self.stores:
             st.refresh()
@@ -315,7 +371,16 @@ class GraphTrainStep:
     def _phase2(self):
         sp = self.split_cap
         torch.autograd.backward(sp["h_conv"], sp["h_leaf"].grad)
+        if self.comm == "graph":
+            # no early per-layer updates on N ranks: the conv gradients are final after the
+            # all-reduce; the conv maps are refreshed after the update
+            pairs = [(p, p.grad if p.grad is not None else torch.zeros_like(p)) for p in self.c_params]
+            self._reduce_half(self.flat_c, self.view_c, pairs, None)
+            self._set_guard(self.flat_c[-1:])
+        else:
+            self._set_guard()
         self.opt.step()
+        self._refresh_late()
 
     def _capture_split(self):
         self.one_graph = False

@@ -146,6 +146,9 @@ def _world1_main(port, q, comm):
                 red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
                 gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True)
                 assert gs.comm == comm and len(red.buckets) >= 2
+                # captured collectives: the split step (each half all-reduced on its own stream and
+                # communicator); between replays: the one-graph step
+                assert gs.split == (comm == "graph")
             losses = [float(gs.step()) for _ in range(3)]
             torch.cuda.synchronize()
             res[mode] = (losses, [p.detach().cpu().numpy().copy() for p in mod.parameters()])

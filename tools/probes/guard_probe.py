@@ -1,0 +1,44 @@
+"""Which replayed step does the step guard skip, and why (not a test): the bench's configs[2]
+module (train_ode dopri5), GraphTrainStep (split or one graph), per step the loss, the solve's
+stats (nfe, status, accepted / rejected, attempts), its status word and the skip count."""
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(ROOT), str(ROOT / "fi-ode_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
+
+
+def run(split: bool, solver: str, steps: int = 30):
+    dev = torch.device("cuda:0")
+    mod = bench.build_module(dev, seed=0, train_ode=True, solver=solver)
+    mod.seed = 1000
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    gs = GraphTrainStep(mod, opt, x, y, split=split)
+    print(f"== split={gs.split} solver={solver}", flush=True)
+    prev = 0
+    for i in range(steps):
+        t0 = time.perf_counter()
+        loss = gs.step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) * 1e3
+        st = mod.last_ode_plan["stats"].cpu().tolist()
+        sw = mod.last_ode_plan.get("status_word")
+        sk = gs.skipped_steps()
+        flag = " <-- skipped" if sk != prev else ""
+        prev = sk
+        print(f"step {i:2d} loss {float(loss):.6f} ms {dt:7.2f} stats {st} status_word "
+              f"{None if sw is None else int(sw[0])} skipped {sk}{flag}", flush=True)
+    gs.close()
+
+
+if __name__ == "__main__":
+    for split in (True, False):
+        run(split, "dopri5")
