@@ -646,25 +646,34 @@ __global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc2[mb] = f16_zero();
   float db2 = 0.f, db1 = 0.f, db3 = 0.f;
-  for (int j = r0; j < r1; j += 2) {
+  // the operands of row pair j + 2 are loaded before the MFMAs of pair j (software pipeline: each
+  // pair's 9 global loads otherwise sit in front of its MFMAs -- the loop was load-latency bound)
+  struct Ops { float A2[4], B2, A3, B3, A1, B1; };
+  auto load = [&](int j, Ops& o) {
     const int jj = j + half;
     const bool ok = jj < r1;
     const int js = ok ? jj : r0;
-    float A2[4];
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) A2[mb] = ok ? a.gz2[(size_t)js * M + 32 * mb + col] : 0.f;
-    const float B2 = a.a1[(size_t)js * M + 32 * w + col];
-    const float A3 = (ok && col < C) ? a.gft[(size_t)js * C + col] : 0.f;
-    const float B3 = a.a2[(size_t)js * M + 32 * w + col];
-    const float A1 = ok ? a.gz1[(size_t)js * M + 32 * w + col] : 0.f;
-    const float B1 = col < C ? hsrc[(size_t)js * C + col] : 0.f;
+    for (int mb = 0; mb < 4; ++mb) o.A2[mb] = ok ? a.gz2[(size_t)js * M + 32 * mb + col] : 0.f;
+    o.B2 = a.a1[(size_t)js * M + 32 * w + col];
+    o.A3 = (ok && col < C) ? a.gft[(size_t)js * C + col] : 0.f;
+    o.B3 = a.a2[(size_t)js * M + 32 * w + col];
+    o.A1 = ok ? a.gz1[(size_t)js * M + 32 * w + col] : 0.f;
+    o.B1 = col < C ? hsrc[(size_t)js * C + col] : 0.f;
+  };
+  Ops cur;
+  if (r0 < r1) load(r0, cur);
+  for (int j = r0; j < r1; j += 2) {
+    Ops nxt = cur;
+    if (j + 2 < r1) load(j + 2, nxt);
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(A2[mb], B2, acc2[mb]);
-    acc3 = mfma32(A3, B3, acc3);
-    acc1 = mfma32(A1, B1, acc1);
-    db2 += (w == 0) ? A2[0] : (w == 1) ? A2[1] : (w == 2) ? A2[2] : A2[3];
-    db1 += A1;
-    db3 += A3;
+    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(cur.A2[mb], cur.B2, acc2[mb]);
+    acc3 = mfma32(cur.A3, cur.B3, acc3);
+    acc1 = mfma32(cur.A1, cur.B1, acc1);
+    db2 += (w == 0) ? cur.A2[0] : (w == 1) ? cur.A2[1] : (w == 2) ? cur.A2[2] : cur.A2[3];
+    db1 += cur.A1;
+    db3 += cur.A3;
+    cur = nxt;
   }
   float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
 #pragma unroll

@@ -39,7 +39,9 @@ from typing import Optional
 import torch
 
 
-SPLIT_DEFAULT = True          # one rank: the three-graph split step (see GraphTrainStep._split_backbone)
+SPLIT_DEFAULT = False         # the three-graph split step (see GraphTrainStep._split_backbone): measured slower
+                              # at the HIP default of 4 hardware queues
+D_CHAINS = True               # one rank: the split step's maps' chains on one stream each (_phase_d_chains)
 
 
 class GraphTrainStep:
@@ -352,6 +354,8 @@ class GraphTrainStep:
         return loss
 
     def _phase_d(self):
+        if self.comm != "graph" and D_CHAINS:
+            return self._phase_d_chains()
         pairs = []
         for st in self.stores:
             pairs += st.param_grads()
@@ -367,6 +371,27 @@ class GraphTrainStep:
         self.opt.step_params(pairs)
         for st in self.stores:
             st.refresh()
+
+    def _phase_d_chains(self):
+        """One rank: each stored map's chain -- backward, Adam of its parameters, next map -- forked
+        on a stream of its own (the four chains are independent; the 4096 -> 512 map's is the
+        longest), the biases' Adam on the phase's stream; joined at the end."""
+        cur = torch.cuda.current_stream()
+        if len(getattr(self, "_d_streams", [])) < len(self.stores):
+            self._d_streams = [torch.cuda.Stream(cur.device) for _ in self.stores]
+        self._set_guard(count=False)
+        for st, ss in zip(self.stores, self._d_streams):
+            ss.wait_stream(cur)
+            with torch.cuda.stream(ss):
+                pairs = st.param_grads()
+                for p, g in pairs:
+                    p.grad = g              # as after the one-graph step: p.grad = this step's gradient
+                self.opt.step_params(pairs)
+                st.refresh()
+        pairs = [(b, b.grad if b.grad is not None else torch.zeros_like(b)) for b in self.d_biases]
+        self.opt.step_params(pairs)
+        for ss in self._d_streams[:len(self.stores)]:
+            cur.wait_stream(ss)
 
     def _phase2(self):
         sp = self.split_cap

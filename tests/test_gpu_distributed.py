@@ -144,10 +144,11 @@ def _world1_main(port, q, comm):
                 gs = GraphTrainStep(mod, opt, x, y, warmup=2)
             else:
                 red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
-                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True)
+                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True,
+                                    split=True)
                 assert gs.comm == comm and len(red.buckets) >= 2
-                # captured collectives: the split step (each half all-reduced on its own stream and
-                # communicator); between replays: the one-graph step
+                # captured collectives: the split step asked for (each half all-reduced on its own
+                # stream and communicator); between replays the one-graph step (gloo-style comm)
                 assert gs.split == (comm == "graph")
             losses = [float(gs.step()) for _ in range(3)]
             torch.cuda.synchronize()

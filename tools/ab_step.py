@@ -35,7 +35,8 @@ def make(setup):
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
-    return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False))
+    return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False),
+                          split=getattr(mod, "_split", None))
 
 
 def default(m):
@@ -81,6 +82,21 @@ def lib_gmn(m):
     RESTORE.append(lambda: setattr(CY, "DENSE_GEMM", True))
 
 
+def one_graph(m):
+    m._split = False              # the round-3 step: one graph, dense maps' chain on the step's queue
+
+
+def split(m):
+    m._split = True               # the three-graph split step (GraphTrainStep split=True)
+
+
+def split_serial(m):
+    m._split = True
+    from fiode_amd import graph_step as GS
+    GS.D_CHAINS = False           # split step, the maps' chains one after another on the D stream
+    RESTORE.append(lambda: setattr(GS, "D_CHAINS", True))
+
+
 def ode_on_main(m):
     m.ode_side_stream = False
 
@@ -91,7 +107,8 @@ def seed1000(m):
 
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
-       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn}
+       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
+       "split": split, "split_serial": split_serial}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}

@@ -34,8 +34,13 @@ def run(split: bool, solver: str, steps: int = 30):
         sk = gs.skipped_steps()
         flag = " <-- skipped" if sk != prev else ""
         prev = sk
-        print(f"step {i:2d} loss {float(loss):.6f} ms {dt:7.2f} stats {st} status_word "
-              f"{None if sw is None else int(sw[0])} skipped {sk}{flag}", flush=True)
+        pl = mod.last_plan
+        yh = pl.get("y_hat")
+        yl = float(yh.gather(1, y[:, None]).min()) if yh is not None else float("nan")
+        print(f"step {i:2d} loss {float(loss):.6f} lyap {float(pl['scalars'][0]):.6f} ode "
+              f"{float(pl['loss_ode']) if 'loss_ode' in pl else float('nan'):.6f} min y_hat[label] {yl:.3e} "
+              f"ms {dt:7.2f} stats {st} status_word {None if sw is None else int(sw[0])} skipped {sk}{flag}",
+              flush=True)
     gs.close()
 
 
