@@ -71,6 +71,7 @@ struct LyapArgs {
   const uint64_t* offset_dev;   // optional device-resident addend of the Philox offset
   DynScalars d;
   float kappa, invN;
+  const float* kappa_dev;    // optional device kappa (the ramp of a captured step), else kappa
   int parts, chunk;
   const float* x_feat;
   const int64_t* y;
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   f32x4 b2w[4];                              // b2 of block w in accumulator order
 #pragma unroll
   for (int g = 0; g < 4; ++g) b2w[g] = *reinterpret_cast<const f32x4*>(a.b2 + 32 * w + 8 * g + 4 * half);
+  const float kappa = a.kappa_dev ? *a.kappa_dev : a.kappa;
   const int K0 = qp_exit_iter(a.conv[0], a.d.max_iter);
   const int K1 = qp_exit_iter(a.conv[1], a.d.max_iter);
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
@@ -387,7 +389,7 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
         }
         const float Vv = (1.0f + hm) - hy;
         const float Vd = fj - fy;                  // jvp of the piecewise-linear V along f
-        const float pre = Vd + a.kappa * Vv;       // vdot + kappa * V.detach() (pl_modules.py:455-457)
+        const float pre = Vd + kappa * Vv;         // vdot + kappa * V.detach() (pl_modules.py:455-457)
         const float viol = pre > 0.f ? pre : 0.f;
         const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
         float g[C], g_nom[C], g_low[C];
@@ -898,6 +900,7 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   a.d.alpha_1 = dyn->alpha_1; a.d.alpha_2 = dyn->alpha_2; a.d.sigma_1 = dyn->sigma_1;
   a.d.tol = dyn->qp_tol; a.d.scale_nominal = dyn->scale_nominal; a.d.max_iter = dyn->qp_max_iter;
   a.kappa = cfg->kappa;
+  a.kappa_dev = io->kappa_dev;
   a.invN = 1.0f / (float)a.N;
   parts_for(B, S, a.parts, a.chunk);
   a.x_feat = io->x_feat; a.y = io->y; a.h_in = io->h; a.masks = io->masks;

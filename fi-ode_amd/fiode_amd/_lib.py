@@ -48,7 +48,7 @@ class LyapIO(ct.Structure):
     _fields_ = [(n, ct.c_void_p) for n in ("x_feat", "y", "h", "masks", "scalars", "h_out", "V", "Vdot",
                                            "f", "f_log", "qp_lower", "qp_nominal", "g_ftilde", "events")] + \
         [("n_events", ct.c_int32), ("offset_dev", ct.c_void_p), ("exp_draws", ct.c_void_p),
-         ("exp_draws_out", ct.c_void_p), ("keep_words_out", ct.c_void_p)]
+         ("exp_draws_out", ct.c_void_p), ("keep_words_out", ct.c_void_p), ("kappa_dev", ct.c_void_p)]
 
 
 LYAP_KERNELS = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_reduce", "k_lyap_static_grads")

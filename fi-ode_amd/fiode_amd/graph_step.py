@@ -29,7 +29,8 @@ once a step was skipped.  (torch.amp's found_inf skip, without a host sync.)
 
 Static inputs: ``step(x, y)`` copies the batch into the captured input buffers.  What the
 captured step bakes in (and ``GraphTrainStep`` checks on every call): the sampler plan of the
-current epoch (S1/S2 split, ``scale_nominal``), kappa (needs ``global_step >= kappa_length``),
+current epoch (S1/S2 split, ``scale_nominal``), the kappa ramp's anchor (the ramp itself follows the
+device step counter),
 batch shape.  Recapture (construct a new GraphTrainStep) at an epoch boundary.
 """
 from __future__ import annotations
@@ -68,8 +69,12 @@ class GraphTrainStep:
         self.comm = comm if multi else "none"
         self.comm_stream = torch.cuda.Stream(dev) if self.comm == "graph" else None
         dyn = module.dyn_fun
-        if module.global_step < dyn.kappa_length:
-            raise ValueError("kappa still ramping (global_step < kappa_length): run those steps eagerly")
+        if module.rng_counter is None:
+            module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        # the kappa ramp (pl_modules.py:447-448) follows the device step counter in the captured
+        # step: global_step = rng_counter + anchor (LyapunovLearning.kappa_device)
+        ramp = dyn.kappa_length and module.global_step < dyn.kappa_length
+        module._kappa_anchor = (module.global_step - int(module.rng_counter.item())) if ramp else None
         self.epoch = module.current_epoch
         self.static_x = x.detach().clone()
         self.static_y = y.detach().clone()
@@ -221,6 +226,7 @@ class GraphTrainStep:
 
     def close(self) -> None:
         """Back to maps computed at the start of each step (eager training of the same module)."""
+        self.module._kappa_anchor = None
         for c in self.piped:
             c.pipeline_off()
         self.piped = []

@@ -38,7 +38,7 @@ class LyapunovLossFn(torch.autograd.Function):
             x_feat.detach().contiguous(), y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"],
             sampler=plan["sampler"], dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"],
             offset=plan["offset"], h=plan.get("h"), masks=plan.get("masks"), debug=plan.get("debug", False),
-            out=plan.get("out"), offset_dev=plan.get("offset_dev"))
+            out=plan.get("out"), offset_dev=plan.get("offset_dev"), kappa_dev=plan.get("kappa_dev"))
         plan["scalars"] = sc
         plan["debug_out"] = dbg
         g = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
@@ -168,7 +168,7 @@ class LyapODELossFn(torch.autograd.Function):
             xf, y, w, plan["dyn"], sample_size=plan["S"], n_uniform=plan["S1"],
             sampler=plan["sampler"], dropout_mode=plan["dropout_mode"], kappa=plan["kappa"], seed=plan["seed"],
             offset=plan["offset"], h=plan.get("h"), masks=plan.get("masks"), debug=plan.get("debug", False),
-            out=plan.get("out"), offset_dev=plan.get("offset_dev"))
+            out=plan.get("out"), offset_dev=plan.get("offset_dev"), kappa_dev=plan.get("kappa_dev"))
         plan["scalars"] = sc
         plan["debug_out"] = dbg
         if pre is not None:
@@ -408,6 +408,21 @@ class LyapunovLearning(nn.Module):
             return self.global_step / dyn.kappa_length * dyn.kappa
         return dyn.kappa
 
+    def kappa_device(self) -> Optional[torch.Tensor]:
+        """The kappa ramp (pl_modules.py:447-448) on the device, for a captured step: with the
+        anchor GraphTrainStep sets (global_step - rng_counter at capture), global_step = rng_counter +
+        anchor is read from the device counter every replay advances; kappa = global_step /
+        kappa_length * kappa in float64 (Python's arithmetic), rounded to float32 like torch's scalar
+        operand, or kappa once global_step >= kappa_length.  None = the host value (eager steps)."""
+        anchor = getattr(self, "_kappa_anchor", None)
+        dyn = self.dyn_fun
+        if anchor is None or self.rng_counter is None or not dyn.kappa_length:
+            return None
+        step = self.rng_counter.double() + float(anchor)
+        L_ = float(dyn.kappa_length)
+        return torch.where(step < L_, step / L_ * float(dyn.kappa),
+                           torch.full_like(step, float(dyn.kappa))).float()
+
     def step_plan(self, y: torch.Tensor, h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None,
                   debug: bool = False, static_state: Optional[torch.Tensor] = None) -> dict:
         mix = self.sampler_scheduler.get_mixer_coefficients(self.current_epoch)
@@ -424,7 +439,7 @@ class LyapunovLearning(nn.Module):
             traj = next(t for t in self.sampler.samplers if isinstance(t, TrajectorySampler))
             h = traj.trajectory(self, static_state, self.h_sample_size - s1)
         plan = dict(dyn=self.dyn_fun.dyn_cfg(), S=self.h_sample_size, S1=s1, sampler=kind, dropout_mode=drop,
-                    kappa=self.current_kappa(), seed=self.seed,
+                    kappa=self.current_kappa(), kappa_dev=self.kappa_device(), seed=self.seed,
                     offset=self._rng_offset if self.rng_counter is None else 0, h=h, masks=masks,
                     debug=debug, out=None, offset_dev=self.rng_counter)
         self._rng_offset += 1
@@ -510,7 +525,7 @@ class LyapunovLearning(nn.Module):
         loss = LyapunovLossFn.apply(static_state.float(), w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"],
                                     w["Q3"], w["b3"], y, plan)
         sc = plan["scalars"]
-        self.log("kappa", plan["kappa"])
+        self.log("kappa", plan["kappa_dev"] if plan.get("kappa_dev") is not None else plan["kappa"])
         self.log("effective_batch_size", sc[1])
         self.log("mean_active_constraints", sc[2])
         self.last_plan = plan
@@ -617,7 +632,7 @@ class LyapunovLearning(nn.Module):
         total = LyapODELossFn.apply(static_state, x_ode, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
                                     w["b3"], h0, y, plan, oplan, p, stream)
         sc = plan["scalars"]
-        self.log("kappa", plan["kappa"])
+        self.log("kappa", plan["kappa_dev"] if plan.get("kappa_dev") is not None else plan["kappa"])
         self.log("effective_batch_size", sc[1])
         self.log("mean_active_constraints", sc[2])
         self.log("loss_ode", plan["loss_ode"])

@@ -92,7 +92,7 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
               dropout_mode: int = L.FIODE_DROPOUT_PHILOX, kappa: float = 2.0, seed: int = 0, offset: int = 0,
               h: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None, debug: bool = False,
               out: Optional[dict] = None, events=None, offset_dev: Optional[torch.Tensor] = None,
-              exp_draws: Optional[torch.Tensor] = None):
+              exp_draws: Optional[torch.Tensor] = None, kappa_dev: Optional[torch.Tensor] = None):
     """The fused training step (fiode_lyap_step).  Returns (scalars[8], grads dict, debug dict).
     ``events``: optional list of len(_lib.LYAP_KERNELS)+1 torch.cuda.Event(enable_timing=True),
     recorded by the library around each of its kernels on the current stream.
@@ -150,6 +150,8 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
                    keep_words=torch.empty((4, N, 4), dtype=torch.int32, device=dev))
         if n_draws:
             dbg["exp_draws"] = torch.empty(n_draws, dtype=torch.float32, device=dev)
+    if kappa_dev is not None:
+        kappa_dev = _need(kappa_dev.reshape(1), "kappa_dev", (1,), torch.float32, dev)
     cfg = L.LyapConfig(B, S, int(n_uniform), int(sampler), int(dropout_mode), float(kappa),
                        int(seed) & (2**64 - 1), int(offset) & (2**64 - 1))
     dc = dyn.to_c()
@@ -167,7 +169,8 @@ def lyap_step(x_feat: torch.Tensor, y: torch.Tensor, weights: Dict[str, torch.Te
                   _ptr(dbg.get("h")), _ptr(dbg.get("V")), _ptr(dbg.get("Vdot")), _ptr(dbg.get("f")),
                   _ptr(dbg.get("f_log")), _ptr(dbg.get("qp_lower")), _ptr(dbg.get("qp_nominal")),
                   _ptr(dbg.get("g_ftilde")), ct.cast(ev_arr, ct.c_void_p) if ev_arr is not None else None, n_ev,
-                  _ptr(offset_dev), _ptr(exp_draws), _ptr(dbg.get("exp_draws")), _ptr(dbg.get("keep_words")))
+                  _ptr(offset_dev), _ptr(exp_draws), _ptr(dbg.get("exp_draws")), _ptr(dbg.get("keep_words")),
+                  _ptr(kappa_dev))
     cg = L.LyapGrads(*[grads[k].data_ptr() for k in WEIGHT_KEYS + ("x_feat",)])
     lib = L.lib()
     nbytes = lib.fiode_lyap_workspace_bytes(ct.byref(cfg), ct.byref(dc))

@@ -111,6 +111,10 @@ typedef struct fiode_lyap_io {
   float* exp_draws_out;     /* optional out: the Exp(1) variates the sampler used, same layout  */
   uint32_t* keep_words_out; /* optional out: [4][N][4] dropout keep words of the 4 mask sets
                                (bit t of word mb = keep hidden unit 32 mb + t)                  */
+  /* optional device-resident kappa (NULL = cfg.kappa): the kappa ramp of pl_modules.py:447-448
+   * (global_step / kappa_length * kappa while global_step < kappa_length) computed on the device,
+   * so a captured step follows it on every replay */
+  const float* kappa_dev;
 } fiode_lyap_io;
 
 /* kernels of one fiode_lyap_step, in launch order (for the profiling events) */

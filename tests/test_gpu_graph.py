@@ -219,3 +219,43 @@ def test_split_step_equals_one_graph_step(train_ode):
     for sa, sb in zip(out[True][2], out[False][2]):
         for k in sa:
             assert torch.equal(sa[k], sb[k]), k
+
+
+def test_kappa_ramp_followed_by_captured_step():
+    """kappa_length > 0 (pl_modules.py:447-448: kappa = global_step / kappa_length * kappa while
+    global_step < kappa_length): the captured step reads kappa from the device step counter, so its
+    replays follow the ramp -- equal to eager steps of a twin at the host's kappa (losses 1e-5,
+    parameters 1e-4 after 3 steps); the ramp is visible in the loss (kappa 0, 0.2, 0.4)."""
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(12)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    mods = []
+    for seed in (0, 1):
+        m = bench.build_module(dev, seed=seed, train_ode=False)
+        m.dyn_fun.kappa_length = 10
+        m.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        mods.append(m)
+    mod, twin = mods
+    twin.load_state_dict(mod.state_dict())
+    twin.seed = mod.seed
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y, warmup=2)
+    topt = twin.configure_optimizers(capturable=True)[0][0]
+    for step in range(3):
+        assert twin.current_kappa() == step / 10 * 2.0
+        loss = float(gs.step())
+        topt.zero_grad(set_to_none=True)
+        l2 = twin.compute_loss(x, y, 32, "relu")
+        l2.backward()
+        topt.step()
+        twin.global_step += 1
+        twin.rng_counter.add_(1)
+        torch.cuda.synchronize()
+        assert abs(loss - float(l2)) <= 1e-5 * max(1.0, abs(loss)), (step, loss, float(l2))
+    assert mod.global_step == 3
+    for a, b in zip(mod.parameters(), twin.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+    gs.close()
