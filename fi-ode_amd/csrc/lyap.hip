@@ -236,13 +236,16 @@ __global__ __launch_bounds__(256) void k_lyap_prep(LyapArgs a) {
   }
 }
 
-// One wave per (32-row tile, pass): the loss pass (pass 0) and the logging pass (pass 1) of a tile
-// are independent, so a workgroup's 4 waves are 2 tiles x 2 passes and 2 workgroups share a CU
-// (LDS 72.9 KB each, <= 256 registers): one wave's QP (VALU) overlaps another's MFMA on every
-// SIMD.  Per wave: layers 1-3, ft -> HBM, the QP to max_iter - 1 for its convergence bits, AND-ed
-// per pass into one word (the batch-global exit, barrier_projection.py:247-249).
+// One wave per 32-row tile, both passes: the loss pass's MLP (dropout masks 0/1) and the logging
+// pass's (masks 2/3) on the MFMA, then ONE QP per lane -- lanes 0..31 take the loss pass of their
+// row, lanes 32..63 the logging pass (a 32x32 accumulator tile leaves every row's outputs on both
+// halves, so one pass per wave would run each row's QP twice).  Per wave: ft -> HBM, the QP to
+// max_iter - 1 for its convergence bits, AND-ed per pass into CONV_SLOTS words (the batch-global
+// exit, barrier_projection.py:247-249).  Persistent: two workgroups per CU (LDS 72.9 KB each), the
+// weight images staged once per workgroup; with more than one tile per SIMD, one wave's QP (VALU)
+// overlaps the other's MFMA.
 #ifndef FWD_WAVES
-#define FWD_WAVES 4           // waves per workgroup: FWD_WAVES / 2 tiles x 2 passes
+#define FWD_WAVES 4           // waves (tiles in flight) per workgroup
 #endif
 __global__ __launch_bounds__(64 * FWD_WAVES, 8 / FWD_WAVES) void k_lyap_fwd(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -261,31 +264,42 @@ __global__ __launch_bounds__(64 * FWD_WAVES, 8 / FWD_WAVES) void k_lyap_fwd(Lyap
 #pragma unroll
     for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
   const int ntiles = (a.N + 31) / 32;
-  const int pass = wave & 1;
-  for (int tile = (FWD_WAVES / 2) * blockIdx.x + (wave >> 1); tile < ntiles; tile += (FWD_WAVES / 2) * gridDim.x) {
+  const int pass = half;                    // this lane's pass in the QP phase
+  for (int tile = FWD_WAVES * blockIdx.x + wave; tile < ntiles; tile += FWD_WAVES * gridDim.x) {
     const int row = tile * 32 + col;
     const bool valid = row < a.N;
     const int rr = valid ? row : a.N - 1;
     const int b = rr / a.S;
     float h[C];
     load_row10(((a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws) + (size_t)rr * C, h);
-    const uint4 k1 = a.kw[(size_t)(2 * pass) * a.N + rr], k2 = a.kw[(size_t)(2 * pass + 1) * a.N + rr];
-    const uint32_t kw1[4] = {k1.x, k1.y, k1.z, k1.w}, kw2[4] = {k2.x, k2.y, k2.z, k2.w};
+    uint4 kq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) kq[q] = a.kw[(size_t)q * a.N + rr];
     LY_T(1);
-    f32x16 z1[4], z2[4];
-    const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
-                               col, half, z1, z2);
+    float ft[C] = {};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t kw1[4] = {kq[2 * p].x, kq[2 * p].y, kq[2 * p].z, kq[2 * p].w};
+      const uint32_t kw2[4] = {kq[2 * p + 1].x, kq[2 * p + 1].y, kq[2 * p + 1].z, kq[2 * p + 1].w};
+      f32x16 z1[4], z2[4];
+      const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw1, kw2, a.drop_scale,
+                                 col, half, z1, z2);
+      float fp[C];
+      gather_ft(z3, half, fp);
+#pragma unroll
+      for (int j = 0; j < C; ++j) ft[j] = (p == pass) ? fp[j] : ft[j];
+    }
     LY_T(2);
-    float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-    gather_ft(z3, half, ft);
+    float lower[C], nominal[C], sig[C], span[C], v[C], mu;
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
     LY_T(3);
     uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
     LY_T(4);
     if (!valid) conv = 0xFFFFFFFFu;
-    conv = wave_and(conv);
-    if (lane == 0) atomicAnd(a.conv + pass * CONV_SLOTS + (blockIdx.x % CONV_SLOTS), conv);
-    if (valid && half == 0) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) conv &= (uint32_t)__shfl_xor((int)conv, o, 64);   // AND within each half
+    if (col == 0) atomicAnd(a.conv + pass * CONV_SLOTS + (blockIdx.x % CONV_SLOTS), conv);
+    if (valid) {
       store_row10(a.ft_ws + ((size_t)pass * a.N + row) * C, ft);
       if (a.qp_nominal) store_row10(a.qp_nominal + ((size_t)pass * a.N + row) * C, nominal);
       if (pass == 0 && a.qp_lower) store_row10(a.qp_lower + (size_t)row * C, lower);
@@ -380,59 +394,60 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
       load_row10(hsrc + (size_t)rr * C, h);
       const uint4 kwa = a.kw[rr], kwb = a.kw[(size_t)a.N + rr];
       if (tile < ntiles) {
+        // lanes 0..31: the loss pass of their row (QP to K0, V / V-dot / hinge, QP backward);
+        // lanes 32..63: the logging pass (QP to K1, active-constraint count) -- one QP per lane
         const int label = (int)a.y[rr / a.S];
+        const bool loss_half = half == 0;
         float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-        load_row10(a.ft_ws + (size_t)rr * C, ft);
+        load_row10(a.ft_ws + ((size_t)half * a.N + rr) * C, ft);
         barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
-        qp_bisect(lower, nominal, K0, a.d.tol, v, mu);
-        // V = (1 + max_{j != y} h_j) - h_y ; j* first index (lya_cands.py:84-94)
-        int js = label == 0 ? 1 : 0;
-        float hm = h[js];
+        qp_bisect(lower, nominal, loss_half ? K0 : K1, a.d.tol, v, mu);
+        float viol = 0.f, active = 0.f;
+        if (loss_half) {
+          // V = (1 + max_{j != y} h_j) - h_y ; j* first index (lya_cands.py:84-94)
+          int js = label == 0 ? 1 : 0;
+          float hm = h[js];
 #pragma unroll
-        for (int j = 0; j < C; ++j)
-          if (j != label && h[j] > hm) { hm = h[j]; js = j; }
-        float hy = 0.f, fy = 0.f, fj = 0.f;
+          for (int j = 0; j < C; ++j)
+            if (j != label && h[j] > hm) { hm = h[j]; js = j; }
+          float hy = 0.f, fy = 0.f, fj = 0.f;
 #pragma unroll
-        for (int j = 0; j < C; ++j) {
-          hy = (j == label) ? h[j] : hy;
-          fy = (j == label) ? v[j] : fy;
-          fj = (j == js) ? v[j] : fj;
+          for (int j = 0; j < C; ++j) {
+            hy = (j == label) ? h[j] : hy;
+            fy = (j == label) ? v[j] : fy;
+            fj = (j == js) ? v[j] : fj;
+          }
+          const float Vv = (1.0f + hm) - hy;
+          const float Vd = fj - fy;                  // jvp of the piecewise-linear V along f
+          const float pre = Vd + kappa * Vv;         // vdot + kappa * V.detach() (pl_modules.py:455-457)
+          viol = pre > 0.f ? pre : 0.f;
+          const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
+          float g[C], g_nom[C], g_low[C];
+#pragma unroll
+          for (int j = 0; j < C; ++j) g[j] = (j == js) ? gp : ((j == label) ? -gp : 0.f);
+          qp_backward_row(g, v, mu, nominal, g_nom, g_low);
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            gft[j] = a.d.scale_nominal ? ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j] : g_nom[j];
+          if (valid) {
+            if (a.V) a.V[row] = Vv;
+            if (a.Vdot) a.Vdot[row] = Vd;
+            if (a.f) store_row10(a.f + (size_t)row * C, v);
+            if (a.g_ftilde) store_row10(a.g_ftilde + (size_t)row * C, gft);
+          }
+        } else {
+          // logging pass: active-constraint count (pl_modules.py:476-482)
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            const float lin = -a.d.alpha_1 * h[j];
+            const float up = a.d.alpha_2 * (1.0f - h[j]);
+            active += (fabsf(v[j] - lin) <= 1e-6f || fabsf(v[j] - up) <= 1e-6f) ? 1.f : 0.f;
+          }
+          if (valid && a.f_log) store_row10(a.f_log + (size_t)row * C, v);
         }
-        const float Vv = (1.0f + hm) - hy;
-        const float Vd = fj - fy;                  // jvp of the piecewise-linear V along f
-        const float pre = Vd + kappa * Vv;         // vdot + kappa * V.detach() (pl_modules.py:455-457)
-        const float viol = pre > 0.f ? pre : 0.f;
-        const float gp = (pre > 0.f && valid) ? a.invN : 0.f;
-        float g[C], g_nom[C], g_low[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) g[j] = (j == js) ? gp : ((j == label) ? -gp : 0.f);
-        qp_backward_row(g, v, mu, nominal, g_nom, g_low);
-#pragma unroll
-        for (int j = 0; j < C; ++j)
-          gft[j] = a.d.scale_nominal ? ((g_nom[j] * span[j]) * (1.0f - sig[j])) * sig[j] : g_nom[j];
-        if (valid && half == 0) {
-          if (a.V) a.V[row] = Vv;
-          if (a.Vdot) a.Vdot[row] = Vd;
-          if (a.f) store_row10(a.f + (size_t)row * C, v);
-          if (a.g_ftilde) store_row10(a.g_ftilde + (size_t)row * C, gft);
-        }
-        // logging pass: QP to K1, active-constraint count (pl_modules.py:476-482)
-        float fl[C], nom1[C], mu1;
-        load_row10(a.ft_ws + ((size_t)a.N + rr) * C, ft);
-        barrier_nominal(a.d, h, ft, lower, nom1, sig, span);
-        qp_bisect(lower, nom1, K1, a.d.tol, fl, mu1);
-        float active = 0.f;
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-          const float lin = -a.d.alpha_1 * h[j];
-          const float up = a.d.alpha_2 * (1.0f - h[j]);
-          active += (fabsf(fl[j] - lin) <= 1e-6f || fabsf(fl[j] - up) <= 1e-6f) ? 1.f : 0.f;
-        }
-        if (valid && half == 0 && a.f_log) store_row10(a.f_log + (size_t)row * C, fl);
-        const bool cnt = valid && half == 0;
-        const float s0 = wave_sum(cnt ? viol : 0.f);
-        const float s1 = wave_sum(cnt && viol > 0.f ? 1.f : 0.f);
-        const float s2 = wave_sum(cnt ? active : 0.f);
+        const float s0 = wave_sum(valid && loss_half ? viol : 0.f);
+        const float s1 = wave_sum(valid && loss_half && viol > 0.f ? 1.f : 0.f);
+        const float s2 = wave_sum(valid && !loss_half ? active : 0.f);
         if (lane == 0) *reinterpret_cast<f32x4*>(a.tile_sc + 4 * tile) = f32x4{s0, s1, s2, 0.f};
       }
       if (half == 0) {
@@ -947,7 +962,14 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
     return 0;
   };
   const int ntiles = (a.N + 31) / 32;
-  const int fwd_blocks = (ntiles + FWD_WAVES / 2 - 1) / (FWD_WAVES / 2);   // FWD_WAVES / 2 tiles x 2 passes per workgroup
+  int fwd_blocks = (ntiles + FWD_WAVES - 1) / FWD_WAVES;                    // one tile (both passes) per wave
+  {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+    if (fwd_blocks > (8 / FWD_WAVES) * ncu) fwd_blocks = (8 / FWD_WAVES) * ncu;   // persistent: resident workgroups
+  }
   const size_t lds_fwd = (size_t)(M + C) * LDQ * sizeof(float);
   if ((rc = mark())) return rc;
   hipLaunchKernelGGL(k_static_proj, dim3(B), dim3(128), 0, st, a);

@@ -1,7 +1,8 @@
 """Kernel timings of the throughput kernels for one library build (not a test): the fused fan-out
 (fiode_lyap_step at B=128, S=256, per-kernel HIP events, median of 20) and the certification of
 one image on the T=40 grid (fiode_certify, median of 3).  FIODE_LIB selects the build.
-usage: python tools/ab_fanout.py [tag]  -> one JSON line"""
+usage: python tools/ab_fanout.py [tag] [--large] [--no-cert]  -> one JSON line
+(--large adds the fan-out at B=1024, S=1024: BASELINE configs[4]'s fan-out on one GPU)"""
 import json
 import pathlib
 import statistics
@@ -15,7 +16,8 @@ import torch  # noqa: E402
 from fiode_amd import _lib as L, ops  # noqa: E402
 from tests._util import make_params  # noqa: E402
 
-tag = sys.argv[1] if len(sys.argv) > 1 else "lib"
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+tag = args[0] if args else "lib"
 dev = torch.device("cuda:0")
 P = make_params(1)
 w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
@@ -36,6 +38,23 @@ for rep in range(23):
             per[k].append(ev[i].elapsed_time(ev[i + 1]) * 1e3)
 out = {"tag": tag, "fanout_us": {k: round(statistics.median(v), 2) for k, v in per.items()},
        "loss": float(sc[0])}
+if "--large" in sys.argv:
+    BL, SL = 1024, 1024
+    xl = torch.randn(BL, 10, generator=g).to(dev)
+    yl = torch.randint(0, 10, (BL,), generator=g).to(dev)
+    perl = {k: [] for k in L.LYAP_KERNELS}
+    for rep in range(8):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(nk + 1)]
+        scl, _, _ = ops.lyap_step(xl, yl, w, dyn, sample_size=SL, n_uniform=816, seed=1, offset=rep, events=ev)
+        torch.cuda.synchronize()
+        if rep >= 2:
+            for i, k in enumerate(L.LYAP_KERNELS):
+                perl[k].append(ev[i].elapsed_time(ev[i + 1]) * 1e3)
+    out["fanout_large_us"] = {k: round(statistics.median(v), 2) for k, v in perl.items()}
+    out["loss_large"] = float(scl[0])
+if "--no-cert" in sys.argv:
+    print(json.dumps(out), flush=True)
+    sys.exit(0)
 grid = ops.certify_grid(40, device=dev)
 xf = torch.randn(10, generator=g).to(dev)
 cd = ops.DynCfg(scale_nominal=False, dropout=0.0)

@@ -4,8 +4,8 @@
 set -u
 O=gpurun_out/${1:-libab}; R=${2:-2}; mkdir -p $O
 for i in $(seq 1 $R); do
-  FIODE_LIB=tools/libfiode_base.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --steps 40 --warmup 10 > $O/base_$i.json 2>/dev/null || { echo "base bench failed"; exit 1; }
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --steps 40 --warmup 10 > $O/new_$i.json 2>/dev/null || { echo "new bench failed"; exit 1; }
+  FIODE_LIB=tools/libfiode_base.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --no-configs --steps 40 --warmup 10 > $O/base_$i.json 2>/dev/null || { echo "base bench failed"; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --no-configs --steps 40 --warmup 10 > $O/new_$i.json 2>/dev/null || { echo "new bench failed"; exit 1; }
 done
 python - "$O" "$R" <<'PY'
 import json, sys

@@ -38,6 +38,8 @@ allp = ws[nb - (64 + 4096) * 8:nb].view(torch.int64).cpu().numpy()
 prof = allp[:64]
 for name, base, nwg in (("k_lyap_fwd", 64, 512), ("k_lyap_bwd", 64 + 2048, 256)):
     st = allp[base:base + 2 * nwg].reshape(nwg, 2).astype(np.float64) * 0.01
+    st = st[st[:, 1] > 0]                      # the launched workgroups (the grid may be smaller)
+    nwg = len(st)
     t0 = st[:, 0].min()
     dur = st[:, 1] - st[:, 0]
     print(f"{name}: span {st[:, 1].max() - t0:.1f} us; workgroup start offsets (us) p50 {np.median(st[:, 0] - t0):.1f} "
