@@ -50,7 +50,12 @@ __device__ __forceinline__ f32x4q q4_zero() { return f32x4q{0.f, 0.f, 0.f, 0.f};
 // per-workgroup start / end stamps of wave 0 (slot base: fwd 64, bwd 64 + 2 * 1024)
 #define LY_STAMP(base, k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
     a.prof[(base) + 2 * blockIdx.x + (k)] = wall_clock64(); } while (0)
+// k_lyap_wgrad: per-workgroup stamps of wave 0 (start, staged, MFMA done, end) in a device array
+// read by fiode_debug_wgrad_stamps (tools/probes/wgrad_probe.py)
+__device__ unsigned long long g_wg_stamps[4 * 1024];
+#define WG_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_wg_stamps[4 * blockIdx.x + (k)] = wall_clock64(); } while (0)
 #else
+#define WG_STAMP(k) do { } while (0)
 #define LY_STAMP(base, k) do { } while (0)
 #define LY_T0() do { } while (0)
 #define LY_T(i) do { } while (0)
@@ -663,46 +668,101 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
 
 // Weight gradients.  Workgroup (image b, part p) reduces rows [b*S + p*chunk, ...) of that image.
 // Wave w: dQ2[:, 32w:32w+32] (4 blocks), dQ3[:, 32w:32w+32], dQ1[32w:32w+32, :], db2/db1 slice w.
-__global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
+// The rows are staged WG_CH at a time into LDS by the whole workgroup with every load in flight at
+// once (row pairs loaded one ahead from HBM left the loop load-latency bound: 16 us for the 40
+// rows per image of the train_ode solve); rows past the chunk's end are zero (A and B operands).
+constexpr int WG_CH = 40;       // rows per staged chunk (the RK4 train solve's 40 evals: one chunk)
+constexpr int WG_LD = 160;      // row stride (floats): a row pair's two halves on disjoint banks
+struct WgStage {
+  float gz2[WG_CH][WG_LD], a1[WG_CH][WG_LD], a2[WG_CH][WG_LD], gz1[WG_CH][WG_LD];
+  float gft[WG_CH][12], h[WG_CH][12];
+};
+constexpr size_t WG_LDS = sizeof(WgStage);
+__global__ __launch_bounds__(256, 1) void k_lyap_wgrad(LyapArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  WgStage& S = *reinterpret_cast<WgStage*>(smem);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   const int b = blockIdx.x / a.parts, p = blockIdx.x - b * a.parts;
   const int r0 = b * a.S + p * a.chunk;
   int r1 = min(r0 + a.chunk, (b + 1) * a.S);
   if (a.s_used) r1 = min(r1, b * a.S + a.s_used[0]);      // rows past the device count are not data
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
+  WG_STAMP(0);
   f32x16 acc2[4], acc3 = f16_zero(), acc1 = f16_zero();
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc2[mb] = f16_zero();
   float db2 = 0.f, db1 = 0.f, db3 = 0.f;
-  // the operands of row pair j + 2 are loaded before the MFMAs of pair j (software pipeline: each
-  // pair's 9 global loads otherwise sit in front of its MFMAs -- the loop was load-latency bound)
-  struct Ops { float A2[4], B2, A3, B3, A1, B1; };
-  auto load = [&](int j, Ops& o) {
-    const int jj = j + half;
-    const bool ok = jj < r1;
-    const int js = ok ? jj : r0;
+  for (int c0 = r0; c0 < r1; c0 += WG_CH) {
+    const int n = min(WG_CH, r1 - c0);
+    // stage: 4 arrays x 32 float4 per row + the gft / h rows, every load of the chunk in flight
+    // before the first LDS store (one memory round trip per chunk)
+    constexpr int NV = WG_CH * 128, NVT = (NV + 255) / 256;
+    constexpr int NS = WG_CH * C * 2, NST = (NS + 255) / 256;
+    static_assert(NV % 256 == 0, "each thread stages one array: q = threadIdx.x & 127 for every u");
+    f32x4 v[NVT];
+    float sv[NST];
+    const int qa = threadIdx.x & 127, arr = qa >> 5, k4 = qa & 31;
+    const float* src = arr == 0 ? a.gz2 : arr == 1 ? a.a1 : arr == 2 ? a.a2 : a.gz1;
+    float* dstb = arr == 0 ? &S.gz2[0][0] : arr == 1 ? &S.a1[0][0] : arr == 2 ? &S.a2[0][0] : &S.gz1[0][0];
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) o.A2[mb] = ok ? a.gz2[(size_t)js * M + 32 * mb + col] : 0.f;
-    o.B2 = a.a1[(size_t)js * M + 32 * w + col];
-    o.A3 = (ok && col < C) ? a.gft[(size_t)js * C + col] : 0.f;
-    o.B3 = a.a2[(size_t)js * M + 32 * w + col];
-    o.A1 = ok ? a.gz1[(size_t)js * M + 32 * w + col] : 0.f;
-    o.B1 = col < C ? hsrc[(size_t)js * C + col] : 0.f;
-  };
-  Ops cur;
-  if (r0 < r1) load(r0, cur);
-  for (int j = r0; j < r1; j += 2) {
-    Ops nxt = cur;
-    if (j + 2 < r1) load(j + 2, nxt);
+    for (int u = 0; u < NVT; ++u) {
+      const int r = (threadIdx.x >> 7) + 2 * u;                 // rows past n: row n - 1 loaded, zeroed below
+      v[u] = *reinterpret_cast<const f32x4*>(src + (size_t)(c0 + min(r, n - 1)) * M + 4 * k4);
+    }
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(cur.A2[mb], cur.B2, acc2[mb]);
-    acc3 = mfma32(cur.A3, cur.B3, acc3);
-    acc1 = mfma32(cur.A1, cur.B1, acc1);
-    db2 += (w == 0) ? cur.A2[0] : (w == 1) ? cur.A2[1] : (w == 2) ? cur.A2[2] : cur.A2[3];
-    db1 += cur.A1;
-    db3 += cur.A3;
-    cur = nxt;
+    for (int u = 0; u < NST; ++u) {
+      const int e = threadIdx.x + u * 256;
+      const int r = (e >> 1) / C, c = (e >> 1) - r * C;
+      const int rs = min(r, n - 1);
+      const float t = (e & 1) ? hsrc[(size_t)(c0 + rs) * C + c] : a.gft[(size_t)(c0 + rs) * C + c];
+      sv[u] = (e < NS && r < n) ? t : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NVT; ++u) {
+      const int r = (threadIdx.x >> 7) + 2 * u;
+      *reinterpret_cast<f32x4*>(dstb + r * WG_LD + 4 * k4) = r < n ? v[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < NST; ++u) {
+      const int e = threadIdx.x + u * 256;
+      if (e < NS) {
+        const int r = (e >> 1) / C, c = (e >> 1) - r * C;
+        if (e & 1) S.h[r][c] = sv[u];
+        else S.gft[r][c] = sv[u];
+      }
+    }
+    __syncthreads();
+    WG_STAMP(1);
+    // LDS operands of pair j + 2 read before the MFMAs of pair j (one wave per SIMD: nothing else
+    // hides the LDS latency in front of the dependent MFMAs)
+    struct Ops { float A2[4], B2, A3, B3, A1, B1; };
+    auto rd = [&](int j, Ops& o) {
+      const int jr = j + half;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) o.A2[mb] = S.gz2[jr][32 * mb + col];
+      o.B2 = S.a1[jr][32 * w + col];
+      o.A3 = col < C ? S.gft[jr][col] : 0.f;
+      o.B3 = S.a2[jr][32 * w + col];
+      o.A1 = S.gz1[jr][32 * w + col];
+      o.B1 = col < C ? S.h[jr][col] : 0.f;
+    };
+    Ops cur;
+    rd(0, cur);
+    for (int j = 0; j < n; j += 2) {
+      Ops nxt = cur;
+      if (j + 2 < n) rd(j + 2, nxt);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(cur.A2[mb], cur.B2, acc2[mb]);
+      acc3 = mfma32(cur.A3, cur.B3, acc3);
+      acc1 = mfma32(cur.A1, cur.B1, acc1);
+      db2 += (w == 0) ? cur.A2[0] : (w == 1) ? cur.A2[1] : (w == 2) ? cur.A2[2] : cur.A2[3];
+      db1 += cur.A1;
+      db3 += cur.A3;
+      cur = nxt;
+    }
+    __syncthreads();
   }
+  WG_STAMP(2);
   float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
@@ -722,6 +782,7 @@ __global__ __launch_bounds__(256) void k_lyap_wgrad(LyapArgs a) {
     slab[SLAB_B1 + 32 * w + col] = db1;
     if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
   }
+  WG_STAMP(3);
 }
 
 // Sum of the slabs (fixed order, deterministic) -> dQ2, dQ3, dQ1, db2, db3; per-image g_u;
@@ -837,7 +898,7 @@ struct WsLayout {
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline void parts_for(int B, int S, int& parts, int& chunk) {
   parts = (256 + B - 1) / B;
-  const int maxp = S / 32 > 0 ? S / 32 : 1;
+  const int maxp = S / 16 > 0 ? S / 16 : 1;        // >= 16 rows per part
   if (parts > maxp) parts = maxp;
   if (parts < 1) parts = 1;
   chunk = (S + parts - 1) / parts;
@@ -995,6 +1056,13 @@ extern "C" int fiode_lyap_step(void* stream, const fiode_lyap_config* cfg, const
   return FIODE_OK;
 }
 
+#ifdef OT_PROFILE
+extern "C" FIODE_API int fiode_debug_wgrad_stamps(unsigned long long* host, int n) {
+  if (n > 4 * 1024) n = 4 * 1024;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // ---- shared with the ODE training path (odetrain.hip): weight gradients of rows (b, s) ------
 namespace fiode_internal {
 size_t wgrad_bytes(int B, int S) {
@@ -1019,7 +1087,7 @@ int launch_wgrad(hipStream_t st, const WgradIO& io) {
   a.nslab = a.B * a.parts;
   a.gu_tiles = nullptr;
   a.grads = io.grads;
-  hipLaunchKernelGGL(k_lyap_wgrad, dim3(a.B * a.parts), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_lyap_wgrad, dim3(a.B * a.parts), dim3(256), WG_LDS, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (a.B * M + RED_COLS - 1) / RED_COLS;
   hipLaunchKernelGGL(k_lyap_reduce, dim3(red_blocks), dim3(256), 0, st, a);
