@@ -13,14 +13,14 @@ import bench  # noqa: E402
 from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
 
 
-def run(split: bool, solver: str, steps: int = 30):
+def run(split: bool, solver: str, steps: int = 30, B: int = 128, S: int = bench.H_SAMPLE):
     dev = torch.device("cuda:0")
-    mod = bench.build_module(dev, seed=0, train_ode=True, solver=solver)
+    mod = bench.build_module(dev, seed=0, train_ode=True, solver=solver, h_sample=S)
     mod.seed = 1000
     opt = mod.configure_optimizers(capturable=True)[0][0]
     g = torch.Generator(device="cpu").manual_seed(1234)
-    x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
-    y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    x = torch.rand(B, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (B,), generator=g).to(dev)
     gs = GraphTrainStep(mod, opt, x, y, split=split)
     print(f"== split={gs.split} solver={solver}", flush=True)
     prev = 0
@@ -37,13 +37,17 @@ def run(split: bool, solver: str, steps: int = 30):
         pl = mod.last_plan
         yh = pl.get("y_hat")
         yl = float(yh.gather(1, y[:, None]).min()) if yh is not None else float("nan")
+        nneg = int((yh.gather(1, y[:, None]) <= 0).sum()) if yh is not None else -1
         print(f"step {i:2d} loss {float(loss):.6f} lyap {float(pl['scalars'][0]):.6f} ode "
-              f"{float(pl['loss_ode']) if 'loss_ode' in pl else float('nan'):.6f} min y_hat[label] {yl:.3e} "
+              f"{float(pl['loss_ode']) if 'loss_ode' in pl else float('nan'):.6f} min y_hat[label] {yl:.3e} (<= 0: {nneg}) "
               f"ms {dt:7.2f} stats {st} status_word {None if sw is None else int(sw[0])} skipped {sk}{flag}",
               flush=True)
     gs.close()
 
 
 if __name__ == "__main__":
-    for split in (True, False):
-        run(split, "dopri5")
+    if "--large" in sys.argv:                 # configs[4]'s shape: B=1024 x S=1024
+        run(False, "dopri5", steps=8, B=1024, S=1024)
+    else:
+        for split in (True, False):
+            run(split, "dopri5")
