@@ -158,8 +158,11 @@ __device__ __forceinline__ void and_by_batch(const CertArgs& a, int batch, bool 
 }
 
 // Two workgroups per CU (LDS: the Q2 image + Q3's C rows, 72.9 KB each; <= 256 registers): the
-// two waves of a SIMD run many tiles each and drift apart, so one wave's QP / barrier VALU work
-// overlaps the other's MFMAs (one resident workgroup per CU left the matrix pipe idle during them).
+// two waves of a SIMD run many tile pairs each and drift apart, so one wave's QP / barrier VALU
+// work overlaps the other's MFMAs (one resident workgroup per CU left the matrix pipe idle during
+// them).  A wave takes two consecutive 32-row tiles: both MLPs (dropout off: plain relu), then one
+// QP per lane -- lanes 0..31 the first tile's rows, 32..63 the second's (a 32x32 accumulator tile
+// leaves each row's outputs on both lane halves, so a wave per tile ran every row's QP twice).
 __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
@@ -173,24 +176,36 @@ __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
 #pragma unroll
     for (int s = 0; s < 5; ++s) q1[mb][s] = a.Q1[(32 * mb + col) * C + 2 * s + half];
   const uint32_t kw[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  const uint32_t ntiles = (a.G + 31) / 32;
+  const uint32_t npairs = (a.G + 63) / 64;
   int cur_b = -1;                    // the batch whose AND this wave accumulates (wave-uniform)
   uint32_t cur_and = 0xFFFFFFFFu;
-  for (uint32_t tile = blockIdx.x * FIODE_WAVES + wave; tile < ntiles; tile += gridDim.x * FIODE_WAVES) {
-    const uint32_t row = tile * 32 + col;
+  for (uint32_t pair = blockIdx.x * FIODE_WAVES + wave; pair < npairs; pair += gridDim.x * FIODE_WAVES) {
+    float h[C] = {}, ft[C] = {};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t rt = pair * 64 + 32 * t + col;          // row of tile t on this lane (both halves)
+      const uint32_t rrt = rt < a.G ? rt : a.G - 1;
+      float ht[C];
+      eta_row(a, rrt, ht);
+      f32x16 z1[4], z2[4];
+      const f32x16 z3 = mlp_tile<false>(Q2s, Q3s, q1, a.u, a.b2, a.b3, ht, kw, kw, 1.0f, col, half, z1, z2);
+      float ftt[C];
+      gather_ft(z3, half, ftt);
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        h[j] = (t == half) ? ht[j] : h[j];
+        ft[j] = (t == half) ? ftt[j] : ft[j];
+      }
+    }
+    const uint32_t row = pair * 64 + lane;                     // this lane's row in the QP phase
     const bool valid = row < a.G;
     const uint32_t rr = valid ? row : a.G - 1;
-    float h[C];
-    eta_row(a, rr, h);
-    f32x16 z1[4], z2[4];
-    const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u, a.b2, a.b3, h, kw, kw, 1.0f, col, half, z1, z2);
-    float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-    gather_ft(z3, half, ft);
+    float lower[C], nominal[C], sig[C], span[C], v[C], mu;
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
     const uint32_t conv = qp_bisect(lower, nominal, a.d.max_iter - 1, a.d.tol, v, mu);
     const int bt = batch_of(a, rr);
     const int b_first = __shfl(bt, 0, 64), b_last = __shfl(bt, 63, 64);
-    if (b_first == b_last) {          // the whole tile in one batch (all but a few boundary tiles)
+    if (b_first == b_last) {          // the whole pair in one batch (all but a few boundary pairs)
       if (b_first != cur_b) {
         if (cur_b >= 0 && (threadIdx.x & 63) == 0) atomicAnd(a.words + cur_b, cur_and);
         cur_b = b_first;
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
     } else {
       and_by_batch(a, bt, valid, conv);
     }
-    if (valid && half == 0) store_row10(a.ft + (size_t)row * C, ft);
+    if (valid) store_row10(a.ft + (size_t)row * C, ft);
   }
   if (cur_b >= 0 && (threadIdx.x & 63) == 0) atomicAnd(a.words + cur_b, cur_and);
 }
@@ -398,8 +413,8 @@ extern "C" int fiode_certify(void* stream, const fiode_certify_config* cfg, cons
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_cert_prep, dim3(1), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
-  const uint32_t ntiles = (a.G + 31) / 32;
-  uint32_t blocks = (ntiles + FIODE_WAVES - 1) / FIODE_WAVES;
+  const uint32_t npairs = (a.G + 63) / 64;
+  uint32_t blocks = (npairs + FIODE_WAVES - 1) / FIODE_WAVES;
   // persistent: two workgroups per CU, each loading the weight images once
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_dyn_fwd(DynEvalArgs a) {
     float h[C];
     load_row10(a.h + (size_t)rr * C, h);
     f32x16 z1[4], z2[4];
-    const f32x16 z3 = mlp_tile(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw, kw, 1.0f, col, half, z1, z2);
+    const f32x16 z3 = mlp_tile<false>(Q2s, Q3s, q1, a.u + (size_t)b * M, a.b2, a.b3, h, kw, kw, 1.0f, col, half, z1, z2);
     float ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
     gather_ft(z3, half, ft);
     barrier_nominal(a.d, h, ft, lower, nominal, sig, span);

@@ -23,12 +23,18 @@ __device__ __forceinline__ void store_row10(float* p, const float (&v)[C]) {
   for (int j = 0; j < 5; ++j) q[j] = make_float2(v[2 * j], v[2 * j + 1]);
 }
 
-// relu(dropout(z)) on one accumulator tile, in place (classification.py:98,100)
+// relu(dropout(z)) on one accumulator tile, in place (classification.py:98,100); DROP = false:
+// plain relu (dropout off: keep = 1, scale = 1 -- the same values, without the per-element mask work)
+template <bool DROP = true>
 __device__ __forceinline__ void dropout_relu(f32x16& z, uint32_t kw, int half, float scale) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const bool keep = (kw >> acc_row(r, half)) & 1u;
-    z[r] = keep ? fmaxf(z[r] * scale, 0.f) : 0.f;
+    if (DROP) {
+      const bool keep = (kw >> acc_row(r, half)) & 1u;
+      z[r] = keep ? fmaxf(z[r] * scale, 0.f) : 0.f;
+    } else {
+      z[r] = fmaxf(z[r], 0.f);
+    }
   }
 }
 
@@ -64,6 +70,7 @@ __device__ __forceinline__ void gather_ft(const f32x16& z3, int half, float (&ft
 
 // Layers 1-2 of the MLP of one wave tile: z1/z2 become the post-dropout-ReLU activations a1^T,
 // a2^T.  q1: hoisted layer-1 A operands.
+template <bool DROP = true>
 __device__ __forceinline__ void mlp12_tile(const float* Q2s, const float (&q1)[4][5], const float* u_row,
                                            const float* b2, const float (&h)[C], const uint32_t (&kw1)[4],
                                            const uint32_t (&kw2)[4], float scale, int col, int half, f32x16 (&z1)[4],
@@ -78,7 +85,7 @@ __device__ __forceinline__ void mlp12_tile(const float* Q2s, const float (&q1)[4
     for (int mb = 0; mb < 4; ++mb) z1[mb] = mfma32(q1[mb][s], bs, z1[mb]);
   }
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) dropout_relu(z1[mb], kw1[mb], half, scale);
+  for (int mb = 0; mb < 4; ++mb) dropout_relu<DROP>(z1[mb], kw1[mb], half, scale);
   // layer 2: z2 = b2 + Q2 a1
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) load_acc_rows(b2, mb, half, z2[mb]);
@@ -95,15 +102,16 @@ __device__ __forceinline__ void mlp12_tile(const float* Q2s, const float (&q1)[4
     __builtin_amdgcn_sched_barrier(0);   // bound the LDS-read hoisting window to one k-block
   }
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) dropout_relu(z2[mb], kw2[mb], half, scale);
+  for (int mb = 0; mb < 4; ++mb) dropout_relu<DROP>(z2[mb], kw2[mb], half, scale);
 }
 
 // The MLP of one wave tile: layers 1-3, returns the layer-3 accumulator (mlp12_tile + layer 3).
+template <bool DROP = true>
 __device__ __forceinline__ f32x16 mlp_tile(const float* Q2s, const float* Q3s, const float (&q1)[4][5],
                                            const float* u_row, const float* b2, const float* b3,
                                            const float (&h)[C], const uint32_t (&kw1)[4], const uint32_t (&kw2)[4],
                                            float scale, int col, int half, f32x16 (&z1)[4], f32x16 (&z2)[4]) {
-  mlp12_tile(Q2s, q1, u_row, b2, h, kw1, kw2, scale, col, half, z1, z2);
+  mlp12_tile<DROP>(Q2s, q1, u_row, b2, h, kw1, kw2, scale, col, half, z1, z2);
   // layer 3: z3 = b3 + Q3 a2 (rows >= 10 of the 32-row tile are zero weights)
   f32x16 z3;
 #pragma unroll
