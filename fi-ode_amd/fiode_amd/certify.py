@@ -53,8 +53,13 @@ def certify_lipschitz(module, images: torch.Tensor, labels: torch.Tensor, T: int
         for i in idx:
             image = images[i:i + 1]
             label = int(labels[i])
-            net_out = module(image)
-            static_state, _ = module.init_coordinates(image, dyn)
+            # the reference runs module(image) and then init_coordinates(image) again
+            # (certify_lipschitz.py:111-113); the backbone is deterministic in eval mode, so its
+            # features are computed once and the validation solve starts from them
+            static_state, state = module.init_coordinates(image, dyn)
+            ts = torch.linspace(0.0, module.t_max, 2, device=dev)
+            sol = module.model.integrate_from(static_state, state, ts=ts, int_params=module.val_solver_params)
+            net_out = module.model.output_fun(sol)[-1]
             out, _ = ops.certify_image(static_state.float().reshape(-1), label, grid, w, cfg, T=T, batches=batches,
                                        eps=eps, min_std=min_std)
             o = out.cpu()

@@ -160,5 +160,13 @@ class IVP(nn.Module):
         ts = self.ts if ts is None else ts
         int_params = dict(rtol=self.ode_tol, atol=self.ode_tol) if int_params is None else dict(int_params)
         static_state, state = self.init_coordinates(x, self.dyn_fun)
+        return self.integrate_from(static_state, state, ts=ts, int_params=int_params)
+
+    def integrate_from(self, static_state, state, ts=None, int_params=None):
+        """`integrate` from init_coordinates' outputs already in hand (the backbone is deterministic:
+        a caller that needs both the features and the solve runs the backbone once)."""
+        from .odeint import odeint
+        ts = self.ts if ts is None else ts
+        int_params = dict(rtol=self.ode_tol, atol=self.ode_tol) if int_params is None else dict(int_params)
         self.dyn_fun.static_state = static_state
         return odeint(self.h_dot, state, ts, **int_params)

@@ -77,3 +77,7 @@ def test_certify_driver_through_module():
     res = certify_lipschitz(mod, x, y, T=12, batches=10)
     assert res.n_images == 3 and len(res.max_violations) == 3
     assert all(np.isfinite(res.max_violations))
+    # the accuracy count from the features computed once = the reference's module(image) call
+    with torch.no_grad():
+        ref = sum(int(int(mod(x[i:i + 1]).argmax(-1)) == int(y[i])) for i in range(3))
+    assert res.correct == ref
