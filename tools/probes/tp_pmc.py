@@ -1,6 +1,7 @@
 """The throughput kernels once each, for rocprofv3 --pmc passes (not a test): 3 fused fan-out
-steps at the bench shape (k_lyap_fwd / k_lyap_bwd) and one certification image on the T=40 grid
-(k_cert_fwd / k_cert_final)."""
+steps at the bench shape (k_lyap_fwd / k_lyap_bwd), one at configs[4]'s B=1024 x S=1024 (the
+dispatches with the larger grid) and one certification image on the T=40 grid (k_cert_fwd /
+k_cert_final)."""
 import pathlib
 import sys
 
@@ -22,6 +23,9 @@ y = torch.randint(0, 10, (B,), generator=g).to(dev)
 dyn = ops.DynCfg(scale_nominal=False, dropout=0.5)
 for r in range(3):
     ops.lyap_step(feat, y, w, dyn, sample_size=S, n_uniform=204, offset=r)
+fl = torch.randn(1024, 10, generator=g).to(dev)
+yl = torch.randint(0, 10, (1024,), generator=g).to(dev)
+ops.lyap_step(fl, yl, w, dyn, sample_size=1024, n_uniform=816, offset=7)
 grid = ops.certify_grid(40, device=dev)
 ops.certify_image(torch.randn(10, generator=g).to(dev), 3, grid, w, ops.DynCfg(scale_nominal=False, dropout=0.0),
                   T=40, batches=10)
