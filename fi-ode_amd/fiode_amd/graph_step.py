@@ -355,7 +355,7 @@ class GraphTrainStep:
             lo = loss.detach().reshape(1)
             self._mine = StepGuard(loss=lo if lo.dtype == torch.float32 else None,
                                    status=m.status_words() if hasattr(m, "status_words") else [])
-        loss.backward()
+        loss.backward(self._unit_grad(loss))
         m.rng_counter.add_(1)
         return loss
 
@@ -482,13 +482,27 @@ class GraphTrainStep:
             self.reducer.arm(self.world, self.comm_stream, force=self.force_comm)
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         self._arm_guard(loss)
-        loss.backward()
+        loss.backward(self._unit_grad(loss))
         if overlap:
             self.reducer.finish()                 # the last buckets, join the comm stream, 1/world
         elif self.comm != "none":
             self.reducer.gather()                 # one multi-tensor copy into the flat bucket
         m.rng_counter.add_(1)
         return loss
+
+    def _unit_grad(self, loss):
+        """The backward seed d loss / d loss = 1 as a fixed tensor made outside the capture and marked
+        (lyapunov.UNIT_GRAD), so the captured step has no fill kernel for it and the fused loss node
+        skips its scaling by it."""
+        from .lyapunov import UNIT_GRAD
+        u = getattr(self, "_unit", None)
+        if u is None or u.device != loss.device or u.dtype != loss.dtype:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("GraphTrainStep: the unit gradient seed must exist before the capture")
+            u = torch.ones((), dtype=loss.dtype, device=loss.device)
+            setattr(u, UNIT_GRAD, True)
+            self._unit = u
+        return u
 
     def _arm_guard(self, loss):
         """Point the optimizer's step guard at this step's loss and solve status words (they are new

@@ -140,6 +140,10 @@ class ODELossMixFn(torch.autograd.Function):
         return go * (1.0 - ctx.p), gunit * go, None, None
 
 
+# attribute GraphTrainStep sets on the gradient seed it passes to backward(): a float32 scalar 1.0
+UNIT_GRAD = "_fiode_unit_grad"
+
+
 class LyapODELossFn(torch.autograd.Function):
     """The configs[1] training loss as ONE autograd node (pl_modules.py:444-500): the fused
     Lyapunov step, the train_ode RK4 solve (launched first on ``ode_stream`` when given, so it
@@ -197,13 +201,19 @@ class LyapODELossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, go):
+        # ode + lyap * ((1 - p) go), summed as autograd's three-node graph sums it (bit for bit,
+        # tests/test_gpu_odetrain.py); when go is GraphTrainStep's unit seed (``UNIT_GRAD``, exactly
+        # 1.0) the products by go are exact and skipped, and (1 - p) is a host scalar: on the captured
+        # step's critical path that drops three small kernels (the seed's ones fill, gunit * go,
+        # go * (1 - p)) in front of / behind the solve's backward
         gunit, xo, w, oplan, ws = ctx.ode
         ctx.ode = None
-        g_y = gunit * go
+        unit = getattr(go, UNIT_GRAD, False)
+        g_y = gunit if unit else gunit * go
         gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
         keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         ode = [gr[k] for k in keys]
-        lyap = torch._foreach_mul(ctx.lyap, go * (1.0 - ctx.p))
+        lyap = torch._foreach_mul(ctx.lyap, (1.0 - ctx.p) if unit else go * (1.0 - ctx.p))
         ctx.lyap = None
         if ctx.split:     # the solve's features are another tensor: its gradient goes there
             torch._foreach_add_(ode[1:], lyap[1:])

@@ -105,10 +105,32 @@ def seed1000(m):
     m.seed = 1000
 
 
+def old_seed(m):
+    """The round-3 fused-loss backward: loss.backward() (a ones fill), g_y = gunit * go,
+    lyap * (go * (1 - p)) and a separate add -- for the A/B of the unit-seed backward."""
+    from fiode_amd import graph_step as GS, lyapunov as LY, ops
+
+    def old_backward(ctx, go):
+        gunit, xo, w, oplan, ws = ctx.ode
+        ctx.ode = None
+        gr, _ = ops.odetrain_backward(gunit * go, xo, w, oplan["dyn"], oplan["cfg"], ws)
+        keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+        ode = [gr[k] for k in keys]
+        lyap = torch._foreach_mul(ctx.lyap, go * (1.0 - ctx.p))
+        ctx.lyap = None
+        torch._foreach_add_(ode, lyap)
+        return (ode[0], None) + tuple(ode[1:]) + (None, None, None, None, None, None)
+    nb, ug = LY.LyapODELossFn.backward, GS.GraphTrainStep._unit_grad
+    LY.LyapODELossFn.backward = staticmethod(old_backward)
+    GS.GraphTrainStep._unit_grad = lambda self, loss: None
+    RESTORE.append(lambda: setattr(LY.LyapODELossFn, "backward", staticmethod(nb)))
+    RESTORE.append(lambda: setattr(GS.GraphTrainStep, "_unit_grad", ug))
+
+
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
        "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
-       "split": split, "split_serial": split_serial}
+       "split": split, "split_serial": split_serial, "old_seed": old_seed}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
