@@ -686,6 +686,20 @@ class _SpectralConvFn(torch.autograd.Function):
 
 _SPECTRAL_GRAD_WEIGHTS = {}
 
+# The conv layers' map-ahead work (map backward, early update, refresh) runs on one stream per layer
+# (False) or on one stream shared by all layers (True; tools/ab_step.py conv_one_stream).
+CONV_STREAM_SHARED = False
+_CONV_STREAMS = {}
+
+
+def _conv_map_stream(device) -> "torch.cuda.Stream":
+    if not CONV_STREAM_SHARED:
+        return torch.cuda.Stream(device)
+    key = str(device)
+    if key not in _CONV_STREAMS:
+        _CONV_STREAMS[key] = torch.cuda.Stream(device)
+    return _CONV_STREAMS[key]
+
 
 class CayleyConv(nn.Conv2d):
     """Orthogonal circular convolution parametrised per frequency: for each of the n*(n/2+1)
@@ -757,8 +771,7 @@ class CayleyConv(nn.Conv2d):
             return False
         from . import ops
         Q, inv, ws = ops.spectral_cayley_forward(self.weight.detach(), self.alpha.detach(), self._n)
-        self._store = {"Q": Q, "inv": inv, "ws": ws, "n": self._n,
-                       "stream": torch.cuda.Stream(self.weight.device)}
+        self._store = {"Q": Q, "inv": inv, "ws": ws, "n": self._n, "stream": _conv_map_stream(self.weight.device)}
         return True
 
     def pipeline_off(self) -> None:

@@ -105,6 +105,12 @@ def seed1000(m):
     m.seed = 1000
 
 
+def conv_one_stream(m):
+    from fiode_amd import cayley as CY
+    CY.CONV_STREAM_SHARED = True          # read when GraphTrainStep turns the maps-ahead pipeline on
+    RESTORE.append(lambda: setattr(CY, "CONV_STREAM_SHARED", False))
+
+
 def old_seed(m):
     """The round-3 fused-loss backward: loss.backward() (a ones fill), g_y = gunit * go,
     lyap * (go * (1 - p)) and a separate add -- for the A/B of the unit-seed backward."""
@@ -130,7 +136,8 @@ def old_seed(m):
 ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
        "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
-       "split": split, "split_serial": split_serial, "old_seed": old_seed}
+       "split": split, "split_serial": split_serial, "old_seed": old_seed,
+       "conv_one_stream": conv_one_stream}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
