@@ -115,13 +115,13 @@ __global__ void __launch_bounds__(256) k_panel_pad(int n, int np, const float* _
 
 typedef fiode_gjb::GJB<PB, 8> PivotGJ;
 __global__ void __launch_bounds__(PivotGJ::NT) k_panel_pivot(int np, int k0, const float* __restrict__ X,
-                                                            float* __restrict__ P, int64_t wstride,
+                                                            int64_t xstride, float* __restrict__ P, int64_t wstride,
                                                             const int32_t* __restrict__ skip) {
   if (skip && *skip) return;
   extern __shared__ __attribute__((aligned(16))) char piv_smem[];
   PivotGJ::Smem& sm = *reinterpret_cast<PivotGJ::Smem*>(piv_smem);
   const int64_t m = blockIdx.x;
-  PivotGJ::load(sm, X + m * wstride + (int64_t)k0 * np + k0, PB, np);
+  PivotGJ::load(sm, X + m * xstride + (int64_t)k0 * np + k0, PB, np);
   __syncthreads();
   PivotGJ::invert(sm);
   PivotGJ::store(sm, P + m * wstride, PB, PB);
@@ -172,7 +172,7 @@ __device__ __forceinline__ void tile_load(float (*dst)[LDT], const float* __rest
 typedef fiode_gjb::GJB<PB, 4> UpdGJ;
 static_assert(sizeof(UpdGJ::Smem) <= 3 * PB * LDT * sizeof(float), "pivot scratch fits the update's LDS");
 
-__global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X,
+__global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const float* __restrict__ X, int64_t xstride,
                                                       const float* __restrict__ P, float* __restrict__ Y,
                                                       float* __restrict__ final_out, int n, int64_t wstride,
                                                       float* __restrict__ P_next, const int32_t* __restrict__ skip) {
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
   const int ib = blockIdx.x * PB, jb = blockIdx.y * PB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
   const int64_t m = blockIdx.z;
-  X += m * wstride;
+  X += m * xstride;
   P += m * wstride;
   Y += m * wstride;
   if (P_next) P_next += m * wstride;
@@ -286,19 +286,27 @@ extern "C" int fiode_block_inverse_cond(void* stream, int32_t batch, int32_t n, 
   float* A = (float*)workspace;
   float* B = A + (size_t)np * np;
   float* Pb[2] = {B + (size_t)np * np, B + (size_t)np * np + (size_t)PB * PB};
-  hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256), (unsigned)batch), dim3(256), 0, st,
-                     n, np, in, A, wstride, skip);
+  // n a multiple of 64 (the 512 x 512 and 128 x 128 systems): the first panel step reads the caller's
+  // matrix in place (row stride n = np, matrices n * n apart) -- no padding copy, one launch fewer
+  // on the dense maps' forward chain; otherwise it reads the I-padded copy in A
+  const bool direct = np == n && (nb > 1 || out != in);     // (one step writing `out` must not read it)
+  if (!direct)
+    hipLaunchKernelGGL(k_panel_pad, dim3((unsigned)(((int64_t)np * np + 255) / 256), (unsigned)batch), dim3(256), 0,
+                       st, n, np, in, A, wstride, skip);
+  const float* X = direct ? in : A;
+  int64_t xstride = direct ? (int64_t)n * n : wstride;
   // the first pivot block on its own; every later one is inverted by the previous update (look-ahead)
-  hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, 0, A,
-                     Pb[0], wstride, skip);
+  hipLaunchKernelGGL(k_panel_pivot, dim3((unsigned)batch), dim3(PivotGJ::NT), sizeof(PivotGJ::Smem), st, np, 0, X,
+                     xstride, Pb[0], wstride, skip);
+  float* Yb[2] = {B, A};                      // ping-pong: a step never writes the matrix it reads
   for (int kb = 0; kb < nb; ++kb) {
     const int k0 = kb * PB;
     const bool last = kb == nb - 1;
-    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, A, Pb[kb & 1], B,
-                       last ? out : nullptr, n, wstride, last ? nullptr : Pb[(kb + 1) & 1], skip);
-    float* t = A;
-    A = B;
-    B = t;
+    float* Y = Yb[kb & 1];
+    hipLaunchKernelGGL(k_panel_update, dim3(nb, nb, (unsigned)batch), dim3(256), 0, st, np, k0, X, xstride,
+                       Pb[kb & 1], Y, last ? out : nullptr, n, wstride, last ? nullptr : Pb[(kb + 1) & 1], skip);
+    X = Y;
+    xstride = wstride;
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
