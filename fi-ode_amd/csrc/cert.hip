@@ -85,6 +85,7 @@ struct CertArgs {
   uint32_t G, ebs;
   int nb, label, T;
   float eps_g, dist, kappa, sqrt_n, sa, sqrt2;
+  float etab[MAXT + 1];   // float32(v / T) for the counts v = 0..T (double quotient, host-rounded)
   DynScalars d;
   const float* x_feat;
   const uint8_t* grid;
@@ -110,12 +111,17 @@ __device__ __forceinline__ int batch_of(const CertArgs& a, uint32_t r) {
   return (int)(b < (uint32_t)(a.nb - 1) ? b : (uint32_t)(a.nb - 1));
 }
 
-// eta row: float32(v / T) with the label's column swapped with column 0 (eval_utils.py:64-69)
-__device__ __forceinline__ void eta_row(const CertArgs& a, uint32_t r, float (&h)[C]) {
+// eta row: float32(v / T) with the label's column swapped with column 0 (eval_utils.py:64-69);
+// the T + 1 possible values come from a table in LDS (stage_etab) -- the per-element float64
+// division they replace was ~14 f64 instructions per value
+__device__ __forceinline__ void stage_etab(const CertArgs& a, float* tab) {
+  for (int v = threadIdx.x; v <= a.T; v += blockDim.x) tab[v] = a.etab[v];
+}
+__device__ __forceinline__ void eta_row(const CertArgs& a, const float* tab, uint32_t r, float (&h)[C]) {
   const uint8_t* g = a.grid + (size_t)r * C;
   float v[C];
 #pragma unroll
-  for (int j = 0; j < C; ++j) v[j] = (float)((double)g[j] / (double)a.T);
+  for (int j = 0; j < C; ++j) v[j] = tab[g[j]];
   float v0 = v[0], vl = v[0];
 #pragma unroll
   for (int j = 0; j < C; ++j) vl = (j == a.label) ? v[j] : vl;
@@ -167,7 +173,9 @@ __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Q2s = smem;
   float* Q3s = smem + M * LDQ;
+  float* tab = smem + (M + C) * LDQ;
   load_weight_images(a.Q2, a.Q3, Q2s, Q3s, C);
+  stage_etab(a, tab);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
   float q1[4][5];
@@ -186,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
       const uint32_t rt = pair * 64 + 32 * t + col;          // row of tile t on this lane (both halves)
       const uint32_t rrt = rt < a.G ? rt : a.G - 1;
       float ht[C];
-      eta_row(a, rrt, ht);
+      eta_row(a, tab, rrt, ht);
       f32x16 z1[4], z2[4];
       const f32x16 z3 = mlp_tile<false>(Q2s, Q3s, q1, a.u, a.b2, a.b3, ht, kw, kw, 1.0f, col, half, z1, z2);
       float ftt[C];
@@ -221,9 +229,10 @@ __global__ __launch_bounds__(256, 2) void k_cert_fwd(CertArgs a) {
 }
 
 // one row: the violation and violation_larger_T of grid row rr (certify_lipschitz.py:120-136)
-__device__ __forceinline__ void cert_row(const CertArgs& a, uint32_t rr, int b, float& viol, float& violT) {
+__device__ __forceinline__ void cert_row(const CertArgs& a, const float* tab, uint32_t rr, int b, float& viol,
+                                         float& violT) {
   float h[C], ft[C], lower[C], nominal[C], sig[C], span[C], v[C], mu;
-  eta_row(a, rr, h);
+  eta_row(a, tab, rr, h);
   load_row10(a.ft + (size_t)rr * C, ft);
   barrier_nominal(a.d, h, ft, lower, nominal, sig, span);
   qp_bisect(lower, nominal, qp_exit_iter(a.words[b], a.d.max_iter), a.d.tol, v, mu);
@@ -270,6 +279,9 @@ __device__ __forceinline__ void max_by_batch(const CertArgs& a, int b, bool vali
 // Persistent grid-stride loop over the rows (one row per lane per pass); each lane keeps the
 // running maxima of the batch its wave is in, flushed when the wave moves on (see and_by_batch).
 __global__ __launch_bounds__(256) void k_cert_final(CertArgs a) {
+  __shared__ float tab[MAXT + 1];
+  stage_etab(a, tab);
+  __syncthreads();
   int cur_b = -1;
   float acc0 = -INFINITY, acc1 = -INFINITY;
   auto flush = [&]() {
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(256) void k_cert_final(CertArgs a) {
     const uint32_t rr = valid ? r : a.G - 1;
     const int b = batch_of(a, rr);
     float viol, violT;
-    cert_row(a, rr, b, viol, violT);
+    cert_row(a, tab, rr, b, viol, violT);
     const int b_first = __shfl(b, 0, 64), b_last = __shfl(b, 63, 64);
     if (b_first == b_last && __all(valid)) {
       if (b_first != cur_b) {
@@ -391,6 +403,8 @@ extern "C" int fiode_certify(void* stream, const fiode_certify_config* cfg, cons
   a.nb = cfg->batches + ((G % cfg->batches) != 0 ? 1 : 0);
   a.label = cfg->label;
   a.T = cfg->T;
+  if (cfg->T > MAXT) return FIODE_EINVAL;
+  for (int v = 0; v <= cfg->T; ++v) a.etab[v] = (float)((double)v / (double)cfg->T);
   a.eps_g = (float)(1.0 / cfg->T);                                   // certify_lipschitz.py:78
   a.dist = (float)(sqrt((double)C) / cfg->T);                        // :81
   const double lfx = (dyn->scale_nominal ? (double)dyn->alpha_1 : 1.0) / (double)cfg->min_std;   // :67-70
@@ -421,7 +435,7 @@ extern "C" int fiode_certify(void* stream, const fiode_certify_config* cfg, cons
     ncu = 256;
   const uint32_t cap = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(k_cert_fwd, dim3(blocks), dim3(256), (size_t)(M + C) * LDQ * sizeof(float), st, a);
+  hipLaunchKernelGGL(k_cert_fwd, dim3(blocks), dim3(256), ((size_t)(M + C) * LDQ + MAXT + 1) * sizeof(float), st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   uint32_t fblocks = (a.G + 255) / 256;
   if (fblocks > 8u * (uint32_t)ncu) fblocks = 8u * (uint32_t)ncu;      // persistent: 8 workgroups per CU
