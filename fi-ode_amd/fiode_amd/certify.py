@@ -34,6 +34,16 @@ def image_shard(n_images: int, rank: int, world: int) -> range:
     return range(lo, min(n_images, lo + per))
 
 
+def _record_stream(x, stream) -> None:
+    """record_stream on every tensor of a (nested) tuple / list: the caching allocator keeps them
+    until `stream` is done with them."""
+    if torch.is_tensor(x):
+        x.record_stream(stream)
+    elif isinstance(x, (tuple, list)):
+        for t in x:
+            _record_stream(t, stream)
+
+
 def certify_lipschitz(module, images: torch.Tensor, labels: torch.Tensor, T: int = 40, batches: int = 10,
                       eps: float = 0.141, grid: Optional[torch.Tensor] = None, indices=None) -> CertifyResult:
     """certify_lipschitz.py:97-143 for the given images (module in eval mode, no dropout)."""
@@ -45,27 +55,50 @@ def certify_lipschitz(module, images: torch.Tensor, labels: torch.Tensor, T: int
     min_std = float(norm.std.min()) if getattr(norm, "std", None) is not None else 1.0
     res = CertifyResult()
     module.eval()
-    idx = range(images.shape[0]) if indices is None else indices
+    idx = list(range(images.shape[0]) if indices is None else indices)
+    labels_h = labels.detach().cpu() if labels.is_cuda else labels       # one host read for all labels
+    # The certification kernels of image i run on the current stream while the host is already
+    # launching image i + 1's; the validation solve (the accuracy count) runs on a side stream, whose
+    # status read (odeint: one host read per solve, as torchdiffeq raises) waits for that stream only,
+    # and every result is read once after the loop -- no host round trip between images.
+    main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    side = torch.cuda.Stream(dev) if main is not None else None
+    pending = []
     with torch.no_grad():
         w = {k: v.detach().float().contiguous() for k, v in dyn.effective_weights().items()}
         cfg = dyn.dyn_cfg()
         cfg.dropout = 0.0
+        ts = torch.linspace(0.0, module.t_max, 2, device=dev)
         for i in idx:
             image = images[i:i + 1]
-            label = int(labels[i])
+            label = int(labels_h[i])
             # the reference runs module(image) and then init_coordinates(image) again
             # (certify_lipschitz.py:111-113); the backbone is deterministic in eval mode, so its
             # features are computed once and the validation solve starts from them
             static_state, state = module.init_coordinates(image, dyn)
-            ts = torch.linspace(0.0, module.t_max, 2, device=dev)
-            sol = module.model.integrate_from(static_state, state, ts=ts, int_params=module.val_solver_params)
-            net_out = module.model.output_fun(sol)[-1]
+            feats = torch.cuda.Event() if main is not None else None
+            if feats is not None:
+                feats.record(main)
             out, _ = ops.certify_image(static_state.float().reshape(-1), label, grid, w, cfg, T=T, batches=batches,
                                        eps=eps, min_std=min_std)
+            if side is not None:
+                side.wait_event(feats)
+                _record_stream((static_state, state), side)
+                with torch.cuda.stream(side):
+                    sol = module.model.integrate_from(static_state, state, ts=ts, int_params=module.val_solver_params)
+                    hit = module.model.output_fun(sol)[-1].argmax(-1) == label
+                hit.record_stream(main)
+            else:
+                sol = module.model.integrate_from(static_state, state, ts=ts, int_params=module.val_solver_params)
+                hit = module.model.output_fun(sol)[-1].argmax(-1) == label
+            pending.append((i, out, hit))
+        if main is not None:
+            main.wait_stream(side)
+        for i, out, hit in pending:
             o = out.cpu()
             vmax, vtmax = float(o[:, 0].max()), float(o[:, 1].max())
             res.n_images += 1
-            res.correct += int(int(net_out.argmax(-1)) == label)
+            res.correct += int(hit.item())
             res.max_violations.append(vmax)
             if vmax < 0:
                 res.certified += 1
