@@ -20,14 +20,14 @@ from . import _lib as L
 
 class AbstractScheduler:
     def sampler_weight(self, epoch_num):
-        raise NotImplementedError("[ERROR] Not Implemented")
+        raise NotImplementedError(f"{type(self).__name__} defines no schedule value")
 
 
 class LinearScheduler(AbstractScheduler):
     """sampler_schedulers.py:14-38."""
 
     def __init__(self, rate, bias=0.0, clamp="min", clamp_val=0.0, start=0):
-        assert clamp_val >= 0, "Schedulers must return positive number"
+        assert clamp_val >= 0, "a schedule value below zero"
         self.rate, self.bias, self.clamp, self.clamp_val, self.start = rate, bias, clamp, clamp_val, start
 
     def sampler_weight(self, epoch_num):
@@ -43,7 +43,7 @@ class ConstantScheduler(AbstractScheduler):
     """sampler_schedulers.py:41-48."""
 
     def __init__(self, constant):
-        assert constant >= 0, "Schedulers must return positive number"
+        assert constant >= 0, "a schedule value below zero"
         self.constant = constant
 
     def sampler_weight(self, epoch_num):
@@ -54,7 +54,7 @@ class SwitchScheduler(AbstractScheduler):
     """sampler_schedulers.py:50-63."""
 
     def __init__(self, start, end, trigger):
-        assert start >= 0 and end >= 0, "Schedulers must return positive number"
+        assert start >= 0 and end >= 0, "a schedule value below zero"
         self.start, self.end, self.trigger = start, end, trigger
 
     def sampler_weight(self, epoch_num):
@@ -65,7 +65,7 @@ class CompositeSamplerScheduler:
     """sampler_schedulers.py:65-77: float64 L1 normalisation with +1e-12."""
 
     def __init__(self, schedulers, scheduler_weights):
-        assert len(schedulers) == len(scheduler_weights), "each scheduler needs a weight"
+        assert len(schedulers) == len(scheduler_weights), f"{len(schedulers)} schedules but {len(scheduler_weights)} weights"
         self.schedulers = list(schedulers)
         self.scheduler_weights = np.array(scheduler_weights, dtype=np.float64)
 
@@ -204,8 +204,8 @@ class CompositeSampler(nn.Module):
 
     def kernel_plan(self, sample_size: int, mixer_coefficients: Sequence[float]) -> Tuple[int, int]:
         """(fiode sampler kind, n_uniform) for the fused step."""
-        assert len(mixer_coefficients) == len(self.samplers), "[ERROR] Each sampler must have a mixer coefficient"
-        assert abs(sum(mixer_coefficients) - 1.0) < 1e-8, "[ERROR] mixer coefficeints need to sum to one."
+        assert len(mixer_coefficients) == len(self.samplers), f"{len(self.samplers)} samplers but {len(mixer_coefficients)} mixer coefficients"
+        assert abs(sum(mixer_coefficients) - 1.0) < 1e-8, f"mixer coefficients sum to {sum(mixer_coefficients)}, not 1"
         split = self._coefficient_to_num_samples(sample_size, mixer_coefficients)
         kinds = [type(s) for s in self.samplers]
         if kinds == [UniformSimplexSampling, CorrectConeSampling]:

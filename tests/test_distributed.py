@@ -141,8 +141,8 @@ def _bucket_worker(rank, world, port, q):
         for p, gr in zip(params, grads):
             p.grad.copy_(gr)
         red.allreduce(world)
-        q.put((rank, (len(red.buckets), [p.grad.clone() for p in params], grads,
-                      red.grads_in_param_order().clone())))
+        q.put((rank, _by_value((len(red.buckets), [p.grad.clone() for p in params], grads,
+                                red.grads_in_param_order().clone()))))
     finally:
         dist.destroy_process_group()
 
@@ -162,6 +162,8 @@ def test_bucketed_allreduce_is_mean_two_ranks():
         p.join(timeout=60)
     nb, g0, raw0, flat0 = out[0]
     _, g1, raw1, _ = out[1]
+    g0, g1, raw0, raw1 = ([torch.from_numpy(t) for t in ts] for ts in (g0, g1, raw0, raw1))
+    flat0 = torch.from_numpy(flat0)
     assert nb >= 3
     for a, b, r0, r1 in zip(g0, g1, raw0, raw1):
         torch.testing.assert_close(a, (r0 + r1) / 2, rtol=1e-6, atol=1e-7)
