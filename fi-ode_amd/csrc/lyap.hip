@@ -25,6 +25,8 @@
 //   k_lyap_wgrad   weight gradients dQ2 = gz2^T a1, dQ3 = gft^T a2, dQ1 = gz1^T h (MFMA, K =
 //                  samples), split per image part into partial slabs (deterministic)
 //   k_lyap_reduce  slab sum, per-image g_u, scalars;  k_lyap_static_grads: dQx, dbx, dx
+//   (the train_ode weight-gradient chain: k_lyap_wgrad also sums g_u from the gz1 rows, and its
+//   k_lyap_reduce runs the static gradients beside the slab sums -- two launches)
 #include "common.h"
 #include "tile.h"
 #include "../../include/fiode.h"
@@ -81,7 +83,7 @@ struct LyapArgs {
   DynScalars d;
   float kappa, invN;
   const float* kappa_dev;    // optional device kappa (the ramp of a captured step), else kappa
-  int parts, chunk;
+  int parts, chunk, ipw;   // k_lyap_wgrad: parts per image, rows per part, images per workgroup
   const float* x_feat;
   const int64_t* y;
   const float* h_in;
@@ -666,61 +668,101 @@ __global__ __launch_bounds__(256, 1) void k_lyap_bwd(LyapArgs a) {
   LY_STAMP(64 + 2048, 1);
 }
 
-// Weight gradients.  Workgroup (image b, part p) reduces rows [b*S + p*chunk, ...) of that image.
-// Wave w: dQ2[:, 32w:32w+32] (4 blocks), dQ3[:, 32w:32w+32], dQ1[32w:32w+32, :], db2/db1 slice w.
-// The rows are staged WG_CH at a time into LDS by the whole workgroup with every load in flight at
-// once (row pairs loaded one ahead from HBM left the loop load-latency bound: 16 us for the 40
-// rows per image of the train_ode solve); rows past the chunk's end are zero (A and B operands).
-constexpr int WG_CH = 40;       // rows per staged chunk (the RK4 train solve's 40 evals: one chunk)
-constexpr int WG_LD = 160;      // row stride (floats): a row pair's two halves on disjoint banks
+// Weight gradients (the train_ode solve's rows; fiode_internal::launch_wgrad).  A row group is
+// ipw images (part p of each; with a device row count only rows s < s_used[0] of an image) -- about
+// 80 rows -- and each group is split over four workgroups by column block cb: dQ2[:, 32cb:+32] (wave
+// w: the 32 x 32 block of rows 32w), dQ3[:, 32cb:+32] (wave 2) and dQ1[32cb:+32, :] (wave 3) on
+// 16x16x4 tiles (C = 10 pads to 16, not 32), db2[32cb:+32] (wave cb), db3 (wave 2 of cb 0).  The
+// four column blocks write disjoint quarters of their group's partial slab, summed by k_lyap_reduce
+// in a fixed order (bit-reproducible).  Round 3 gave each workgroup all columns of 20 rows: the same
+// MFMA cycles per wave (dQ3 / dQ1 were padded 32 x 32 blocks), 4x the slabs (19.7 MB written and
+// re-read per RK4 step).  Rows are staged WG_CH at a time, every load of a chunk in flight at once.
+// Blocks past 4 x nslab sum g_u[b] = the image's gz1 rows in row order (independent of the slabs).
+constexpr int WG_CH = 40;       // rows per staged chunk (the RK4 solve's 40 evals of an image)
+constexpr int WG_LDA = 160;     // gz2 row stride: a row pair's two halves on disjoint banks
+constexpr int WG_LDN = 32;      // 32-column rows (a1, a2, gz1 of the column block): likewise
 struct WgStage {
-  float gz2[WG_CH][WG_LD], a1[WG_CH][WG_LD], a2[WG_CH][WG_LD], gz1[WG_CH][WG_LD];
+  float gz2[WG_CH][WG_LDA];
+  float a1[WG_CH][WG_LDN], a2[WG_CH][WG_LDN], gz1[WG_CH][WG_LDN];
   float gft[WG_CH][12], h[WG_CH][12];
 };
 constexpr size_t WG_LDS = sizeof(WgStage);
+static_assert(WG_LDS <= 160 * 1024, "wgrad stage fits the LDS");
 __global__ __launch_bounds__(256, 1) void k_lyap_wgrad(LyapArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   WgStage& S = *reinterpret_cast<WgStage*>(smem);
+  if ((int)blockIdx.x >= 4 * a.nslab) {      // g_u[b][i] = sum of image b's gz1 rows, in row order
+    const int q = ((int)blockIdx.x - 4 * a.nslab) * 256 + threadIdx.x;
+    if (q < a.B * M) {
+      const int b = q / M, i = q - b * M;
+      const int n = a.s_used ? min(a.S, a.s_used[0]) : a.S;
+      const float* gz = a.gz1 + (size_t)b * a.S * M + i;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      int r = 0;
+      for (; r + 4 <= n; r += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += gz[(size_t)(r + u) * M];
+      for (; r < n; ++r) acc[0] += gz[(size_t)r * M];
+      a.g_u[q] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, col = lane & 31;
-  const int b = blockIdx.x / a.parts, p = blockIdx.x - b * a.parts;
-  const int r0 = b * a.S + p * a.chunk;
-  int r1 = min(r0 + a.chunk, (b + 1) * a.S);
-  if (a.s_used) r1 = min(r1, b * a.S + a.s_used[0]);      // rows past the device count are not data
+  const int j16 = lane & 15, q16 = lane >> 4;
+  // the four column blocks of a group are blocks grp + k * nslab: with nslab % 8 == 0 they share an
+  // XCD (blocks are dealt round-robin over the 8 XCDs), so three of the four gz2 reads hit its L2
+  const int grp = (int)blockIdx.x % a.nslab, cb = (int)blockIdx.x / a.nslab;
+  const int g = grp / a.parts, p = grp - g * a.parts;
   const float* hsrc = (a.sampler == FIODE_SAMPLER_GIVEN) ? a.h_in : a.h_ws;
   WG_STAMP(0);
-  f32x16 acc2[4], acc3 = f16_zero(), acc1 = f16_zero();
+  f32x16 acc2 = f16_zero();
+  f32x4q dq[2] = {q4_zero(), q4_zero()};     // wave 2: dQ3 tiles, wave 3: dQ1 tiles
+  float db2 = 0.f, db3 = 0.f;
+  // stage registers: gz2 32 float4 per row, the column block of a1 / a2 / gz1 8 float4 each, gft /
+  // h rows; rows past n load row n - 1 and are stored as zeros (A and B operands)
+  constexpr int NW = WG_CH * 32 / 256;                        // gz2 float4 per thread
+  constexpr int NN = (WG_CH * 24 + 255) / 256;                // narrow float4 per thread
+  constexpr int NS = WG_CH * C * 2, NST = (NS + 255) / 256;
+  f32x4 vw[NW], vn[NN];
+  float sv[NST];
+  const int k4 = threadIdx.x & 31;
+  auto load = [&](int c0, int n) {            // rows c0 .. c0 + n - 1 (n <= WG_CH) -> registers
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) acc2[mb] = f16_zero();
-  float db2 = 0.f, db1 = 0.f, db3 = 0.f;
-  for (int c0 = r0; c0 < r1; c0 += WG_CH) {
-    const int n = min(WG_CH, r1 - c0);
-    // stage: 4 arrays x 32 float4 per row + the gft / h rows, every load of the chunk in flight
-    // before the first LDS store (one memory round trip per chunk)
-    constexpr int NV = WG_CH * 128, NVT = (NV + 255) / 256;
-    constexpr int NS = WG_CH * C * 2, NST = (NS + 255) / 256;
-    static_assert(NV % 256 == 0, "each thread stages one array: q = threadIdx.x & 127 for every u");
-    f32x4 v[NVT];
-    float sv[NST];
-    const int qa = threadIdx.x & 127, arr = qa >> 5, k4 = qa & 31;
-    const float* src = arr == 0 ? a.gz2 : arr == 1 ? a.a1 : arr == 2 ? a.a2 : a.gz1;
-    float* dstb = arr == 0 ? &S.gz2[0][0] : arr == 1 ? &S.a1[0][0] : arr == 2 ? &S.a2[0][0] : &S.gz1[0][0];
+    for (int u = 0; u < NW; ++u) {
+      const int r = (threadIdx.x >> 5) + 8 * u;
+      vw[u] = *reinterpret_cast<const f32x4*>(a.gz2 + (size_t)(c0 + min(r, n - 1)) * M + 4 * k4);
+    }
 #pragma unroll
-    for (int u = 0; u < NVT; ++u) {
-      const int r = (threadIdx.x >> 7) + 2 * u;                 // rows past n: row n - 1 loaded, zeroed below
-      v[u] = *reinterpret_cast<const f32x4*>(src + (size_t)(c0 + min(r, n - 1)) * M + 4 * k4);
+    for (int u = 0; u < NN; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      const int r = e / 24, rem = e - r * 24, arr = rem >> 3, c4 = rem & 7;
+      const float* src = arr == 0 ? a.a1 : arr == 1 ? a.a2 : a.gz1;
+      vn[u] = e < WG_CH * 24 ? *reinterpret_cast<const f32x4*>(src + (size_t)(c0 + min(r, n - 1)) * M + 32 * cb + 4 * c4)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
       const int e = threadIdx.x + u * 256;
       const int r = (e >> 1) / C, c = (e >> 1) - r * C;
       const int rs = min(r, n - 1);
-      const float t = (e & 1) ? hsrc[(size_t)(c0 + rs) * C + c] : a.gft[(size_t)(c0 + rs) * C + c];
+      const float t = e < NS ? ((e & 1) ? hsrc[(size_t)(c0 + rs) * C + c] : a.gft[(size_t)(c0 + rs) * C + c]) : 0.f;
       sv[u] = (e < NS && r < n) ? t : 0.f;
     }
+  };
+  auto store = [&](int n) {                   // registers -> LDS (the previous chunk's readers are done)
 #pragma unroll
-    for (int u = 0; u < NVT; ++u) {
-      const int r = (threadIdx.x >> 7) + 2 * u;
-      *reinterpret_cast<f32x4*>(dstb + r * WG_LD + 4 * k4) = r < n ? v[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NW; ++u) {
+      const int r = (threadIdx.x >> 5) + 8 * u;
+      *reinterpret_cast<f32x4*>(&S.gz2[r][4 * k4]) = r < n ? vw[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < NN; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < WG_CH * 24) {
+        const int r = e / 24, rem = e - r * 24, arr = rem >> 3, c4 = rem & 7;
+        float* dst = arr == 0 ? &S.a1[r][4 * c4] : arr == 1 ? &S.a2[r][4 * c4] : &S.gz1[r][4 * c4];
+        *reinterpret_cast<f32x4*>(dst) = r < n ? vn[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
@@ -731,62 +773,149 @@ __global__ __launch_bounds__(256, 1) void k_lyap_wgrad(LyapArgs a) {
         else S.gft[r][c] = sv[u];
       }
     }
+  };
+  auto compute = [&](int n) {
+    // dQ2 block (rows 32w, columns 32cb): row pairs, LDS operands of pair j + 2 read before the
+    // MFMA of pair j (one wave per SIMD: nothing else hides the LDS latency)
+    {
+      float av = S.gz2[half][32 * w + col], bv = S.a1[half][col];
+      for (int j = 0; j < n; j += 2) {
+        float an = av, bn = bv;
+        if (j + 2 < n) {
+          an = S.gz2[j + 2 + half][32 * w + col];
+          bn = S.a1[j + 2 + half][col];
+        }
+        acc2 = mfma32(av, bv, acc2);
+        if (w == cb) db2 += av;
+        av = an;
+        bv = bn;
+      }
+    }
+    if (w >= 2) {                             // dQ3 (wave 2) / dQ1 (wave 3) on 16x16x4 tiles, row quads
+      const int nq = (n + 3) >> 2;
+      auto ld = [&](int s4, float (&o)[3]) {
+        const int r = 4 * s4 + q16;
+        if (w == 2) {
+          o[0] = j16 < C ? S.gft[r][j16] : 0.f;
+          o[1] = S.a2[r][j16];
+          o[2] = S.a2[r][16 + j16];
+        } else {
+          o[0] = j16 < C ? S.h[r][j16] : 0.f;
+          o[1] = S.gz1[r][j16];
+          o[2] = S.gz1[r][16 + j16];
+        }
+      };
+      float o[3], on[3];
+      ld(0, o);
+      for (int s4 = 0; s4 < nq; ++s4) {
+        on[0] = o[0]; on[1] = o[1]; on[2] = o[2];
+        if (s4 + 1 < nq) ld(s4 + 1, on);
+        if (w == 2) {
+          db3 += o[0];
+          dq[0] = mfma16q(o[0], o[1], dq[0]);
+          dq[1] = mfma16q(o[0], o[2], dq[1]);
+        } else {
+          dq[0] = mfma16q(o[1], o[0], dq[0]);
+          dq[1] = mfma16q(o[2], o[0], dq[1]);
+        }
+        o[0] = on[0]; o[1] = on[1]; o[2] = on[2];
+      }
+    }
+  };
+  // the group's chunks: images g * ipw .. (g + 1) * ipw - 1, rows r0 .. r1 of each (part p, and
+  // with a device row count only rows s < s_used[0]), WG_CH rows at a time; the next chunk's loads
+  // are in flight while the current chunk's MFMAs run
+  const int b_end = min(a.B, (g + 1) * a.ipw);
+  auto rows_of = [&](int b, int& r0, int& r1) {
+    r0 = b * a.S + p * a.chunk;
+    r1 = min(r0 + a.chunk, (b + 1) * a.S);
+    if (a.s_used) r1 = min(r1, b * a.S + a.s_used[0]);        // rows past the device count are not data
+  };
+  auto next = [&](int& b, int& c0, int& r1) {   // first chunk at or after (b, c0) that has rows
+    while (b < b_end && c0 >= r1) {
+      if (++b < b_end) rows_of(b, c0, r1);
+    }
+  };
+  int b = g * a.ipw, c0 = 0, r1 = 0;
+  if (b < b_end) rows_of(b, c0, r1);
+  next(b, c0, r1);
+  if (b < b_end) {
+    int n = min(WG_CH, r1 - c0);
+    load(c0, n);
+    store(n);
     __syncthreads();
     WG_STAMP(1);
-    // LDS operands of pair j + 2 read before the MFMAs of pair j (one wave per SIMD: nothing else
-    // hides the LDS latency in front of the dependent MFMAs)
-    struct Ops { float A2[4], B2, A3, B3, A1, B1; };
-    auto rd = [&](int j, Ops& o) {
-      const int jr = j + half;
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) o.A2[mb] = S.gz2[jr][32 * mb + col];
-      o.B2 = S.a1[jr][32 * w + col];
-      o.A3 = col < C ? S.gft[jr][col] : 0.f;
-      o.B3 = S.a2[jr][32 * w + col];
-      o.A1 = S.gz1[jr][32 * w + col];
-      o.B1 = col < C ? S.h[jr][col] : 0.f;
-    };
-    Ops cur;
-    rd(0, cur);
-    for (int j = 0; j < n; j += 2) {
-      Ops nxt = cur;
-      if (j + 2 < n) rd(j + 2, nxt);
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma32(cur.A2[mb], cur.B2, acc2[mb]);
-      acc3 = mfma32(cur.A3, cur.B3, acc3);
-      acc1 = mfma32(cur.A1, cur.B1, acc1);
-      db2 += (w == 0) ? cur.A2[0] : (w == 1) ? cur.A2[1] : (w == 2) ? cur.A2[2] : cur.A2[3];
-      db1 += cur.A1;
-      db3 += cur.A3;
-      cur = nxt;
+    while (true) {
+      int bn = b, cn = c0 + WG_CH, rn = r1;
+      next(bn, cn, rn);
+      const bool more = bn < b_end;
+      const int nn = more ? min(WG_CH, rn - cn) : 0;
+      if (more) load(cn, nn);                 // in flight during this chunk's MFMAs
+      compute(n);
+      __syncthreads();
+      if (!more) break;
+      store(nn);
+      __syncthreads();
+      b = bn; c0 = cn; r1 = rn; n = nn;
     }
-    __syncthreads();
   }
   WG_STAMP(2);
-  float* slab = a.slabs + (size_t)blockIdx.x * SLAB;
+  float* slab = a.slabs + (size_t)grp * SLAB;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int r = 0; r < 16; ++r) slab[SLAB_Q2 + (32 * w + acc_row(r, half)) * M + 32 * cb + col] = acc2[r];
+  if (w == 2) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) slab[SLAB_Q2 + (32 * mb + acc_row(r, half)) * M + 32 * w + col] = acc2[mb][r];
+    for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = acc_row(r, half);
-    if (i < C) slab[SLAB_Q3 + i * M + 32 * w + col] = acc3[r];
-    if (col < C) slab[SLAB_Q1 + (32 * w + i) * C + col] = acc1[r];
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * q16 + r;
+        if (i < C) slab[SLAB_Q3 + i * M + 32 * cb + 16 * hb + j16] = dq[hb][r];
+      }
+  } else if (w == 3) {
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (j16 < C) slab[SLAB_Q1 + (32 * cb + 16 * hb + 4 * q16 + r) * C + j16] = dq[hb][r];
   }
-  db2 += shfl_xor32(db2);
-  db1 += shfl_xor32(db1);
-  db3 += shfl_xor32(db3);
-  if (half == 0) {
-    slab[SLAB_B2 + 32 * w + col] = db2;
-    slab[SLAB_B1 + 32 * w + col] = db1;
-    if (w == 0 && col < C) slab[SLAB_B3 + col] = db3;
+  if (w == cb) {
+    db2 += shfl_xor32(db2);
+    if (half == 0) slab[SLAB_B2 + 32 * cb + col] = db2;
+  }
+  if (w == 2 && cb == 0) {
+    db3 += __shfl_xor(db3, 16, 64);
+    db3 += shfl_xor32(db3);
+    if (q16 == 0 && j16 < C) slab[SLAB_B3 + j16] = db3;
   }
   WG_STAMP(3);
 }
 
-// Sum of the slabs (fixed order, deterministic) -> dQ2, dQ3, dQ1, db2, db3; per-image g_u;
-// scalars.  Workgroup w < n_el_blocks sums 64 consecutive slab entries: its 4 waves each add a
+// one item of the static gradients (k_lyap_static_grads; the wgrad chain's k_lyap_reduce)
+__device__ __forceinline__ void static_grads_item(const LyapArgs& a, int e) {
+  if (e < M * FIODE_X) {
+    const int i = e / FIODE_X, c = e - i * FIODE_X;
+    float s = 0.f;
+#pragma unroll 16
+    for (int b = 0; b < a.B; ++b) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.x_feat[(size_t)b * FIODE_X + c], s);
+    a.grads.Qx[e] = s;
+  } else if (e < M * FIODE_X + M) {
+    const int i = e - M * FIODE_X;
+    float s = 0.f;
+#pragma unroll 16
+    for (int b = 0; b < a.B; ++b) s += a.g_u[(size_t)b * M + i];
+    a.grads.bx[i] = s;
+    a.grads.b1[i] = s;
+  } else if (a.grads.x_feat && e < M * FIODE_X + M + a.B * FIODE_X) {
+    const int q = e - M * FIODE_X - M, b = q / FIODE_X, c = q - b * FIODE_X;
+    float s = 0.f;
+#pragma unroll 16
+    for (int i = 0; i < M; ++i) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.Qx[i * FIODE_X + c], s);
+    a.grads.x_feat[q] = s;
+  }
+}
+
+// Sum of the slabs (fixed order, deterministic) -> dQ2, dQ3, dQ1, db2, db3; then per-image g_u
+// and the scalars (fused fan-out backward) or the static gradients (weight-gradient chain).  Workgroup w < n_el_blocks sums 64 consecutive slab entries: its 4 waves each add a
 // quarter of the slabs (8 independent loads in flight per lane), then combine through LDS.
 // The last workgroup reduces the per-tile scalars.
 constexpr int RED_COLS = 64;
@@ -820,19 +949,19 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
       else if (e < SLAB_B1) a.grads.b2[e - SLAB_B2] = t;
       else if (e >= SLAB_B3 && e < SLAB_B3 + C) a.grads.b3[e - SLAB_B3] = t;
     }
-  } else if ((int)blockIdx.x < n_el_blocks + n_gu_blocks) {      // g_u[b][i] = sum over the image's parts
+  } else if (!a.gu_tiles) {       // weight-gradient chain: g_u is final (k_lyap_wgrad) -> static grads
+    static_grads_item(a, ((int)blockIdx.x - n_el_blocks) * 256 + threadIdx.x);
+  } else if ((int)blockIdx.x < n_el_blocks + n_gu_blocks) {      // g_u[b][i] = sum over the image's tiles
     const int q = (blockIdx.x - n_el_blocks) * RED_COLS + (threadIdx.x & (RED_COLS - 1));
     if (threadIdx.x < RED_COLS && q < a.B * M) {
       const int b = q / M, i = q - b * M;
       float s = 0.f;
-      if (a.gu_tiles) {           // fused backward: the tiles holding rows of image b, in order
+      {                           // fused backward: the tiles holding rows of image b, in order
         const int t0 = (int)(((size_t)b * a.S) / 32), t1 = (int)(((size_t)(b + 1) * a.S - 1) / 32);
         for (int t = t0; t <= t1; ++t) {
           const int seg = b - (int)(((size_t)t * 32) / a.S);
           s += a.gu_tiles[((size_t)t * a.nseg + seg) * M + i];
         }
-      } else {
-        for (int p = 0; p < a.parts; ++p) s += a.slabs[(size_t)(b * a.parts + p) * SLAB + SLAB_B1 + i];
       }
       a.g_u[q] = s;
     }
@@ -867,27 +996,7 @@ __global__ __launch_bounds__(256) void k_lyap_reduce(LyapArgs a) {
 // dQx = g_u^T x ; dbx = db1 = sum_b g_u ; dx = g_u Qx   (expand backward, pl_modules.py:400)
 // (the fixed-order sums are unrolled so their loads are in flight together: 33 -> ~10 us)
 __global__ __launch_bounds__(256) void k_lyap_static_grads(LyapArgs a) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < M * FIODE_X) {
-    const int i = e / FIODE_X, c = e - i * FIODE_X;
-    float s = 0.f;
-#pragma unroll 16
-    for (int b = 0; b < a.B; ++b) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.x_feat[(size_t)b * FIODE_X + c], s);
-    a.grads.Qx[e] = s;
-  } else if (e < M * FIODE_X + M) {
-    const int i = e - M * FIODE_X;
-    float s = 0.f;
-#pragma unroll 16
-    for (int b = 0; b < a.B; ++b) s += a.g_u[(size_t)b * M + i];
-    a.grads.bx[i] = s;
-    a.grads.b1[i] = s;
-  } else if (a.grads.x_feat && e < M * FIODE_X + M + a.B * FIODE_X) {
-    const int q = e - M * FIODE_X - M, b = q / FIODE_X, c = q - b * FIODE_X;
-    float s = 0.f;
-#pragma unroll 16
-    for (int i = 0; i < M; ++i) s = __fmaf_rn(a.g_u[(size_t)b * M + i], a.Qx[i * FIODE_X + c], s);
-    a.grads.x_feat[q] = s;
-  }
+  static_grads_item(a, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ---- workspace ----------------------------------------------------------------------------------
@@ -1065,35 +1174,60 @@ extern "C" FIODE_API int fiode_debug_wgrad_stamps(unsigned long long* host, int 
 
 // ---- shared with the ODE training path (odetrain.hip): weight gradients of rows (b, s) ------
 namespace fiode_internal {
-size_t wgrad_bytes(int B, int S) {
-  int parts, chunk;
-  parts_for(B, S, parts, chunk);
-  return al((size_t)B * parts * SLAB * 4) + al((size_t)B * M * 4);
+// Weight-gradient grid: row groups of ~80 rows (ipw images, or one part of an image), at most 256,
+// each on four workgroups (column blocks, k_lyap_wgrad) that fill one 77 KB partial slab together.
+// S is the exact rows per image (rk4) or, with a device row count (dopri5: S = the eval capacity),
+// an upper bound: the estimate then takes 64 rows per image.  nwg = the row groups (= slabs).
+struct WgGrid { int parts, chunk, ipw, nwg; };
+WgGrid wgrad_grid(int B, int S, bool exact_rows) {
+  WgGrid g{};
+  const long long se = exact_rows ? S : (S < 64 ? S : 64);
+  long long t = (long long)B * se / 80;
+  if (t < 1) t = 1;
+  if (t > 256) t = 256;
+  g.parts = 1;
+  g.ipw = 1;
+  if (t >= B) {
+    const int maxp = (int)(se / 80 > 0 ? se / 80 : 1);
+    g.parts = (int)(t / B) < maxp ? (int)(t / B) : maxp;
+  } else {
+    g.ipw = (int)((B + t - 1) / t);
+  }
+  g.chunk = (S + g.parts - 1) / g.parts;
+  g.chunk = (g.chunk + 1) & ~1;
+  g.nwg = (B + g.ipw - 1) / g.ipw * g.parts;
+  return g;
+}
+
+size_t wgrad_bytes(int B, int S, bool exact_rows) {
+  const WgGrid g = wgrad_grid(B, S, exact_rows);
+  return al((size_t)g.nwg * SLAB * 4) + al((size_t)B * M * 4);
 }
 
 int launch_wgrad(hipStream_t st, const WgradIO& io) {
   LyapArgs a{};
   a.B = io.B; a.S = io.S; a.N = io.B * io.S;
   a.s_used = io.s_used;
-  parts_for(a.B, a.S, a.parts, a.chunk);
+  const WgGrid g = wgrad_grid(a.B, a.S, io.s_used == nullptr);
+  a.parts = g.parts; a.chunk = g.chunk; a.ipw = g.ipw;
   a.sampler = FIODE_SAMPLER_GIVEN;
   a.h_in = io.h; a.x_feat = io.x_feat; a.Qx = io.Qx;
   a.a1 = const_cast<float*>(io.a1); a.a2 = const_cast<float*>(io.a2);
   a.gz2 = const_cast<float*>(io.gz2); a.gz1 = const_cast<float*>(io.gz1); a.gft = const_cast<float*>(io.gft);
   char* ws = static_cast<char*>(io.workspace);
   a.slabs = reinterpret_cast<float*>(ws);
-  a.g_u = reinterpret_cast<float*>(ws + al((size_t)a.B * a.parts * SLAB * 4));
+  a.g_u = reinterpret_cast<float*>(ws + al((size_t)g.nwg * SLAB * 4));
   a.tile_sc = nullptr;
-  a.nslab = a.B * a.parts;
+  a.nslab = g.nwg;
   a.gu_tiles = nullptr;
   a.grads = io.grads;
-  hipLaunchKernelGGL(k_lyap_wgrad, dim3(a.B * a.parts), dim3(256), WG_LDS, st, a);
-  FIODE_HIP_CHECK(hipGetLastError());
-  const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (a.B * M + RED_COLS - 1) / RED_COLS;
-  hipLaunchKernelGGL(k_lyap_reduce, dim3(red_blocks), dim3(256), 0, st, a);
+  // one launch: the slab workgroups + g_u blocks (independent: g_u reads the gz1 rows); then one
+  // launch for the slab sums beside the static gradients, which need only the finished g_u
+  hipLaunchKernelGGL(k_lyap_wgrad, dim3(4 * g.nwg + (a.B * M + 255) / 256), dim3(256), WG_LDS, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   const int sg_items = M * FIODE_X + M + a.B * FIODE_X;
-  hipLaunchKernelGGL(k_lyap_static_grads, dim3((sg_items + 255) / 256), dim3(256), 0, st, a);
+  const int red_blocks = (SLAB + RED_COLS - 1) / RED_COLS + (sg_items + 255) / 256;
+  hipLaunchKernelGGL(k_lyap_reduce, dim3(red_blocks), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }

@@ -1750,7 +1750,7 @@ OtLayout ot_layout(int B, int E, int A = 0) {
   L.xs = o; o += (size_t)OT_XRING * 2 * nt4 * 8 * OT4_XSTRIDE + 1024;   // the reduction granules follow: one clear for both
   L.xr = o; o += al(A > 0 ? 2 * nt4 * 2 * OT_XV * 8 : 0);
   L.kw = o; o += al((size_t)E * 2 * B * 16);
-  L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E));
+  L.wg = o; o += al(fiode_internal::wgrad_bytes(B, E, A == 0));
   L.ys = o; o += al((size_t)A * B * C * 4);
   L.alog = o; o += al((size_t)A * ALOG_W * 8);
   L.meta = o; o += al(META_N * 8);

@@ -17,10 +17,10 @@ struct WgradIO {
   const float *a1, *a2;           // [B*S][M] post-dropout-ReLU activations
   const float *gz2, *gz1;         // [B*S][M] gradients at the layer-2 / layer-1 pre-activations
   const float* gft;               // [B*S][C] gradient at the MLP output
-  void* workspace;                // wgrad_bytes(B, S)
+  void* workspace;                // wgrad_bytes(B, S, s_used == nullptr)
   const int32_t* s_used;          // optional device count: only rows s < s_used[0] of each image count
   fiode_lyap_grads grads;         // outputs (all overwritten)
 };
-size_t wgrad_bytes(int B, int S);
+size_t wgrad_bytes(int B, int S, bool exact_rows);   // exact_rows: S rows per image (else a bound, s_used set)
 int launch_wgrad(hipStream_t st, const WgradIO& io);
 }  // namespace fiode_internal
