@@ -44,10 +44,58 @@ __device__ __forceinline__ int64_t wpos(const DArgs& a, int r, int c) {   // X (
   return a.wide ? (int64_t)c * a.cin + r : (int64_t)r * a.cin + c;
 }
 
-__global__ void __launch_bounds__(NT) k_dense_prep(DArgs a, const float* __restrict__ G, float* __restrict__ M) {
+// Squared Frobenius norm partials of each W[b] (NPART per matrix, each a fixed-order sum over its
+// block's float4 stride): the norm the prep kernel finishes in a fixed order -- one 2-8 MB streaming
+// read over NPART x batch workgroups in place of torch's vector_norm reduction (~10 us on the dense
+// maps' forward chain).
+constexpr int NPART = 64;
+__global__ void __launch_bounds__(NT) k_dense_sumsq(DArgs a, float* __restrict__ part) {
+  __shared__ float red[NT / 64];
+  const int b = blockIdx.y;
+  const int64_t n = (int64_t)a.cout * a.cin;
+  const float* Wb = a.W + (int64_t)b * n;
+  float acc = 0.f;
+  if ((n & 3) == 0 && ((uintptr_t)Wb & 15u) == 0) {
+    const f32x4* W4 = reinterpret_cast<const f32x4*>(Wb);
+#pragma unroll 4
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < (n >> 2); i += (int64_t)NPART * NT) {
+      const f32x4 v = W4[i];
+      acc = fmaf(v[0], v[0], acc);
+      acc = fmaf(v[1], v[1], acc);
+      acc = fmaf(v[2], v[2], acc);
+      acc = fmaf(v[3], v[3], acc);
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)NPART * NT) acc = fmaf(Wb[i], Wb[i], acc);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b * NPART + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ||W[b]|| from the NPART partials, the same fixed order in every workgroup (wave 0's lanes, then a
+// butterfly); block 0 also writes it to nrm_out
+__device__ __forceinline__ float dense_norm(const float* __restrict__ part, int b, float* nrm_out) {
+  __shared__ float sn;
+  if (threadIdx.x < 64) {
+    float v = part[b * NPART + threadIdx.x];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (threadIdx.x == 0) {
+      sn = sqrtf(v);
+      if (nrm_out && blockIdx.x == 0) nrm_out[b] = sn;
+    }
+  }
+  __syncthreads();
+  return sn;
+}
+static_assert(NPART == 64, "dense_norm: one partial per lane of wave 0");
+
+__global__ void __launch_bounds__(NT) k_dense_prep(DArgs a, const float* __restrict__ G, float* __restrict__ M,
+                                                   const float* __restrict__ part, float* __restrict__ nrm_out) {
   const int b = blockIdx.y, k = a.k;
   const float* Wb = a.W + (int64_t)b * a.cout * a.cin;
-  const float s = a.alpha[b] / a.nrm[b];
+  const float s = a.alpha[b] / (part ? dense_norm(part, b, nrm_out) : a.nrm[b]);
   for (int idx = blockIdx.x * NT + threadIdx.x; idx < k * k; idx += gridDim.x * NT) {
     const int i = idx / k, j = idx % k;
     float m = s * (wx(a, Wb, i, j) - wx(a, Wb, j, i));
@@ -347,7 +395,38 @@ extern "C" int fiode_dense_cayley_prep(void* stream, const fiode_dense_config* c
   a.alpha = alpha;
   a.nrm = nrm;
   hipLaunchKernelGGL(k_dense_prep, grid_for((int64_t)a.k * a.k, batch), dim3(NT), 0, (hipStream_t)stream, a,
-                     a.R > a.k ? G : nullptr, M);
+                     a.R > a.k ? G : nullptr, M, (const float*)nullptr, (float*)nullptr);
+  DENSE_RET();
+}
+
+extern "C" size_t fiode_dense_norm_workspace_bytes(const fiode_dense_config* cfg) {
+  return cfg && cfg->batch > 0 ? (size_t)cfg->batch * NPART * sizeof(float) : 0;
+}
+
+extern "C" int fiode_dense_norm_partials(void* stream, const fiode_dense_config* cfg, const float* W, void* workspace,
+                                         size_t workspace_bytes) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!W || !workspace) return FIODE_EINVAL;
+  if (workspace_bytes < fiode_dense_norm_workspace_bytes(cfg)) return FIODE_EWORKSPACE;
+  a.W = W;
+  hipLaunchKernelGGL(k_dense_sumsq, dim3(NPART, batch), dim3(NT), 0, (hipStream_t)stream, a, (float*)workspace);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_cayley_prep_normed(void* stream, const fiode_dense_config* cfg, const float* W,
+                                              const float* alpha, const void* workspace, float* nrm_out,
+                                              const float* G, float* M) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!W || !alpha || !workspace || !nrm_out || !M || (a.R > a.k && !G)) return FIODE_EINVAL;
+  a.W = W;
+  a.alpha = alpha;
+  a.nrm = nullptr;
+  hipLaunchKernelGGL(k_dense_prep, grid_for((int64_t)a.k * a.k, batch), dim3(NT), 0, (hipStream_t)stream, a,
+                     a.R > a.k ? G : nullptr, M, (const float*)workspace, nrm_out);
   DENSE_RET();
 }
 

@@ -170,6 +170,9 @@ def _load():
         "fiode_small_cayley_backward": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp, _vp,
                                                    _vp, _vp]),
         "fiode_dense_cayley_prep": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
+        "fiode_dense_norm_workspace_bytes": (ct.c_size_t, [ct.POINTER(DenseConfig)]),
+        "fiode_dense_norm_partials": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, ct.c_size_t]),
+        "fiode_dense_cayley_prep_normed": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_finish": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_ginv": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_h": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp]),

@@ -151,14 +151,29 @@ def _dense_prep(W: torch.Tensor, alpha: torch.Tensor, M: Optional[torch.Tensor] 
     b, cout, cin = Wb.shape
     wide = cin > cout
     k = cout if wide else cin
-    nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
+    cfg = L.DenseConfig(b, cout, cin)
+    lib, st = L.lib(), ops._stream(W.device)
+    if not DENSE_NORM_PARTIALS:
+        nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
+    else:
+        # ||W|| as 64 partial sums per matrix ahead of the G GEMM, finished by the prep kernel (no
+        # torch reduction on the map's forward chain)
+        part = torch.empty(lib.fiode_dense_norm_workspace_bytes(ct.byref(cfg)) // 4, dtype=torch.float32,
+                           device=W.device)
+        L.check(lib.fiode_dense_norm_partials(st, ct.byref(cfg), Wb.data_ptr(), part.data_ptr(), part.numel() * 4),
+                "fiode_dense_norm_partials")
     Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
     G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
-    cfg = L.DenseConfig(b, cout, cin)
     if M is None:
         M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
-    L.check(L.lib().fiode_dense_cayley_prep(ops._stream(W.device), ct.byref(cfg), Wb.data_ptr(), al.data_ptr(),
-                                            nrm.data_ptr(), ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
+    if not DENSE_NORM_PARTIALS:
+        L.check(lib.fiode_dense_cayley_prep(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), nrm.data_ptr(),
+                                            ops._ptr(G), M.data_ptr()), "fiode_dense_cayley_prep")
+    else:
+        nrm = torch.empty(b, dtype=torch.float32, device=W.device)
+        L.check(lib.fiode_dense_cayley_prep_normed(st, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), part.data_ptr(),
+                                                   nrm.data_ptr(), ops._ptr(G), M.data_ptr()),
+                "fiode_dense_cayley_prep_normed")
     return dict(Wb=Wb, al=al, nrm=nrm, wide=wide, k=k, Vp=Vp, cfg=cfg), M
 
 
@@ -438,6 +453,7 @@ def cayley(W: torch.Tensor) -> torch.Tensor:
 SPECTRAL_BWD_ON_MAIN = False
 DENSE_BWD_ON_MAIN = True
 DENSE_GEMM = True          # GMn by fiode_dense_gemm (tools/ab_step.py `lib_gmn` measures the library form)
+DENSE_NORM_PARTIALS = True  # ||W|| by fiode_dense_norm_partials + the prep kernel (`torch_norm`: vector_norm)
 SMALL_BWD_ON_MAIN = False
 STEP_STREAM: Optional[torch.cuda.Stream] = None
 

@@ -175,6 +175,11 @@ class LyapODELossFn(torch.autograd.Function):
             out=plan.get("out"), offset_dev=plan.get("offset_dev"), kappa_dev=plan.get("kappa_dev"))
         plan["scalars"] = sc
         plan["debug_out"] = dbg
+        ctx.lyap = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+        # lyap * (1 - p) for a unit seed (GraphTrainStep), made here on the fan-out's stream before
+        # it joins the solve: this multi-tensor kernel runs beside the solve instead of after its
+        # backward (on the captured step's critical path)
+        ctx.lyap_unit = torch._foreach_mul(ctx.lyap, 1.0 - float(p))
         if pre is not None:
             main = torch.cuda.current_stream(xf.device)
             main.wait_event(pre[1])
@@ -193,7 +198,6 @@ class LyapODELossFn(torch.autograd.Function):
                                            gunit.data_ptr()), "fiode_ode_loss_mix")
         plan["loss_ode"] = loss_ode
         plan["y_hat"] = y_hat
-        ctx.lyap = [grads[k] for k in ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
         ctx.ode = (gunit, xo, w, oplan, ws)
         ctx.p = float(p)
         ctx.split = x_ode is not None
@@ -213,8 +217,8 @@ class LyapODELossFn(torch.autograd.Function):
         gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
         keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         ode = [gr[k] for k in keys]
-        lyap = torch._foreach_mul(ctx.lyap, (1.0 - ctx.p) if unit else go * (1.0 - ctx.p))
-        ctx.lyap = None
+        lyap = ctx.lyap_unit if unit else torch._foreach_mul(ctx.lyap, go * (1.0 - ctx.p))
+        ctx.lyap = ctx.lyap_unit = None
         if ctx.split:     # the solve's features are another tensor: its gradient goes there
             torch._foreach_add_(ode[1:], lyap[1:])
             gx, gxo = lyap[0], ode[0]

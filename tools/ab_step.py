@@ -133,7 +133,32 @@ def old_seed(m):
     RESTORE.append(lambda: setattr(GS.GraphTrainStep, "_unit_grad", ug))
 
 
-ALL = {"default": default, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
+def torch_norm(m):
+    from fiode_amd import cayley as CY
+    CY.DENSE_NORM_PARTIALS = False        # the dense maps' norm by torch.linalg.vector_norm
+    RESTORE.append(lambda: setattr(CY, "DENSE_NORM_PARTIALS", True))
+
+
+def late_scale(m):
+    """The unit-seed backward with lyap * (1 - p) made in the backward, after the solve's backward."""
+    from fiode_amd import lyapunov as LY, ops
+
+    def late_backward(ctx, go):
+        gunit, xo, w, oplan, ws = ctx.ode
+        ctx.ode = None
+        gr, _ = ops.odetrain_backward(gunit, xo, w, oplan["dyn"], oplan["cfg"], ws)
+        keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+        ode = [gr[k] for k in keys]
+        lyap = torch._foreach_mul(ctx.lyap, 1.0 - ctx.p)
+        ctx.lyap = ctx.lyap_unit = None
+        torch._foreach_add_(ode, lyap)
+        return (ode[0], None) + tuple(ode[1:]) + (None, None, None, None, None, None)
+    nb = LY.LyapODELossFn.backward
+    LY.LyapODELossFn.backward = staticmethod(late_backward)
+    RESTORE.append(lambda: setattr(LY.LyapODELossFn, "backward", staticmethod(nb)))
+
+
+ALL = {"default": default, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
        "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
        "split": split, "split_serial": split_serial, "old_seed": old_seed,
