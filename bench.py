@@ -284,7 +284,11 @@ def main():
             from fiode_amd.graph_step import GraphTrainStep
             # comm: RCCL collectives captured in the step ("graph", the default over nccl) or eager
             # between two replays ("eager"); FIODE_COMM overrides (e.g. a runtime that cannot capture)
-            gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world, comm=os.environ.get("FIODE_COMM"))
+            # placement_trials: the fastest of a few captures on different side streams (the executor's
+            # hardware-queue placement of the step's branches; GraphTrainStep._select_placement)
+            gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world, comm=os.environ.get("FIODE_COMM"),
+                                   placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "4")))
+            last["placement_ms"] = gstep.placement_ms
             last["comm"] = gstep.comm if world > 1 else None
 
             def step():
@@ -317,6 +321,8 @@ def main():
         if strict and (health["status"] or not health["loss_finite"]):
             raise RuntimeError(f"unhealthy timed run: {health}")
         health["comm"] = last.get("comm")
+        if last.get("placement_ms") is not None:
+            health["placement_ms"] = last["placement_ms"]     # per trial capture; the fastest is kept
         return float(dt.item()), mod, x, y, health
 
     def certify_companion(n_img: int = 2):

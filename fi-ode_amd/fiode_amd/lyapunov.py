@@ -311,6 +311,9 @@ class LyapunovLearning(nn.Module):
         # step, the solve, the mix) as in round 1
         self.fused_ode_loss = True
         self._side_streams = None
+        # capture points of the Cayley maps' prefetch (_prefetch_weights): the 4096 -> 512 map right
+        # after the input kernels, the other maps after conv layer 2 (None: all of them at the input)
+        self._prefetch_late_at = 2
         self.logged: Dict[str, float] = {}
         self._out = None
 
@@ -467,9 +470,12 @@ class LyapunovLearning(nn.Module):
 
         Capture order: the hipGraph executor dispatches nodes in capture order over a few hardware
         queues, so maps captured ahead of the main stream's first kernels hold those kernels back.
-        The launches are therefore captured right after the step's input kernels (a hook on the
-        backbone's first layer), the linear / dynamics maps first, then the conv maps (conv maps
-        computed one step ahead by GraphTrainStep skip their launch here).  Measured alternatives
+        The launches are therefore captured by a hook on the backbone's conv stack: the 4096 -> 512
+        map (the first one the step needs, and the longest chain) right after the step's input
+        kernels, the other linear maps and the dynamics' maps after conv layer 2 (``_prefetch_late_at``;
+        round 4: 1.476 -> 1.416 ms with both sides' captures picked from 4 placements,
+        tools/ab_step.py), then the conv maps (conv maps computed one step ahead by GraphTrainStep
+        skip their launch here).  Measured alternatives
         (deferral past conv layers, one stream per map, one chain for all
         linear maps, one batched inverse for both 512 x 512 systems) were all slower or equal."""
         if not getattr(self, "_in_input_hook", False):
@@ -478,14 +484,19 @@ class LyapunovLearning(nn.Module):
 
             at = getattr(self, "_prefetch_at", -1)      # tools/ab_step.py probes later capture points
 
+            late = getattr(self, "_prefetch_late_at", None)   # the maps after the first: after this conv layer
+
             def hook(i, _t=target, _at=at):
-                if i == _at:
-                    _t.after_conv_hook = None
+                if i == _at or (late is not None and i == late):
+                    if late is None or i == late:
+                        _t.after_conv_hook = None
                     self._in_input_hook = True
+                    self._prefetch_part = None if late is None else ("first" if i == _at else "rest")
                     try:
                         self._prefetch_weights(device)
                     finally:
                         self._in_input_hook = False
+                        self._prefetch_part = None
             target.after_conv_hook = hook
             return
         if self._side_streams is None:
@@ -495,11 +506,16 @@ class LyapunovLearning(nn.Module):
         for m in self.init_coordinates.modules():
             if hasattr(m, "prefetch") and m is not self.dyn_fun:
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
+        order = getattr(self, "_map_streams", (1, 2, 3, 3))   # side stream of each linear map, then dyn's
+        part = getattr(self, "_prefetch_part", None)
         for i, l in enumerate(lins):
-            l.prefetch(s[1 + min(i, 2)])
-        self.dyn_fun.prefetch(s[3])
-        for c in convs:
-            c.prefetch(s[0])
+            if part is None or (part == "first") == (i == 0):
+                l.prefetch(s[order[min(i, 2)]])
+        if part != "first":
+            self.dyn_fun.prefetch(s[order[3]])
+        if part != "rest":             # (before conv layer 0: a map prefetched later would go unused)
+            for c in convs:
+                c.prefetch(s[0])
 
     def compute_loss(self, x, y, batch_size=None, act="relu", h=None, masks=None, debug=False):
         """pl_modules.py:390-502 with the per-sample graph fused (LyapunovLossFn)."""

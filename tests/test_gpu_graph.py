@@ -259,3 +259,30 @@ def test_kappa_ramp_followed_by_captured_step():
     for a, b in zip(mod.parameters(), twin.parameters()):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
     gs.close()
+
+
+def test_placement_trials_keep_results_bit_identical():
+    """GraphTrainStep(placement_trials=3) -- captures on fresh side streams, the fastest kept, the
+    trial replays' updates undone -- replays the same losses and parameters, bit for bit, as a
+    single capture from the same state."""
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    out = {}
+    for trials in (1, 3):
+        mod = bench.build_module(dev, seed=0, train_ode=True)
+        mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        opt = mod.configure_optimizers(capturable=True)[0][0]
+        gs = GraphTrainStep(mod, opt, x, y, warmup=2, placement_trials=trials)
+        assert (gs.placement_ms is None) == (trials == 1)
+        assert int(mod.rng_counter) == 0 and mod.global_step == 0
+        losses = [float(gs.step()) for _ in range(3)]
+        torch.cuda.synchronize()
+        out[trials] = (losses, [p.detach().clone() for p in mod.parameters()])
+        gs.close()
+    assert len(out[3][0]) == 3 and out[1][0] == out[3][0]
+    for a, b in zip(out[1][1], out[3][1]):
+        assert torch.equal(a, b)

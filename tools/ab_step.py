@@ -35,7 +35,9 @@ def make(setup):
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
+    import os
     return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False),
+                          placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "1")),
                           split=getattr(mod, "_split", None))
 
 
@@ -158,7 +160,44 @@ def late_scale(m):
     RESTORE.append(lambda: setattr(LY.LyapODELossFn, "backward", staticmethod(nb)))
 
 
-ALL = {"default": default, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
+def ms_213(m):
+    m._map_streams = (2, 1, 3, 3)       # the 4096 -> 512 map on side stream 2, 512 -> 512 on 1
+
+
+def ms_321(m):
+    m._map_streams = (3, 2, 1, 1)
+
+
+def ms_3222(m):
+    m._map_streams = (3, 2, 2, 2)
+
+
+def ms_0(m):
+    m._map_streams = (0, 2, 3, 3)       # the 4096 -> 512 map on the conv maps' stream
+
+
+def all_first(m):
+    m._prefetch_late_at = None  # every map prefetched right after the input kernels (before r04bc)
+
+
+def late0(m):
+    m._prefetch_late_at = 0     # the 4096 -> 512 map before the conv stack, the other maps after conv 0
+
+
+def late1(m):
+    m._prefetch_late_at = 1
+
+
+def late2(m):
+    m._prefetch_late_at = 2
+
+
+def late3(m):
+    m._prefetch_late_at = 3     # ... after the last conv layer
+
+
+ALL = {"default": default, "all_first": all_first, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
+       "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
        "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
        "split": split, "split_serial": split_serial, "old_seed": old_seed,
