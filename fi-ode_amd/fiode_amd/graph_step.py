@@ -172,9 +172,9 @@ class GraphTrainStep:
         a recapture on the same streams reproduces its time (tools/probes/placement_probe.py,
         DESIGN.md section 4).  Each trial captures on fresh pool streams for the module's map
         prefetch and ODE solve and times a few replays; the winner's streams are restored and
-        captured again.  The replays' updates are undone (parameters, optimizer state, Philox
-        counter, step count, maps computed ahead) -- the results of the kept graph are those of any
-        capture, bit for bit."""
+        captured again.  Every trial replays from the same state, and the replays' updates are undone
+        (parameters, optimizer state, Philox counter, step count, maps computed ahead) -- the results
+        of the kept graph are those of any capture, bit for bit."""
         import time
         m = self.module
         snap = self._snapshot()
@@ -187,6 +187,10 @@ class GraphTrainStep:
                 self.g_opt.replay()
 
         def clock():
+            # every trial replays from the same state (the adaptive solve's NFE follows the state)
+            self._restore(snap)
+            m.global_step = gstep
+            self.refresh_maps()
             best = float("inf")
             for _ in range(2):
                 for _ in range(2):

@@ -508,10 +508,12 @@ class LyapunovLearning(nn.Module):
                 (convs if hasattr(m, "spectral_weight") else lins).append(m)
         order = getattr(self, "_map_streams", (1, 2, 3, 3))   # side stream of each linear map, then dyn's
         part = getattr(self, "_prefetch_part", None)
+        nfirst = getattr(self, "_prefetch_first_lins", 1)       # linear maps in the first stage
+        dyn_first = getattr(self, "_prefetch_dyn_first", False)
         for i, l in enumerate(lins):
-            if part is None or (part == "first") == (i == 0):
+            if part is None or (part == "first") == (i < nfirst):
                 l.prefetch(s[order[min(i, 2)]])
-        if part != "first":
+        if part is None or (part == "first") == dyn_first:
             self.dyn_fun.prefetch(s[order[3]])
         if part != "rest":             # (before conv layer 0: a map prefetched later would go unused)
             for c in convs:

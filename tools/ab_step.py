@@ -176,6 +176,19 @@ def ms_0(m):
     m._map_streams = (0, 2, 3, 3)       # the 4096 -> 512 map on the conv maps' stream
 
 
+def first_ab(m):
+    m._prefetch_first_lins = 2  # the 4096 -> 512 and 512 -> 512 maps before the conv stack
+
+
+def first_dyn(m):
+    m._prefetch_dyn_first = True   # the dynamics' maps before the conv stack too
+
+
+def late2_first_ab(m):
+    m._prefetch_first_lins = 2
+    m._prefetch_dyn_first = True
+
+
 def all_first(m):
     m._prefetch_late_at = None  # every map prefetched right after the input kernels (before r04bc)
 
@@ -196,7 +209,8 @@ def late3(m):
     m._prefetch_late_at = 3     # ... after the last conv layer
 
 
-ALL = {"default": default, "all_first": all_first, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
+ALL = {"default": default, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
+       "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
        "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
