@@ -203,18 +203,28 @@ class GraphTrainStep:
                 best = min(best, (time.perf_counter() - t) / reps)
             return best
 
-        def streams():
-            return (getattr(m, "_side_streams", None), getattr(m, "_ode_stream", None))
+        stores = [c._store for c in self.piped if getattr(c, "_store", None) is not None]
 
+        def streams():
+            return (getattr(m, "_side_streams", None), getattr(m, "_ode_stream", None),
+                    [st["stream"] for st in stores], getattr(self, "capture_stream", None))
+
+        def use(sv):
+            m._side_streams, m._ode_stream, conv, self.capture_stream = sv
+            for st, cs in zip(stores, conv):
+                st["stream"] = cs
+
+        dev = self.static_x.device
         trials_t = [(clock(), streams())]
         for _ in range(trials - 1):
-            m._side_streams = None
-            m._ode_stream = None
+            # fresh pool streams for the maps' prefetch, the ODE solve, the conv maps computed ahead
+            # and the capture itself
+            use((None, None, [torch.cuda.Stream(dev) for _ in stores], torch.cuda.Stream(dev)))
             self._capture()
             trials_t.append((clock(), streams()))
         best = min(range(len(trials_t)), key=lambda i: trials_t[i][0])
         if best != len(trials_t) - 1:
-            m._side_streams, m._ode_stream = trials_t[best][1]
+            use(trials_t[best][1])
             self._capture()
         torch.cuda.synchronize()
         self._restore(snap)
@@ -234,7 +244,8 @@ class GraphTrainStep:
         # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it
         # ("operation not permitted when stream is capturing" -> the watchdog terminates the process)
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb, capture_error_mode="thread_local"):
+        with torch.cuda.graph(self.g_fb, stream=getattr(self, "capture_stream", None),
+                              capture_error_mode="thread_local"):
             self.loss = self._fwd_bwd()
             if self.one_graph:
                 self.opt.step()
@@ -242,7 +253,8 @@ class GraphTrainStep:
         self.g_opt = None
         if not self.one_graph:
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self.g_opt, stream=getattr(self, "capture_stream", None),
+                                  capture_error_mode="thread_local"):
                 self.opt.step()
                 self._refresh_late()
 
