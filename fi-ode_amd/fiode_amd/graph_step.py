@@ -222,7 +222,15 @@ class GraphTrainStep:
             use((None, None, [torch.cuda.Stream(dev) for _ in stores], torch.cuda.Stream(dev)))
             self._capture()
             trials_t.append((clock(), streams()))
-        best = min(range(len(trials_t)), key=lambda i: trials_t[i][0])
+        times = [t for t, _ in trials_t]
+        import torch.distributed as dist
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            # N ranks: one decision for all (the slowest rank's time per trial), so every rank
+            # captures the same number of times -- the captured collectives stay in step
+            tt = torch.tensor(times, dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            times = tt.tolist()
+        best = min(range(len(times)), key=lambda i: times[i])
         if best != len(trials_t) - 1:
             use(trials_t[best][1])
             self._capture()
@@ -233,7 +241,7 @@ class GraphTrainStep:
         self.n_replays = 0
         self.refresh_maps()
         torch.cuda.synchronize()
-        self.placement_ms = [round(t * 1e3, 4) for t, _ in trials_t]
+        self.placement_ms = [round(t * 1e3, 4) for t in times]
         self.placement_pick = best
 
     def _capture(self):

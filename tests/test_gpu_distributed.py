@@ -142,6 +142,13 @@ def _world1_main(port, q, comm):
             opt = mod.configure_optimizers(capturable=True)[0][0]
             if mode == "ref":
                 gs = GraphTrainStep(mod, opt, x, y, warmup=2)
+            elif comm == "graph_placement":
+                # the one-graph step with the collectives captured, picked from 3 placements (the
+                # decision all-reduced over the ranks; bench.py's N-rank configuration)
+                red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
+                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm="graph", force_comm=True,
+                                    split=False, placement_trials=3)
+                assert gs.comm == "graph" and not gs.split and len(gs.placement_ms) == 3
             else:
                 red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
                 gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True,
@@ -162,7 +169,7 @@ def _world1_main(port, q, comm):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["graph", "eager"])
+@pytest.mark.parametrize("comm", ["graph", "eager", "graph_placement"])
 def test_world1_rccl_bucketed_allreduce_equals_single(comm):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
