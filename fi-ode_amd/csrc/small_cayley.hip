@@ -88,31 +88,35 @@ __device__ __forceinline__ void wave_gj16(float (*m)[KM + 1], int k) {
   for (int e = 0; e < 4; ++e) m[i][4 * cg + e] = x[e];
 }
 
-// Copy the n = R k floats of one matrix (W layout) into LDS in the tall layout, 8 loads in flight
-// per thread (a strided loop with one load per trip waits out the full memory latency each trip).
-// Returns this thread's sum of squares of the values it loaded (fixed order).
-__device__ __forceinline__ float load_tall(const SCArgs& a, const float* __restrict__ src, float* dst) {
+// Copy the n = R k floats (n <= FIODE_SMALL_CAYLEY_MAX_RK = 32 x 256) of one or two matrices (W
+// layout) into LDS in the tall layout with every load in flight at once (one memory round trip:
+// the 512 -> 10 map's backward took six dependent round trips with 8 loads per thread in flight).
+// Returns this thread's sum of squares of the first matrix's values it loaded (fixed order).
+constexpr int LMAX = FIODE_SMALL_CAYLEY_MAX_RK / NT;
+__device__ __forceinline__ float load_tall(const SCArgs& a, const float* __restrict__ src, float* dst,
+                                           const float* __restrict__ src2 = nullptr, float* dst2 = nullptr) {
   const int tid = threadIdx.x, k = a.k, n = a.R * a.k;
+  float v[LMAX], v2[LMAX];
+#pragma unroll
+  for (int u = 0; u < LMAX; ++u) {
+    const int w = u * NT + tid;
+    v[u] = w < n ? src[w] : 0.f;
+    v2[u] = (src2 && w < n) ? src2[w] : 0.f;
+  }
   float ss = 0.f;
-  for (int base = 0; base < n; base += 8 * NT) {
-    float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int w = base + u * NT + tid;
-      v[u] = w < n ? src[w] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int w = base + u * NT + tid;
-      if (w < n) {
-        const int r = a.wide ? w % a.cin : w / a.cin, c = a.wide ? w / a.cin : w % a.cin;
-        dst[r * k + c] = v[u];
-        ss = fmaf(v[u], v[u], ss);
-      }
+  for (int u = 0; u < LMAX; ++u) {
+    const int w = u * NT + tid;
+    if (w < n) {
+      const int r = a.wide ? w % a.cin : w / a.cin, c = a.wide ? w / a.cin : w % a.cin;
+      dst[r * k + c] = v[u];
+      if (dst2) dst2[r * k + c] = v2[u];
+      ss = fmaf(v[u], v[u], ss);
     }
   }
   return ss;
 }
+static_assert(FIODE_SMALL_CAYLEY_MAX_RK % NT == 0, "load_tall: whole trips");
 
 // Sum over rows r in [k, R) of X[r][i] * Y[r][j] for the k*k entries (i, j), fixed order: the
 // rows are split into P = 256 / k^2 contiguous parts, each summed with 8 independent accumulators
@@ -211,8 +215,7 @@ __global__ void __launch_bounds__(NT) k_small_cayley_bwd(SCArgs a) {
   const float* Gq = a.gQ + (int64_t)b * a.cout * a.cin;
   const float nrm = a.nrm[b], al = a.alpha[b];
   const float s = al / nrm;
-  load_tall(a, Wb, Wt);
-  load_tall(a, Gq, G);
+  load_tall(a, Wb, Wt, Gq, G);
   if (tid < k * k) iv[tid / k][tid % k] = a.inv[(int64_t)b * k * k + tid];
   __syncthreads();
   for (int idx = tid; idx < R * k; idx += NT) X[idx] = Wt[idx] * s;
