@@ -48,7 +48,7 @@ __device__ __forceinline__ int64_t wpos(const DArgs& a, int r, int c) {   // X (
 // block's float4 stride): the norm the prep kernel finishes in a fixed order -- one 2-8 MB streaming
 // read over NPART x batch workgroups in place of torch's vector_norm reduction (~10 us on the dense
 // maps' forward chain).
-constexpr int NPART = 64;
+constexpr int NPART = 256;      // 8 float4 per thread of the 4096 x 512 map: two load round trips
 __global__ void __launch_bounds__(NT) k_dense_sumsq(DArgs a, float* __restrict__ part) {
   __shared__ float red[NT / 64];
   const int b = blockIdx.y;
@@ -79,7 +79,8 @@ __global__ void __launch_bounds__(NT) k_dense_sumsq(DArgs a, float* __restrict__
 __device__ __forceinline__ float dense_norm(const float* __restrict__ part, int b, float* nrm_out) {
   __shared__ float sn;
   if (threadIdx.x < 64) {
-    float v = part[b * NPART + threadIdx.x];
+    const float* pb = part + b * NPART + 4 * threadIdx.x;
+    float v = (pb[0] + pb[1]) + (pb[2] + pb[3]);
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (threadIdx.x == 0) {
       sn = sqrtf(v);
@@ -89,7 +90,7 @@ __device__ __forceinline__ float dense_norm(const float* __restrict__ part, int 
   __syncthreads();
   return sn;
 }
-static_assert(NPART == 64, "dense_norm: one partial per lane of wave 0");
+static_assert(NPART == 256, "dense_norm: four partials per lane of wave 0");
 
 __global__ void __launch_bounds__(NT) k_dense_prep(DArgs a, const float* __restrict__ G, float* __restrict__ M,
                                                    const float* __restrict__ part, float* __restrict__ nrm_out) {

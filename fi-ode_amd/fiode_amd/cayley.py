@@ -156,7 +156,7 @@ def _dense_prep(W: torch.Tensor, alpha: torch.Tensor, M: Optional[torch.Tensor] 
     if not DENSE_NORM_PARTIALS:
         nrm = torch.linalg.vector_norm(Wb, dim=(-2, -1)).contiguous()
     else:
-        # ||W|| as 64 partial sums per matrix ahead of the G GEMM, finished by the prep kernel (no
+        # ||W|| as 256 partial sums per matrix ahead of the G GEMM, finished by the prep kernel (no
         # torch reduction on the map's forward chain)
         part = torch.empty(lib.fiode_dense_norm_workspace_bytes(ct.byref(cfg)) // 4, dtype=torch.float32,
                            device=W.device)

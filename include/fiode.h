@@ -356,7 +356,7 @@ typedef struct fiode_dense_config {
 FIODE_API int fiode_dense_cayley_prep(void* stream, const fiode_dense_config* cfg, const float* W, const float* alpha,
                                       const float* nrm, const float* G, float* M);
 /* ||W[b]|| in two stream-ordered steps around the G GEMM (replaces torch.linalg.vector_norm on the
- * map's forward chain): fiode_dense_norm_partials writes 64 fixed-order partial sums of squares per
+ * map's forward chain): fiode_dense_norm_partials writes 256 fixed-order partial sums of squares per
  * matrix into the workspace; fiode_dense_cayley_prep_normed = fiode_dense_cayley_prep with the norm
  * finished from those partials (same order in every workgroup), also written to nrm_out [b]. */
 FIODE_API size_t fiode_dense_norm_workspace_bytes(const fiode_dense_config* cfg);
