@@ -320,6 +320,13 @@ def main():
         # Adam as NaN -- or a failed solve); reported, the timed work was done
         if strict and (health["status"] or not health["loss_finite"]):
             raise RuntimeError(f"unhealthy timed run: {health}")
+        # a companion line (strict=False) whose steps were skipped or whose solve failed did not
+        # train (a failed solve may even stop early): it is marked invalid, never a throughput claim
+        why = [k for k, bad in (("solve status", health["status"] != 0), ("non-finite loss", not health["loss_finite"]),
+                                ("guard-skipped steps", health["skipped_steps"] > 0)) if bad]
+        health["valid"] = not why
+        if why:
+            health["invalid_reason"] = ", ".join(why)
         health["comm"] = last.get("comm")
         if last.get("placement_ms") is not None:
             health["placement_ms"] = last["placement_ms"]     # per trial capture; the fastest is kept
@@ -376,7 +383,7 @@ def main():
         # 1e-3: cifar_train.yaml:30,32), backprop through the adaptive solve
         e3, m3, _, _, h3 = timed_run(True, args.steps, args.warmup, solver="dopri5", strict=False)
         st3 = m3.last_ode_plan["stats"].cpu().tolist()
-        dopri5_step = {"images_per_s": round(world * B_PER_RANK * args.steps / e3, 2),
+        dopri5_step = {"valid": h3["valid"], "images_per_s": round(world * B_PER_RANK * args.steps / e3, 2),
                        "ms_per_step": round(e3 / args.steps * 1e3, 4), "device_status": h3,
                        "last_solve": {"nfe": st3[0], "n_accept": st3[4], "n_reject": st3[5]},
                        "workload": "BASELINE configs[2]: the configs[1] step with train_ode_solver dopri5, "
@@ -389,7 +396,8 @@ def main():
         k4 = max(1, min(args.steps, 10))
         e4, m4, _, _, h4 = timed_run(True, k4, 2, solver="dopri5", batch=1024, h_sample=1024, strict=False)
         st4 = m4.last_ode_plan["stats"].cpu().tolist()
-        large_batch = {"images_per_s": round(world * 1024 * k4 / e4, 2), "ms_per_step": round(e4 / k4 * 1e3, 4),
+        large_batch = {"valid": h4["valid"], "images_per_s": round(world * 1024 * k4 / e4, 2),
+                       "ms_per_step": round(e4 / k4 * 1e3, 4),
                        "steps": k4, "rows_per_rank": 1024 * 1024, "device_status": h4,
                        "last_solve": {"nfe": st4[0], "n_accept": st4[4], "n_reject": st4[5]},
                        "workload": "BASELINE configs[4]: train step at B=1024 x h_sample 1024 per rank (S1=819 "

@@ -14,7 +14,9 @@
 // Step guard (fiode_step_guard): a step whose train_ode solve failed (status word) or whose loss is
 // not finite -- or, on N ranks, any rank's such step (the guard slot of the all-reduced gradient
 // bucket) -- leaves p, m, v and the step counts as they were, like torch.cuda.amp's found_inf skip
-// but decided on the device; k_adam_steps counts the skipped steps in a sticky word.
+// but decided on the device; k_adam_steps counts the skipped steps in a sticky word.  Unlike
+// found_inf the guard does not scan the gradients: a finite loss with a non-finite gradient still
+// updates; a caller that needs that check writes it into the guard's flag word.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -169,12 +171,13 @@ extern "C" int fiode_adam_step(void* stream, const fiode_adam_config* cfg, float
     a.t_dev[i] = step ? step[i] : nullptr;
   }
   a.blk0[a.n] = (int)blocks;
-  if (blocks == 0) return FIODE_OK;
+  // the step counts advance even when every tensor is empty (torch's Adam counts such steps too)
   if (cfg->increment_steps) {
     hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     const hipError_t e0 = hipGetLastError();
     if (e0 != hipSuccess) return FIODE_EHIP + (int)e0;
   }
+  if (blocks == 0) return FIODE_OK;
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;

@@ -1452,8 +1452,8 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   // the reduction granules still hold the forward's last tags (and a previous sweep's on the same
   // workspace): continue the epoch sequence where the last user of the workspace left it, so no
   // stale granule can carry a current tag.  Every workgroup reads imeta[3] before its first
-  // exchange; workgroup 0 advances it only after its last exchange, which no workgroup passes
-  // before all have published theirs.
+  // exchange; workgroup 0 advances it only after its last exchange completed, which no workgroup
+  // passes before all have published theirs (end of the kernel).
   unsigned rep = (unsigned)a.imeta[3];
   if (rep == 0u) rep = 1u;
   int buf = 0;
@@ -1692,7 +1692,13 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   float gy0[C];
   vjp(gf0, gy0);                     // eval 0: f0 = f(y0)
   (void)gy0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.imeta[3] = (int32_t)rep;
+  // Only a sweep whose every exchange completed advances the epoch word: then every workgroup has
+  // published its last exchange, whose tag was computed from the imeta[3] it read at the start, so
+  // no workgroup can still read the word after this store.  A sweep with a timed-out exchange (its
+  // outputs are NaN) moves the word far past any tag it may have written, so a later sweep on the
+  // same workspace cannot match them.
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !S.dead) a.imeta[3] = (int32_t)rep;
+  if (threadIdx.x == 0 && S.dead) atomicMax(a.imeta + 3, (int32_t)(rep + 65536u));
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }

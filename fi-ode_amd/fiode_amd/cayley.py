@@ -306,96 +306,6 @@ class _SmallCayleyFn(torch.autograd.Function):
         return gW.reshape(wshape), ga.reshape(ashape)
 
 
-def map_forward(W: torch.Tensor, alpha: torch.Tensor):
-    """cayley_scaled(W, alpha) of a real ROCm matrix (or a per-matrix batch) with the fused kernels
-    and no autograd: (Q, saved) where ``saved`` = (kind, Wb, al, nrm, inv) is what map_backward
-    needs -- the forward of _SmallCayleyFn (k <= 16) or _DenseCayleyFn, exactly."""
-    from . import ops, _lib as L
-    if SMALL_FUSED and _small_ok(W):
-        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
-        al = alpha.detach().reshape(-1).contiguous().float()
-        b, cout, cin = Wb.shape
-        k = min(cout, cin)
-        Q = torch.empty_like(Wb)
-        inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
-        nrm = torch.empty(b, dtype=torch.float32, device=W.device)
-        L.check(L.lib().fiode_small_cayley_forward(ops._stream(W.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
-                                                   Q.data_ptr(), inv.data_ptr(), nrm.data_ptr()),
-                "fiode_small_cayley_forward")
-        return Q.reshape(W.shape), ("small", Wb, al, nrm, inv)
-    st, M = _dense_prep(W, alpha)
-    inv = _block_inverse(M)
-    Q = _dense_finish(st, inv)
-    return Q.reshape(W.shape), ("dense", st["Wb"], st["al"], st["nrm"], inv)
-
-
-def map_backward(saved, gQ: torch.Tensor, wshape, ashape):
-    """(dL/dW, dL/dalpha) of map_forward's map from dL/dQ: the backward of _SmallCayleyFn /
-    _DenseCayleyFn, exactly."""
-    from . import ops, _lib as L
-    kind, Wb, al, nrm, inv = saved
-    if kind == "dense":
-        return _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape)
-    b, cout, cin = Wb.shape
-    gQb = gQ.reshape(b, cout, cin).contiguous().float()
-    gW = torch.empty_like(Wb)
-    ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
-    L.check(L.lib().fiode_small_cayley_backward(ops._stream(Wb.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
-                                                nrm.data_ptr(), inv.data_ptr(), gQb.data_ptr(), gW.data_ptr(),
-                                                ga.data_ptr()), "fiode_small_cayley_backward")
-    return gW.reshape(wshape), ga.reshape(ashape)
-
-
-class MapStore:
-    """A dense / small Cayley map computed AHEAD into fixed buffers (the split training step,
-    graph_step.GraphTrainStep(split=True)): ``Q`` is a leaf tensor (requires_grad) that the layer
-    uses in place of cayley_scaled(W, alpha), so the step's backward stops at it and leaves dL/dQ in
-    ``Q.grad``; ``backward()`` turns that into (dL/dW, dL/dalpha) with the stored inverse, and
-    ``refresh()`` recomputes the map from the current parameters into the same buffers -- the same
-    kernels on the same parameters as a map computed at the start of the next step, so the same Q
-    bit for bit.  ``weight_fn`` / ``alpha_fn`` give the map's input (e.g. a stack of several
-    layers' weights); ``wshape`` / ``ashape`` its shapes; ``grads_fn(gW, ga)`` -> the
-    [(parameter, gradient)] pairs of the map's parameters (default: weight_fn() / alpha_fn() are
-    the parameters themselves)."""
-
-    def __init__(self, weight_fn, alpha_fn, grads_fn=None, params=None):
-        self.weight_fn, self.alpha_fn = weight_fn, alpha_fn
-        self.grads_fn = grads_fn
-        self.params = list(params) if params is not None else None
-        with torch.no_grad():
-            W, a = weight_fn(), alpha_fn()
-            Q, saved = map_forward(W, a)
-        self.wshape, self.ashape = tuple(W.shape), tuple(a.shape)
-        self.Q = Q.detach().clone().requires_grad_(True)
-        kind, Wb, al, nrm, inv = saved
-        # W / alpha themselves when map_forward's operand is a view of the parameter (the backward
-        # runs before the parameter's update), else a private buffer the refresh writes into
-        params = {W.data_ptr(), a.data_ptr()}
-        keep = lambda t: t if t.data_ptr() in params else t.detach().clone()
-        self.saved = (kind, keep(Wb), keep(al), nrm.detach().clone(), inv.detach().clone())
-
-    @torch.no_grad()
-    def refresh(self) -> None:
-        Q, saved = map_forward(self.weight_fn(), self.alpha_fn())
-        self.Q.copy_(Q)
-        for dst, src in zip(self.saved[1:], saved[1:]):
-            if dst.data_ptr() != src.data_ptr():
-                dst.copy_(src)
-
-    @torch.no_grad()
-    def backward(self):
-        """(dL/dW, dL/dalpha) from Q.grad (zeros when the step left no gradient)."""
-        g = self.Q.grad if self.Q.grad is not None else torch.zeros_like(self.Q)
-        return map_backward(self.saved, g, self.wshape, self.ashape)
-
-    def param_grads(self):
-        """[(parameter, gradient)] of the map's parameters for this step (map backward)."""
-        gW, ga = self.backward()
-        if self.grads_fn is not None:
-            return self.grads_fn(gW, ga)
-        return [(self.weight_fn(), gW), (self.alpha_fn(), ga)]
-
-
 def _small_ok(W: torch.Tensor) -> bool:
     from . import _lib as L
     cout, cin = W.shape[-2], W.shape[-1]
@@ -521,7 +431,6 @@ class CayleyLinear(nn.Linear):
         self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
         self._Q = None
         self._pre = None
-        self._mstore: Optional[MapStore] = None     # map computed ahead (split training step)
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -536,27 +445,9 @@ class CayleyLinear(nn.Linear):
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
         the layers before it); the next training forward joins it."""
-        if self._mstore is not None:
-            return
         self._pre = _prefetch(stream, self.effective_weight)
 
-    def pipeline_on(self) -> bool:
-        """Keep this layer's map in a MapStore (computed now, then ahead of every step by the
-        split training step).  Only for real ROCm float32 weights."""
-        if not (self.weight.is_cuda and self.weight.dtype == torch.float32):
-            return False
-        self._mstore = MapStore(lambda: self.weight, lambda: self.alpha)
-        return True
-
-    def pipeline_off(self) -> None:
-        self._mstore = None
-
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self._mstore is not None and self.training and torch.is_grad_enabled():
-            Q = self._mstore.Q
-            self._pre = None
-            self._Q = Q.detach()
-            return F.linear(x, Q, self.bias)
         if self._pre is not None and self.training:
             Q = _take(self._pre)
             self._pre = None

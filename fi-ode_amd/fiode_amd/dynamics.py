@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .cayley import CayleyLinear, MapStore, cayley_scaled
+from .cayley import CayleyLinear, cayley_scaled
 
 
 class LipsLinear(nn.Linear):
@@ -63,30 +63,8 @@ class OrthoClassDynProjectSimplexLips(nn.Module):
     # -- parameters as the kernels take them ---------------------------------------------------
     def prefetch(self, stream) -> None:
         """Compute the next effective_weights() on a side stream (joined at the next call)."""
-        if getattr(self, "_mstore", None) is not None:
-            return
         from .cayley import _prefetch
         self._pre = _prefetch(stream, self._effective_weights)
-
-    def pipeline_on(self) -> list:
-        """Maps computed ahead (the split training step): the batched 128x10-shaped map and
-        mlp_to_mlp's map in MapStores; returns the stores."""
-        if not (self.cayley and self.hidden_to_mlp.weight.is_cuda):
-            return []
-        l1, lx, l3 = self.hidden_to_mlp, self.U_x, self.mlp_to_hidden
-        self._mstore = MapStore(lambda: torch.stack([l1.weight, lx.weight, l3.weight.t()]),
-                                lambda: torch.cat([l1.alpha, lx.alpha, l3.alpha]),
-                                grads_fn=lambda gW, ga: [(l1.weight, gW[0]), (lx.weight, gW[1]),
-                                                         (l3.weight, gW[2].t().contiguous()),
-                                                         (l1.alpha, ga[0:1]), (lx.alpha, ga[1:2]),
-                                                         (l3.alpha, ga[2:3])],
-                                params=[l1.weight, lx.weight, l3.weight, l1.alpha, lx.alpha, l3.alpha])
-        self.mlp_to_mlp.pipeline_on()
-        return [self._mstore, self.mlp_to_mlp._mstore]
-
-    def pipeline_off(self) -> None:
-        self._mstore = None
-        self.mlp_to_mlp.pipeline_off()
 
     def effective_weights(self) -> Dict[str, torch.Tensor]:
         pre = getattr(self, "_pre", None)
@@ -100,12 +78,6 @@ class OrthoClassDynProjectSimplexLips(nn.Module):
         """Q = cayley(alpha W / ||W||) for each layer (differentiable), with the biases.  The three
         128x10-shaped maps (hidden_to_mlp, U_x and the transpose of mlp_to_hidden) run as one
         batched Cayley map (per-matrix norms and alphas); mlp_to_mlp on its own."""
-        st = getattr(self, "_mstore", None)
-        if st is not None and self.training and torch.is_grad_enabled():
-            Qb = st.Q
-            return {"Q1": Qb[0], "b1": self.hidden_to_mlp.bias, "Qx": Qb[1], "bx": self.U_x.bias,
-                    "Q2": self.mlp_to_mlp._mstore.Q, "b2": self.mlp_to_mlp.bias,
-                    "Q3": Qb[2].t(), "b3": self.mlp_to_hidden.bias}
         if self.cayley:
             l1, lx, l3 = self.hidden_to_mlp, self.U_x, self.mlp_to_hidden
             Wb = torch.stack([l1.weight, lx.weight, l3.weight.t()])

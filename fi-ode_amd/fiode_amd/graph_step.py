@@ -40,16 +40,12 @@ from typing import Optional
 import torch
 
 
-SPLIT_DEFAULT = False         # the three-graph split step (see GraphTrainStep._split_backbone): measured slower
-                              # at the HIP default of 4 hardware queues
-D_CHAINS = True               # one rank: the split step's maps' chains on one stream each (_phase_d_chains)
-
 
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
                  comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False,
-                 guard: bool = True, split: Optional[bool] = None, placement_trials: int = 1):
+                 guard: bool = True, placement_trials: int = 1):
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")
@@ -90,18 +86,6 @@ class GraphTrainStep:
         # views, which the RCCL all-reduce and the optimizer graph use.
         self.persistent = False
         self.single = world == 1 and not self.force_comm
-        from .optim import _KernelStepMixin
-        if split is None:
-            split = SPLIT_DEFAULT
-        once = getattr(module, "ode_reuse_features", True) or not getattr(module, "train_ode", False)
-        # split: one rank, or N ranks whose collectives are captured (RCCL): each half all-reduces
-        # its own gradients on its own stream and process group
-        self.split = bool(split and (self.single or self.comm == "graph") and maps_ahead and once
-                          and isinstance(optimizer, _KernelStepMixin) and self._split_backbone() is not None
-                          and getattr(module.dyn_fun, "cayley", False))
-        self.stores, self.d_params, self.split_cap = [], [], {}
-        if self.split:
-            warmup = max(int(warmup), 2)
 
         # Warm-up iterations (lazy optimizer state, library handles, workspaces) run real updates on
         # the constructor's batch; the reference's Lightning loop makes no such updates, so the
@@ -112,13 +96,6 @@ class GraphTrainStep:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for it in range(warmup):
-                if self.split and it == 1:
-                    self._split_on()                # after one plain iteration (input sizes, alphas)
-                if self.split and it >= 1:
-                    self._phase1()
-                    self._phase_d()
-                    self._phase2()
-                    continue
                 if it == 0 and multi:
                     reducer.record_order()          # the order the backward finalises the gradients
                 self._fwd_bwd(bucket_plan=False)
@@ -132,16 +109,13 @@ class GraphTrainStep:
         self.skipped.zero_()
         torch.cuda.synchronize(dev)
 
-        if self.split:
-            self.refresh_maps()                     # the stores hold maps of the warm-up's parameters
-            torch.cuda.synchronize(dev)
-        elif maps_ahead:
+        if maps_ahead:
             self._maps_ahead_on()
         self.comm_fallback = None
         try:
             self._capture()
         except Exception as exc:                   # noqa: BLE001 - rethrown unless it is the comm capture
-            if self.comm != "graph" or self.split:
+            if self.comm != "graph":
                 raise
             # the collectives could not be captured by this runtime: eager bucket all-reduces
             # between two graphs instead (the reason is kept in comm_fallback)
@@ -150,9 +124,9 @@ class GraphTrainStep:
             self.comm, self.comm_fallback = "eager", repr(exc)
             self._capture()
         self.placement_ms = None
-        if placement_trials > 1 and not self.split and self.comm != "eager":
+        if placement_trials > 1 and self.comm != "eager":
             self._select_placement(int(placement_trials))
-        if self.reducer is not None and (world > 1 or self.force_comm) and not self.split:
+        if self.reducer is not None and (world > 1 or self.force_comm):
             views = [self.reducer.flat.data_ptr() <= p.grad.data_ptr() < self.reducer.flat.data_ptr()
                      + self.reducer.flat.numel() * self.reducer.flat.element_size() for p in self.params]
             if not all(views):
@@ -245,8 +219,6 @@ class GraphTrainStep:
         self.placement_pick = best
 
     def _capture(self):
-        if self.split:
-            return self._capture_split()
         self.one_graph = self.single or self.comm == "graph"
         # capture_error_mode "thread_local": the process group's watchdog thread polls its events
         # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it
@@ -308,224 +280,23 @@ class GraphTrainStep:
         checkpoint or any update outside the replays)."""
         for c in self.piped:
             c.refresh_map()
-        for st in self.stores:
-            st.refresh()
 
     def close(self) -> None:
-        """Back to maps computed at the start of each step (eager training of the same module)."""
+        """Back to maps computed at the start of each step (eager training of the same module), and
+        the optimizer's step guard disarmed: the guard reads this graph's loss / status / slot
+        tensors, which no later eager step writes, so a guard left armed would keep skipping (or
+        keep passing) on a stale verdict."""
         self.module._kappa_anchor = None
         for c in self.piped:
             c.pipeline_off()
         self.piped = []
-        if self.split:
-            from .cayley import CayleyLinear
-            for mod in self.module.modules():
-                if isinstance(mod, CayleyLinear):
-                    mod.pipeline_off()
-            if hasattr(self.module.dyn_fun, "pipeline_off"):
-                self.module.dyn_fun.pipeline_off()
-            bb = self._split_backbone()
-            if bb is not None:
-                bb.split_capture = None
-            self.stores = []
+        self._disarm_guard()
 
-    # ---- the split step ----------------------------------------------------------------------
-    # One replay = three graphs.  F1 (stream s0): the forward through the maps computed ahead, the
-    # fused loss, and the backward down to the conv stack's output (a leaf there), the dense /
-    # small maps' outputs Q (leaves: MapStore) and the head / dynamics biases.  Then, concurrently:
-    # D (stream s1): each dense / small Cayley map's backward from dL/dQ, the Adam update of the
-    # head and dynamics parameters, and their maps for the next step (MapStore.refresh); F2 (s0):
-    # the conv stack's backward from dL/d(conv output) with the conv layers' early Adam updates and
-    # next maps (the maps-ahead hooks), then Adam for the rest (conv biases).  The next F1 waits
-    # for both.  Same kernels on the same values as the one-graph step (bit-identical losses and
-    # parameters, tests/test_gpu_graph.py); what changes is that the ~0.3 ms chain of the dense
-    # maps' backward + update + next forward (latency-bound panel inverses, small GEMMs) runs on
-    # its own stream beside the conv backward instead of before / after it on the step's queue.
-    def _split_backbone(self):
-        from .models import KWLargeConcat
-        root = getattr(self.module, "init_coordinates", None)
-        if root is None:
-            return None
-        for mod in root.modules():
-            if isinstance(mod, KWLargeConcat):
-                return mod
-        return None
-
-    def _split_on(self):
-        from .cayley import CayleyConv, CayleyLinear
-        self._maps_ahead_on()
-        if self.single and not self.early:
-            raise RuntimeError("split step: the conv layers' early updates are unavailable")
-        bb = self._split_backbone()
-        bb.split_capture = self.split_cap
-        dyn = self.module.dyn_fun
-        stores, d_params = [], []
-        for mod in bb.modules():
-            if isinstance(mod, CayleyLinear):
-                if not mod.pipeline_on():
-                    raise RuntimeError("split step: a CayleyLinear map cannot be stored")
-                stores.append(mod._mstore)
-                d_params += [mod.weight, mod.alpha] + ([mod.bias] if mod.bias is not None else [])
-        dstores = dyn.pipeline_on() if hasattr(dyn, "pipeline_on") else []
-        if not dstores:
-            raise RuntimeError("split step: the dynamics maps cannot be stored")
-        stores += dstores
-        for st in dstores:
-            d_params += st.params if st.params is not None else [st.weight_fn(), st.alpha_fn()]
-        d_params += [lin.bias for lin in (dyn.hidden_to_mlp, dyn.U_x, dyn.mlp_to_mlp, dyn.mlp_to_hidden)
-                     if lin.bias is not None]
-        conv = [p for c in bb.modules() if isinstance(c, CayleyConv) for p in c.parameters()]
-        ids = {id(p) for p in d_params} | {id(p) for p in conv}
-        if len({id(p) for p in d_params}) != len(d_params) or any(id(p) not in ids for p in self.params):
-            raise RuntimeError("split step: parameters outside the conv stack, head and dynamics")
-        self.stores, self.d_params = stores, d_params
-        self.d_biases = [p for p in d_params if not any(p is q for st in stores
-                                                        for q in (st.params or [st.weight_fn(), st.alpha_fn()]))]
-        dev = self.static_x.device
-        self.s0, self.s1 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-        self.ev1, self.ev_d = torch.cuda.Event(), torch.cuda.Event()
-        self.c_params = [p for p in self.params if id(p) not in {id(q) for q in d_params}]
-        if self.comm == "graph":
-            # N ranks: one flat gradient buffer per half (+ its guard slot), all-reduced on its
-            # own stream; the D half on a second process group (= a second RCCL communicator)
-            import torch.distributed as dist
-            self.pg_d = dist.new_group(backend="nccl")
-            self.flat_d, self.view_d = self._flat(d_params)
-            self.flat_c, self.view_c = self._flat(self.c_params)
-
-    def _flat(self, params):
-        n = sum(p.numel() for p in params)
-        flat = torch.zeros(n + 1, dtype=params[0].dtype, device=params[0].device)
-        views, o = {}, 0
-        for p in params:
-            views[id(p)] = flat[o:o + p.numel()].view_as(p)
-            o += p.numel()
-        return flat, views
-
-    def _reduce_half(self, flat, views, pairs, group):
-        """N ranks: this half's gradients into its flat buffer + this rank's guard verdict in the
-        slot, one all-reduce (captured), the mean; returns the pairs on the bucket views."""
-        import torch.distributed as dist
-        torch._foreach_copy_([views[id(p)] for p, _ in pairs], [g for _, g in pairs])
-        if self._mine is not None:
-            self._mine.write_flag(flat[-1:])
-        dist.all_reduce(flat, group=group)
-        flat.div_(self.world)
-        out = [(p, views[id(p)]) for p, _ in pairs]
-        for p, v in out:
-            p.grad = v
-        return out
-
-    def _set_guard(self, slot=None, count=True):
-        if not self._guard_ok:
-            return
-        from .optim import StepGuard
-        if slot is None:
-            g = self._mine
-            self.opt.guard = StepGuard(loss=g.loss, status=g.status, skipped=self.skipped if count else None)
-        else:
-            self.opt.guard = StepGuard(flag=slot, skipped=self.skipped if count else None)
-
-    def _phase1(self):
-        m = self.module
-        for p in self.params:
-            p.grad = None
-        for st in self.stores:
-            st.Q.grad = None
-        self.split_cap.clear()
-        loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
-        if "h_leaf" not in self.split_cap:
-            raise RuntimeError("split step: the backbone did not stop at its conv output")
-        self._mine = None
-        if self._guard_ok:
-            from .optim import StepGuard
-            lo = loss.detach().reshape(1)
-            self._mine = StepGuard(loss=lo if lo.dtype == torch.float32 else None,
-                                   status=m.status_words() if hasattr(m, "status_words") else [])
-        loss.backward(self._unit_grad(loss))
-        m.rng_counter.add_(1)
-        return loss
-
-    def _phase_d(self):
-        if self.comm != "graph" and D_CHAINS:
-            return self._phase_d_chains()
-        pairs = []
-        for st in self.stores:
-            pairs += st.param_grads()
-        for b in self.d_biases:
-            pairs.append((b, b.grad if b.grad is not None else torch.zeros_like(b)))
-        if self.comm == "graph":
-            pairs = self._reduce_half(self.flat_d, self.view_d, pairs, self.pg_d)
-            self._set_guard(self.flat_d[-1:], count=False)
-        else:
-            for p, g in pairs:
-                p.grad = g                  # as after the one-graph step: p.grad = this step's gradient
-            self._set_guard(count=False)
-        self.opt.step_params(pairs)
-        for st in self.stores:
-            st.refresh()
-
-    def _phase_d_chains(self):
-        """One rank: each stored map's chain -- backward, Adam of its parameters, next map -- forked
-        on a stream of its own (the four chains are independent; the 4096 -> 512 map's is the
-        longest), the biases' Adam on the phase's stream; joined at the end."""
-        cur = torch.cuda.current_stream()
-        if len(getattr(self, "_d_streams", [])) < len(self.stores):
-            self._d_streams = [torch.cuda.Stream(cur.device) for _ in self.stores]
-        self._set_guard(count=False)
-        for st, ss in zip(self.stores, self._d_streams):
-            ss.wait_stream(cur)
-            with torch.cuda.stream(ss):
-                pairs = st.param_grads()
-                for p, g in pairs:
-                    p.grad = g              # as after the one-graph step: p.grad = this step's gradient
-                self.opt.step_params(pairs)
-                st.refresh()
-        pairs = [(b, b.grad if b.grad is not None else torch.zeros_like(b)) for b in self.d_biases]
-        self.opt.step_params(pairs)
-        for ss in self._d_streams[:len(self.stores)]:
-            cur.wait_stream(ss)
-
-    def _phase2(self):
-        sp = self.split_cap
-        torch.autograd.backward(sp["h_conv"], sp["h_leaf"].grad)
-        if self.comm == "graph":
-            # no early per-layer updates on N ranks: the conv gradients are final after the
-            # all-reduce; the conv maps are refreshed after the update
-            pairs = [(p, p.grad if p.grad is not None else torch.zeros_like(p)) for p in self.c_params]
-            self._reduce_half(self.flat_c, self.view_c, pairs, None)
-            self._set_guard(self.flat_c[-1:])
-        else:
-            self._set_guard()
-        self.opt.step()
-        self._refresh_late()
-
-    def _capture_split(self):
-        self.one_graph = False
-        self.g_fb = self.g_opt = None
-        self.g1, self.gd, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g1, stream=self.s0, capture_error_mode="thread_local"):
-            self.loss = self._phase1()
-        with torch.cuda.graph(self.gd, stream=self.s1, capture_error_mode="thread_local"):
-            self._phase_d()
-        with torch.cuda.graph(self.g2, stream=self.s0, capture_error_mode="thread_local"):
-            self._phase2()
-
-    def _replay_split(self):
-        cur = torch.cuda.current_stream(self.static_x.device)
-        self.s0.wait_stream(cur)
-        with torch.cuda.stream(self.s0):
-            self.s0.wait_event(self.ev_d)           # the previous step's head / dynamics maps
-            self.g1.replay()
-            self.ev1.record(self.s0)
-        with torch.cuda.stream(self.s1):
-            self.s1.wait_event(self.ev1)
-            self.gd.replay()
-            self.ev_d.record(self.s1)
-        with torch.cuda.stream(self.s0):
-            self.g2.replay()
-        cur.wait_stream(self.s0)
-        cur.wait_event(self.ev_d)
+    def _disarm_guard(self) -> None:
+        if hasattr(self.opt, "guard"):
+            self.opt.guard = None
+        if self.reducer is not None and hasattr(self.reducer, "guard_writer"):
+            self.reducer.guard_writer = None
 
     def _snapshot(self):
         """Copies of what a warm-up iteration changes: parameters, optimizer state (None where a
@@ -595,6 +366,7 @@ class GraphTrainStep:
         """Point the optimizer's step guard at this step's loss and solve status words (they are new
         tensors in every eager iteration; fixed graph-pool tensors inside the capture)."""
         if not self._guard_ok:
+            self._disarm_guard()            # no guard of an earlier GraphTrainStep on this optimizer
             return
         from .optim import StepGuard
         status = self.module.status_words() if hasattr(self.module, "status_words") else []
@@ -628,13 +400,6 @@ class GraphTrainStep:
             self.static_x.copy_(x, non_blocking=True)
         if y is not None:
             self.static_y.copy_(y, non_blocking=True)
-        if self.split:
-            self._replay_split()
-            m.global_step += 1
-            self.n_replays += 1
-            if self.check_every > 0 and self.n_replays % self.check_every == 0:
-                self.check_status()
-            return self.loss
         self.g_fb.replay()
         if not self.one_graph:
             self._between(warmup=False)

@@ -68,7 +68,6 @@ class KWLargeConcat(nn.Module):
 
         self.spatial_major = True
         self.fused_transforms = True      # sconv.hip rfft2 / irfft2 (+ GroupSort) around the GEMMs
-        self.split_capture = None         # dict: graph_step's split step (conv output as a leaf)
 
     def forward(self, x):
         """On ROCm the conv stack runs spatial-major ([h, w, C, B]: FFT and GEMM operands without
@@ -105,13 +104,6 @@ class KWLargeConcat(nn.Module):
                 h = m(h)
             i += 1
         h = h.permute(3, 2, 0, 1).reshape(h.shape[3], -1)
-        sp = getattr(self, "split_capture", None)
-        if sp is not None and torch.is_grad_enabled() and h.requires_grad:
-            # the split training step (graph_step.GraphTrainStep(split=True)): the step's backward
-            # stops at the conv stack's output, which is backpropagated separately
-            sp["h_conv"] = h
-            h = h.detach().requires_grad_(True)
-            sp["h_leaf"] = h
         for m in mods[i + 1:]:
             h = m(h)
         return h

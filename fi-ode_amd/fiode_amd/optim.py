@@ -194,6 +194,10 @@ class _KernelStepMixin:
                                    "(device step counts)")
             if any(on_dev) or len({float(s) for s in steps}) != 1:
                 return False                    # mixed step placement / counts: torch's path
+            if self.guard is not None:
+                # the host would count the step before the device decides to skip it, so a skipped
+                # step would still move the bias correction: guarded steps need device counts
+                raise RuntimeError("FiodeAdam: a step guard needs device step counts (capturable=True)")
             for s in steps:
                 s += 1
             host_step = float(steps[0])

@@ -147,16 +147,12 @@ def _world1_main(port, q, comm):
                 # decision all-reduced over the ranks; bench.py's N-rank configuration)
                 red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
                 gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm="graph", force_comm=True,
-                                    split=False, placement_trials=3)
-                assert gs.comm == "graph" and not gs.split and len(gs.placement_ms) == 3
+                                    placement_trials=3)
+                assert gs.comm == "graph" and len(gs.placement_ms) == 3
             else:
                 red = GradAllReducer([p for p in mod.parameters() if p.requires_grad])
-                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True,
-                                    split=True)
+                gs = GraphTrainStep(mod, opt, x, y, reducer=red, world=1, warmup=2, comm=comm, force_comm=True)
                 assert gs.comm == comm and len(red.buckets) >= 2
-                # captured collectives: the split step asked for (each half all-reduced on its own
-                # stream and communicator); between replays the one-graph step (gloo-style comm)
-                assert gs.split == (comm == "graph")
             losses = [float(gs.step()) for _ in range(3)]
             torch.cuda.synchronize()
             res[mode] = (losses, [p.detach().cpu().numpy().copy() for p in mod.parameters()])

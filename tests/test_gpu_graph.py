@@ -188,39 +188,6 @@ def test_graph_replays_without_runtime_queue_override():
     assert mod.device_status() == 0
 
 
-@pytest.mark.parametrize("train_ode", [False, True])
-def test_split_step_equals_one_graph_step(train_ode):
-    """The split step (GraphTrainStep(split=True): F1 forward + backward to the conv output and
-    the stored maps' outputs; then, on two streams, the dense / small maps' backward + update + next
-    maps, and the conv stack's backward + updates) computes the same thing as the one-graph step:
-    the same losses and parameters, bit for bit, over 3 replays."""
-    import bench
-    from fiode_amd.graph_step import GraphTrainStep
-    dev = _dev()
-    g = torch.Generator(device="cpu").manual_seed(11)
-    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
-    y = torch.randint(0, 10, (32,), generator=g).to(dev)
-    out = {}
-    for split in (True, False):
-        mod = bench.build_module(dev, seed=0, train_ode=train_ode)
-        mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
-        opt = mod.configure_optimizers(capturable=True)[0][0]
-        gs = GraphTrainStep(mod, opt, x, y, warmup=2, split=split)
-        assert gs.split == split
-        losses = [float(gs.step()) for _ in range(3)]
-        torch.cuda.synchronize()
-        gs.check_status()
-        out[split] = (losses, [p.detach().clone() for p in mod.parameters()],
-                      [{k: v.detach().clone() for k, v in s.items() if torch.is_tensor(v)} for s in opt.state.values()])
-        gs.close()
-    assert out[True][0] == out[False][0]
-    for a, b in zip(out[True][1], out[False][1]):
-        assert torch.equal(a, b)
-    for sa, sb in zip(out[True][2], out[False][2]):
-        for k in sa:
-            assert torch.equal(sa[k], sb[k]), k
-
-
 def test_kappa_ramp_followed_by_captured_step():
     """kappa_length > 0 (pl_modules.py:447-448: kappa = global_step / kappa_length * kappa while
     global_step < kappa_length): the captured step reads kappa from the device step counter, so its

@@ -119,3 +119,53 @@ def test_adam_kernel_guard_flag():
         sa, sb = opt.state[p], topt.state[r]
         assert float(sa["step"]) == float(sb["step"]) == 2.0
         assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
+
+
+def test_close_disarms_guard_for_eager_steps():
+    """After a captured step whose last replay was poisoned (NaN loss, guard verdict 'skip'), close()
+    disarms the optimizer's guard: the guard read that replay's graph-pool loss and status words,
+    which no eager step writes, so an armed leftover would skip every later step silently.  One
+    eager step after close() must move the parameters; a guard=False GraphTrainStep built on the
+    same optimizer leaves no guard either."""
+    import bench
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(23)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5")
+    mod.train_ode_max_attempts = 1                   # every solve fails: status 2, NaN loss
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y, warmup=1, check_every=0)
+    assert opt.guard is not None
+    lo = gs.step()
+    torch.cuda.synchronize()
+    assert not bool(torch.isfinite(lo)) and gs.skipped_steps() == 1
+    gs.close()
+    assert opt.guard is None
+    mod.train_ode_max_attempts = None                # a healthy eager step
+    before = [p.detach().clone() for p in mod.parameters()]
+    opt.zero_grad(set_to_none=True)
+    loss = mod.compute_loss(x, y, 32, "relu")
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(loss))
+    moved = sum(not torch.equal(a, b) for a, b in zip(before, mod.parameters()))
+    assert moved >= len(before) // 2, (moved, len(before))        # 0 if a stale guard skipped it
+    gs2 = GraphTrainStep(mod, opt, x, y, warmup=1, guard=False)
+    assert opt.guard is None
+    gs2.close()
+
+
+def test_guard_refused_with_host_step_counts():
+    """A guard on the host-count path (capturable=False) is refused: the host would count a step
+    the device then skips, moving the bias correction of every later step."""
+    from fiode_amd.optim import FiodeAdam, StepGuard
+    dev = _dev()
+    p = torch.nn.Parameter(torch.randn(64, device=dev))
+    opt = FiodeAdam([p], lr=1e-2, capturable=False)
+    opt.guard = StepGuard(flag=torch.zeros(1, device=dev))
+    p.grad = torch.randn_like(p)
+    with pytest.raises(RuntimeError, match="device step counts"):
+        opt.step()

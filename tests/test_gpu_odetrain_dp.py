@@ -165,3 +165,124 @@ def test_lazy_keep_words_equal_drawn_up_front():
     assert n >= 8
     assert torch.equal(kw["dopri5"][:n], kw["rk4"][:n])
     assert int(torch.count_nonzero(kw["dopri5"][:n])) > 0
+
+
+def _attempt_log(ws, cfg, A):
+    """(accept decisions, dt, error ratio) per attempt from the device's saved attempt log."""
+    at = __import__("fiode_amd.ops", fromlist=["odetrain_saved"]).odetrain_saved(ws, cfg)["attempts"][:A].cpu()
+    return [bool(a) for a in at[:, 3].numpy()], at[:, 1].numpy(), at[:, 2].numpy()
+
+
+@pytest.mark.parametrize("B,seed", [(128, 4), (1024, 8)])
+def test_controller_unpinned_matches_float64_oracle(B, seed):
+    """The train-mode dopri5 solve against the float64 restatement (oracle/dopri5_train.py) with
+    NOTHING pinned but the dropout masks: the oracle runs its own QPs (own batch-global exits) and
+    its own step-size controller, so torchdiffeq's accept rule ratio <= 1 (models.py:235-241,
+    RKAdaptiveStepsizeODESolver) decides every attempt on the oracle side.  B = 1,024 is configs[4]'s
+    per-rank batch.  The device must take the same attempts (NFE, accept / reject sequence), its
+    per-attempt dt and error ratio must agree to float32-vs-float64 precision, and y(t1) must agree
+    within 1e-3: each eval's QP solution is only fixed to the bisection resolution (the batch-global
+    exit at max |eps| < 1e-4), and the solve chains ~190 evals through the stages."""
+    ops, dev, P, x, h0, cfg, masks, w = _setup(B, seed, 1e-3)
+    dyn = ops.DynCfg(scale_nominal=False, dropout=0.5)
+    xt, h0t = torch.from_numpy(x).to(dev), torch.from_numpy(h0).to(dev)
+    y, st, ws = ops.odetrain_forward(xt, h0t, w, dyn, cfg, masks=torch.from_numpy(masks).to(dev))
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[3] == 0, s
+    nfe, A = int(s[0]), int(s[6])
+    acc, dts, ratios = _attempt_log(ws, cfg, A)
+    W64 = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).double() for k in KEYS}
+    tr = D.Trace()
+    with torch.no_grad():
+        yr, info = D.dopri5_train(torch.from_numpy(x).double(), torch.from_numpy(h0).double(), W64,
+                                  torch.from_numpy(masks), 0.0, 1.0, 1e-3, 1e-3, scale_nominal=False, p=0.5,
+                                  max_attempts=64, trace=tr)
+    oacc = [r["accept"] for r in tr.attempts]
+    odt = np.array([float(r["dt"]) for r in tr.attempts])
+    orat = np.array([float(r["ratio"]) for r in tr.attempts])
+    print(f"B={B}: device nfe {nfe} attempts {A} ({sum(acc)} accepted); oracle nfe {info['nfe']} attempts "
+          f"{len(oacc)} ({sum(oacc)} accepted); min |ratio - 1| {float(np.abs(orat - 1).min()):.3e}")
+    assert (info["nfe"], oacc) == (nfe, acc)
+    assert np.allclose(dts, odt, rtol=1e-3, atol=0), np.abs(dts / odt - 1).max()
+    assert np.allclose(ratios, orat, rtol=2e-2, atol=1e-3), np.abs(ratios - orat).max()
+    err = float((y.cpu().double() - yr).abs().max())
+    print(f"B={B}: max |y_dev - y_oracle| {err:.3e}")
+    assert err <= 1e-3, err
+
+
+def test_config5_nan_state_reproduced_by_oracle():
+    """configs[4] (B = 1,024 x S = 1,024, train_ode dopri5 tol 1e-3): the captured training step of
+    bench.py's module skips its third step on a NaN loss -- F.nll_loss(torch.log(y_hat), y)
+    (pl_modules.py:494-497) of a solve whose y_hat[label] <= 0 for some images.  At that state (the
+    parameters after two updates, the same batch), the solve is re-run on the device with the same
+    Philox dropout stream and its keep words exported, and the float64 oracle (own QPs, own
+    controller, the same keep masks) is run on the same features and weights: the oracle must also
+    drive those images' label component to <= 0, i.e. the reference's own arithmetic takes the log of
+    a non-positive value there and the NaN is not a device artefact.  A float32 run of the oracle is
+    reported beside it."""
+    import bench
+    from fiode_amd import _lib as L, ops
+    from fiode_amd.graph_step import GraphTrainStep
+    from tests.test_gpu_sampler import masks_from_keep_words
+    dev = _dev()
+    B, S = 1024, 1024
+    mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5", h_sample=S)
+    mod.seed = 1000
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = torch.rand(B, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (B,), generator=g).to(dev)
+    gs = GraphTrainStep(mod, opt, x, y, check_every=0)
+    nan_step = None
+    for i in range(8):
+        loss = gs.step()
+        torch.cuda.synchronize()
+        if not bool(torch.isfinite(loss).all()):
+            nan_step = i
+            break
+    assert nan_step is not None, "no NaN step in 8 replays"
+    assert gs.skipped_steps() == 1                 # the guard kept the update away
+    yh_graph = mod.last_plan["y_hat"].detach().clone()
+    counter = int(mod.rng_counter.item()) - 1      # the replay's Philox offset (advanced after it)
+    gs.close()
+    with torch.no_grad():
+        feat = mod.init_coordinates.param_map(x).float().contiguous()
+        w = {k: v.detach().float().contiguous() for k, v in mod.dyn_fun.effective_weights().items()}
+    cfg = ops.odetrain_config(B, 0.0, 1.0, 0.0, L.FIODE_DROPOUT_PHILOX, seed=mod.seed, offset=0, method="dopri5",
+                              rtol=1e-3, atol=1e-3, max_attempts=64)
+    h0 = torch.full((B, 10), 0.1, device=dev)
+    yd, st, ws = ops.odetrain_forward(feat, h0, w, ops.DynCfg(scale_nominal=False, dropout=0.5), cfg,
+                                      offset_dev=torch.tensor([counter], dtype=torch.int64, device=dev))
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[3] == 0, s
+    nfe, A = int(s[0]), int(s[6])
+    lab = y.long().cpu()
+    yl_dev = yd.cpu().double().gather(1, lab[:, None])[:, 0]
+    yl_graph = yh_graph.cpu().double().gather(1, lab[:, None])[:, 0]
+    neg = torch.nonzero(yl_dev <= 0)[:, 0]
+    print(f"NaN at replay {nan_step}; graph y_hat[label] <= 0: {int((yl_graph <= 0).sum())} "
+          f"(min {float(yl_graph.min()):.3e}); re-run: {len(neg)} (min {float(yl_dev.min()):.3e}), nfe {nfe}")
+    assert len(neg) >= 1
+    masks = masks_from_keep_words(ops.odetrain_saved(ws, cfg)["keep_words"][:nfe].reshape(nfe * 2, B, 4)) \
+        .reshape(nfe, 2, B, 128).cpu()
+    acc, _, _ = _attempt_log(ws, cfg, A)
+    res = {}
+    for dt_ in (torch.float64, torch.float32):
+        Wo = {k: v.cpu().to(dt_) for k, v in w.items()}
+        tr = D.Trace()
+        with torch.no_grad():
+            yr, info = D.dopri5_train(feat.cpu().to(dt_), h0.cpu().to(dt_), Wo, masks, 0.0, 1.0, 1e-3, 1e-3,
+                                      scale_nominal=False, p=0.5, max_attempts=64, trace=tr)
+        yl = yr.double().gather(1, lab[:, None])[:, 0]
+        res[dt_] = (yl, info["nfe"], [r["accept"] for r in tr.attempts])
+        print(f"oracle {dt_}: nfe {info['nfe']} (device {nfe}), accepts equal {res[dt_][2] == acc}, "
+              f"y_hat[label] <= 0: {int((yl <= 0).sum())} (min {float(yl.min()):.3e}); at the device's "
+              f"negative images: {[round(float(v), 5) for v in yl[neg]]} vs device "
+              f"{[round(float(v), 5) for v in yl_dev[neg]]}")
+    yl64 = res[torch.float64][0]
+    # the reference's arithmetic (float64 restatement, its own QPs and controller) also reaches a
+    # non-positive label component: log(y_hat) is NaN there too
+    assert bool((yl64 <= 0).any())
+    assert bool((yl64[neg] <= 0).any())

@@ -37,8 +37,7 @@ def make(setup):
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
     import os
     return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False),
-                          placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "1")),
-                          split=getattr(mod, "_split", None))
+                          placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "1")))
 
 
 def default(m):
@@ -84,19 +83,6 @@ def lib_gmn(m):
     RESTORE.append(lambda: setattr(CY, "DENSE_GEMM", True))
 
 
-def one_graph(m):
-    m._split = False              # the round-3 step: one graph, dense maps' chain on the step's queue
-
-
-def split(m):
-    m._split = True               # the three-graph split step (GraphTrainStep split=True)
-
-
-def split_serial(m):
-    m._split = True
-    from fiode_amd import graph_step as GS
-    GS.D_CHAINS = False           # split step, the maps' chains one after another on the D stream
-    RESTORE.append(lambda: setattr(GS, "D_CHAINS", True))
 
 
 def ode_on_main(m):
@@ -213,8 +199,7 @@ ALL = {"default": default, "all_first": all_first, "first_ab": first_ab, "first_
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
-       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "one_graph": one_graph,
-       "split": split, "split_serial": split_serial, "old_seed": old_seed,
+       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "old_seed": old_seed,
        "conv_one_stream": conv_one_stream}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]

@@ -1,5 +1,5 @@
 """Which replayed step does the step guard skip, and why (not a test): the bench's configs[2]
-module (train_ode dopri5), GraphTrainStep (split or one graph), per step the loss, the solve's
+module (train_ode dopri5), GraphTrainStep, per step the loss, the solve's
 stats (nfe, status, accepted / rejected, attempts), its status word and the skip count."""
 import pathlib
 import sys
@@ -13,7 +13,7 @@ import bench  # noqa: E402
 from fiode_amd.graph_step import GraphTrainStep  # noqa: E402
 
 
-def run(split: bool, solver: str, steps: int = 30, B: int = 128, S: int = bench.H_SAMPLE):
+def run(solver: str, steps: int = 30, B: int = 128, S: int = bench.H_SAMPLE):
     dev = torch.device("cuda:0")
     mod = bench.build_module(dev, seed=0, train_ode=True, solver=solver, h_sample=S)
     mod.seed = 1000
@@ -21,8 +21,8 @@ def run(split: bool, solver: str, steps: int = 30, B: int = 128, S: int = bench.
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(B, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (B,), generator=g).to(dev)
-    gs = GraphTrainStep(mod, opt, x, y, split=split)
-    print(f"== split={gs.split} solver={solver}", flush=True)
+    gs = GraphTrainStep(mod, opt, x, y, check_every=0)
+    print(f"== solver={solver}", flush=True)
     prev = 0
     for i in range(steps):
         t0 = time.perf_counter()
@@ -47,7 +47,6 @@ def run(split: bool, solver: str, steps: int = 30, B: int = 128, S: int = bench.
 
 if __name__ == "__main__":
     if "--large" in sys.argv:                 # configs[4]'s shape: B=1024 x S=1024
-        run(False, "dopri5", steps=8, B=1024, S=1024)
+        run("dopri5", steps=8, B=1024, S=1024)
     else:
-        for split in (True, False):
-            run(split, "dopri5")
+        run("dopri5")
