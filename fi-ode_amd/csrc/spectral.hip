@@ -28,6 +28,7 @@
 #include "common.h"
 #include "fiode.h"
 #include "gj.h"
+#include "gjb.h"
 
 namespace {
 
@@ -483,6 +484,44 @@ __global__ void __launch_bounds__(NT) k_spec_inv(SpecArgs a) {
     }
 }
 
+// The same inverse through the real embedding E = [[Mr, -Mi], [Mi, Mr]] (2K x 2K): E^-1 =
+// [[Xr, -Xi], [Xi, Xr]] for M^-1 = Xr + i Xi, and E's symmetric part is the embedding of M's
+// Hermitian part (>= I), so E is positive-real and the blocked Gauss-Jordan of gjb.h (16-wide pivot
+// blocks in one wave's registers, MFMA rank-16 updates, look-ahead) inverts it without pivoting.
+// One workgroup per frequency as k_spec_inv, but the per-round critical path is one 16 x 16
+// in-register elimination instead of a 2 x 2 pivot round of the register-tiled complex kernel
+// (K = 64, conv 4's 40 frequencies: k_spec_inv<64> took 51 us on the step's chain).
+template <int NP, int NW>
+__global__ void __launch_bounds__(64 * NW) k_spec_inv_re(SpecArgs a) {
+  typedef fiode_gjb::GJB<NP, NW> G;
+  constexpr int K = NP / 2;
+  extern __shared__ __attribute__((aligned(16))) char gjb_smem[];
+  typename G::Smem& sm = *reinterpret_cast<typename G::Smem*>(gjb_smem);
+  const int f = blockIdx.x;
+  const c32* Mf = a.B1 + (int64_t)f * K * K;
+  for (int t = threadIdx.x; t < K * K; t += G::NT) {
+    const int i = t / K, j = t % K;
+    const c32 m = Mf[t];
+    sm.cm[i][j] = m.x;               // cm[r][c] = E[r][c] (gjb.h: row-major in, row-major out)
+    sm.cm[K + i][K + j] = m.x;
+    sm.cm[i][K + j] = -m.y;
+    sm.cm[K + i][j] = m.y;
+  }
+  __syncthreads();
+  G::invert(sm);
+  c32* Qf = a.Q + (int64_t)f * a.cout * a.cin;
+  c32* If = a.inv + (int64_t)f * K * K;
+  for (int t = threadIdx.x; t < K * K; t += G::NT) {
+    const int i = t / K, j = t % K;
+    const c32 v = make_float2(sm.cm[i][j], sm.cm[K + i][j]);
+    If[t] = v;
+    c32 q = cscale(v, 2.0f);
+    if (i == j) q.x -= 1.0f;
+    if (a.wide) Qf[(int64_t)j * a.cin + i] = q;
+    else Qf[(int64_t)i * a.cin + j] = q;
+  }
+}
+
 // Q bottom = -2 sc V inv, tile (rows K + 16 tr.., cols 16 tc..)
 __global__ void __launch_bounds__(TL * TL) k_spec_qbot(SpecArgs a) {
   __shared__ c32 Vt[TL][KP + 1], It[KP][TL + 1];
@@ -624,12 +663,20 @@ __global__ void __launch_bounds__(TL * TL) k_spec_gv(SpecArgs a) {
 }
 
 // ---- taps: TP (co, ci) pairs per block, FG frequency groups per pair ---------------------------
-constexpr int TAPS_TP = 32, TAPS_FG = 8;
-__global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
+// 256 threads = TP pairs x FG frequency groups; each thread sums its pair's frequencies f = fg,
+// fg + FG, ...  Few pairs (the 3 -> 32 first conv: 96 pairs over 544 frequencies) take FG = 64, so
+// the grid has 24 blocks and each thread 9 frequencies instead of 3 blocks with 68 each (44 us ->
+// a few us on the step's chain); the others keep FG = 8.  The root index of tap (da, db) at (ka, kb)
+// is ka da + kb db in (-1.5 n, 1.5 n): one conditional add / subtract instead of an integer modulo
+// by the runtime n per tap.
+constexpr int TAPS_THREADS = 256;
+template <int FG>
+__global__ void __launch_bounds__(TAPS_THREADS) k_spec_taps(SpecArgs a) {
+  constexpr int TP = TAPS_THREADS / FG;
   __shared__ c32 roots[64];
-  __shared__ float red[TAPS_FG][TAPS][TAPS_TP + 1];
-  const int tid = threadIdx.x, pl = tid % TAPS_TP, fg = tid / TAPS_TP;
-  for (int m = tid; m < a.n; m += TAPS_TP * TAPS_FG) roots[m] = root(m, a.n);
+  __shared__ float red[FG][TAPS][TP + 1];
+  const int tid = threadIdx.x, pl = tid % TP, fg = tid / TP;
+  for (int m = tid; m < a.n; m += TAPS_THREADS) roots[m] = root(m, a.n);
   __syncthreads();
   __shared__ float slot[2];
   float nrm;
@@ -637,8 +684,9 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
   const float D = block_sum_fixed(a.dpart, a.ndpart, &slot[1]);
   const float cw = a.alpha[0] * D / (nrm * nrm * nrm);
   if (blockIdx.x == 0 && tid == 0) a.galpha[0] = D / nrm;
-  const int pair = blockIdx.x * TAPS_TP + pl;
+  const int pair = blockIdx.x * TP + pl;
   const int npair = a.cout * a.cin;
+  const int n = a.n;
   float w[TAPS], g[TAPS];
 #pragma unroll
   for (int t = 0; t < TAPS; ++t) {
@@ -646,15 +694,15 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
     g[t] = 0.f;
   }
   if (pair < npair) {
-#pragma unroll 4
-    for (int f = fg; f < a.nf; f += TAPS_FG) {
+#pragma unroll 2
+    for (int f = fg; f < a.nf; f += FG) {
       const int ka = f / a.half, kb = f - ka * a.half;
       c32 e[TAPS];
       c32 wf = make_float2(0.f, 0.f);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
-        int m = (ka * (t / KS + SH) + kb * (t % KS + SH)) % a.n;
-        m = m < 0 ? m + a.n : m;
+        int m = ka * (t / KS + SH) + kb * (t % KS + SH);
+        m = m < 0 ? m + n : (m >= n ? m - n : m);
         e[t] = roots[m];
         wf.x = fmaf(w[t], e[t].x, wf.x);
         wf.y = fmaf(w[t], e[t].y, wf.y);
@@ -669,12 +717,12 @@ __global__ void __launch_bounds__(TAPS_TP * TAPS_FG) k_spec_taps(SpecArgs a) {
   for (int t = 0; t < TAPS; ++t) red[fg][t][pl] = g[t];
   __syncthreads();
   // fixed-order sum over the frequency groups; thread (pl, t) writes tap t of its pair
-  for (int idx = tid; idx < TAPS_TP * TAPS; idx += TAPS_TP * TAPS_FG) {
+  for (int idx = tid; idx < TP * TAPS; idx += TAPS_THREADS) {
     const int p = idx / TAPS, t = idx % TAPS;
     float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < TAPS_FG; ++q) s += red[q][t][p];
-    const int pr = blockIdx.x * TAPS_TP + p;
+#pragma unroll 8
+    for (int q = 0; q < FG; ++q) s += red[q][t][p];
+    const int pr = blockIdx.x * TP + p;
     if (pr < npair) a.gw[(int64_t)pr * TAPS + t] = s;
   }
 }
@@ -759,7 +807,12 @@ extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_
   else {
     const int nt = a.K / TL;
     hipLaunchKernelGGL(k_spec_gram, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
-    if (a.K <= 32) hipLaunchKernelGGL((k_spec_inv<32, 2, 2, 256>), dim3(a.nf), dim3(256), 0, st, a);
+    if (a.K == 32)
+      hipLaunchKernelGGL((k_spec_inv_re<64, 8>), dim3(a.nf), dim3(512), sizeof(fiode_gjb::GJB<64, 8>::Smem), st, a);
+    else if (a.K == 64)
+      hipLaunchKernelGGL((k_spec_inv_re<128, 16>), dim3(a.nf), dim3(1024), sizeof(fiode_gjb::GJB<128, 16>::Smem), st,
+                         a);
+    else if (a.K <= 32) hipLaunchKernelGGL((k_spec_inv<32, 2, 2, 256>), dim3(a.nf), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
     if (a.R > a.K) hipLaunchKernelGGL(k_spec_qbot, dim3(a.nf, ((a.R - a.K) / TL) * nt), dim3(TL * TL), 0, st, a);
   }
@@ -795,7 +848,11 @@ extern "C" int fiode_spectral_cayley_backward(void* stream, const fiode_spectral
     hipLaunchKernelGGL(k_spec_kk<true>, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a, (const c32*)a.B2, a.B1, -1.0f);
     hipLaunchKernelGGL(k_spec_gv, dim3(a.nf, (a.R / TL) * nt), dim3(TL * TL), 0, st, a);
   }
-  hipLaunchKernelGGL(k_spec_taps, dim3((a.cout * a.cin + TAPS_TP - 1) / TAPS_TP), dim3(TAPS_TP * TAPS_FG), 0, st, a);
+  const int npair = a.cout * a.cin;
+  if (npair <= 1024)
+    hipLaunchKernelGGL(k_spec_taps<64>, dim3((npair + 3) / 4), dim3(TAPS_THREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_spec_taps<8>, dim3((npair + 31) / 32), dim3(TAPS_THREADS), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
