@@ -253,6 +253,267 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
   }
 }
 
+// ---- persistent block inverse: the whole elimination in ONE launch ---------------------------
+// For n = 64 NB (NB = 2..8: the 128 x 128 dynamics map, the two 512 x 512 backbone maps) the panel
+// steps above are 1 + NB dependent launches of ~13 us each; their critical path is the look-ahead
+// pivot inversion plus a kernel boundary per step.  k_pinv runs them inside one launch:
+//   * one "chain" workgroup (blockIdx.x 0) computes every pivot block itself,
+//       X_kk^(k-1) = X_kk^(k-2) - X_k,k-1^(k-2) (P_{k-1} X_k-1,k^(k-2)),   P_k = (X_kk^(k-1))^-1
+//     (two 64^3 MFMA products + the gjb.h blocked Gauss-Jordan), and publishes P_k;
+//   * NB^2 tile workgroups each keep one 64 x 64 tile of X in registers and apply step k once P_k
+//     is published: X_kk <- P_k,  X_ik <- -X_ik P_k,  X_kj <- P_k X_kj,
+//     X_ij <- X_ij - X_ik^(k-1) (P_k X_kj^(k-1)) -- the operands of step k are tiles of version k-1,
+//     published by their owners into per-version slots (written once each: no write-after-read);
+//   * per step the chain's inputs are tiles of version k-2, so the tile workgroups have a whole
+//     pivot inversion of slack: the step's critical path is the chain's two products + one 64 x 64
+//     inversion + one hand-off of P_k, with no kernel boundary.
+// Hand-offs follow MI355X_MICROARCH.md's valid form (row 1): payload tiles are 16-B sc1 (write-
+// through) buffer stores, every storing wave drains vmcnt before the workgroup barrier, one lane
+// stores the flag (agent-scope atomic); the consumer polls it relaxed from one lane, the others
+// wait at a barrier, and every load of handed-off bytes is a 16-B sc1 buffer load.  Correctness does
+// not depend on placement or residency order (a workgroup that waits only ever waits for data of
+// earlier steps, which depend on nothing later); every spin is bounded (~0.5 s: the output turns
+// NaN).  The flags start at zero (the caller zeroes a new workspace) and the last workgroup to
+// finish zeroes them again, so no call leaves state for the next.
+// Tiles travel in the MFMA accumulator layout: f4 e = (4 w + bj) 64 + lane holds rows 16 w + 4 q
+// + (0..3), column 16 bj + i of the tile (lane = 16 q + i).
+constexpr int PI_TILE = PB * PB;                   // floats per tile
+constexpr unsigned PI_SPIN_LIMIT = 1u << 22;
+
+struct PinvWs {                                    // per-system workspace layout (floats / words)
+  static __host__ __device__ size_t flag_words(int nb) { return (size_t)nb * nb * nb + nb + 1; }
+  static __host__ __device__ size_t flag_floats(int nb) { return (flag_words(nb) + 63) / 64 * 64; }
+  static __host__ __device__ size_t total_floats(int nb) {      // + an n x n copy of the input for in == out
+    return flag_floats(nb) + (size_t)nb * nb * nb * PI_TILE + (size_t)nb * PI_TILE + (size_t)nb * nb * PI_TILE;
+  }
+  static __host__ __device__ size_t copy_offset(int nb) { return total_floats(nb) - (size_t)nb * nb * PI_TILE; }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pi_rsrc(const float* base, size_t floats) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(floats * sizeof(float)), 0x00020000);
+}
+typedef unsigned int pi_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v pi_load(__amdgpu_buffer_rsrc_t r, int e) {      // sc1: L2-served, fresh
+  const pi_u4 u = __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 16);
+  return f4v{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3])};
+}
+__device__ __forceinline__ void pi_store(__amdgpu_buffer_rsrc_t r, int e, f4v v) {   // sc1: write-through
+  const pi_u4 u = pi_u4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, e * 16, 0, 16);
+}
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+__device__ __forceinline__ void pi_signal(unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains its stores
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32_t*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane polls, the workgroup waits at the barrier; false (and *dead set) after the spin limit
+__device__ __forceinline__ void pi_wait(const unsigned* flag, int& dead) {
+  if (threadIdx.x == 0 && !dead) {
+    unsigned spins = 0;
+    while (__hip_atomic_load((gu32_t*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      if (++spins > PI_SPIN_LIMIT) {
+        dead = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+// a published tile -> LDS, column-major (B operand: dst[col][row]) or row-major (A operand)
+__device__ __forceinline__ void pi_to_bt(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = threadIdx.x + 256 * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+    *reinterpret_cast<f4v*>(&dst[16 * bj + (ln & 15)][16 * w + 4 * (ln >> 4)]) = pi_load(r, e);
+  }
+}
+__device__ __forceinline__ void pi_to_a(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = threadIdx.x + 256 * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+    const f4v v = pi_load(r, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[16 * w + 4 * (ln >> 4) + k][16 * bj + (ln & 15)] = v[k];
+  }
+}
+// this thread's accumulator registers <-> LDS (row-major A image / column-major B image)
+__device__ __forceinline__ void acc_to_a(float (*dst)[LDT], const f4v (&acc)[4], int w, int i, int q) {
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[16 * w + 4 * q + k][16 * bj + i] = acc[bj][k];
+}
+__device__ __forceinline__ void acc_to_bt(float (*dst)[LDT], const f4v (&acc)[4], int w, int i, int q) {
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj) *reinterpret_cast<f4v*>(&dst[16 * bj + i][16 * w + 4 * q]) = acc[bj];
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int64_t in_stride, float* __restrict__ out,
+                                              float* ws_all, int64_t wstride, const int32_t* __restrict__ skip) {
+  if (skip && *skip) return;                  // (uniform)
+  constexpr int n = NB * PB;
+  __shared__ __attribute__((aligned(16))) float lds[4][PB][LDT + 0];
+  __shared__ int dead;
+  const int m = blockIdx.y;
+  in += (int64_t)m * in_stride;
+  out += (int64_t)m * n * n;
+  float* ws = ws_all + (int64_t)m * wstride;
+  unsigned* tflag = reinterpret_cast<unsigned*>(ws);                 // [NB][NB][NB]
+  unsigned* pflag = tflag + NB * NB * NB;                            // [NB]
+  unsigned* arrive = pflag + NB;
+  float* V = ws + PinvWs::flag_floats(NB);                           // [NB versions][NB][NB] tiles
+  float* Pt = V + (size_t)NB * NB * NB * PI_TILE;                    // [NB] tiles
+  const size_t vfloats = (size_t)NB * NB * NB * PI_TILE;
+  const __amdgpu_buffer_rsrc_t rV = pi_rsrc(V, vfloats), rP = pi_rsrc(Pt, (size_t)NB * PI_TILE);
+  auto vtile = [&](int ver, int ti, int tj) { return ((ver * NB + ti) * NB + tj) * (PI_TILE / 4); };   // f4 index
+  auto ptile = [&](int k) { return k * (PI_TILE / 4); };
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
+  if (threadIdx.x == 0) dead = 0;
+  __syncthreads();
+  f4v acc[4];
+
+  if (blockIdx.x == 0) {
+    // ---- the chain: every pivot block and its inverse --------------------------------------------
+    typedef fiode_gjb::GJB<PB, 4> CG;
+    static_assert(sizeof(CG::Smem) <= 2 * sizeof(float) * PB * LDT, "pivot scratch fits two LDS tiles");
+    CG::Smem& sm = *reinterpret_cast<CG::Smem*>(&lds[0][0][0]);     // cm = lds[0] (row stride LDT)
+    float (*sX)[LDT] = lds[2];
+    float (*sB)[LDT] = lds[3];
+    static_assert(CG::LDM == LDT, "the pivot image doubles as the product's A operand");
+    CG::load(sm, in, PB, n);
+    __syncthreads();
+    for (int k = 0;; ++k) {
+      CG::invert(sm);                                                // cm: P_k (row-major)
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) {
+        f4v v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = sm.cm[16 * w + 4 * q + r][16 * bj + i];
+        pi_store(rP, ptile(k) + (4 * w + bj) * 64 + lane, v);
+      }
+      pi_signal(&pflag[k]);
+      if (k + 1 == NB) break;
+      // X_{k+1,k+1}^(k) = X_{k+1,k+1}^(k-1) - X_{k+1,k}^(k-1) (P_k X_{k,k+1}^(k-1))
+      const int k1 = k + 1;
+      if (k == 0) {                                                  // version -1 = the input
+        tile_load(sB, in + k1 * PB, n, true);                        // X_01 (column-major)
+        tile_load(sX, in + (int64_t)k1 * PB * n, n, false);          // X_10
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(k1 * PB + 16 * w + 4 * q + r) * n + k1 * PB + 16 * bj + i];
+      } else {
+        pi_wait(&tflag[((k - 1) * NB + k) * NB + k1], dead);
+        pi_wait(&tflag[((k - 1) * NB + k1) * NB + k], dead);
+        pi_wait(&tflag[((k - 1) * NB + k1) * NB + k1], dead);
+        pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, k1) * 4, PI_TILE));
+        pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, k1, k) * 4, PI_TILE));
+        const __amdgpu_buffer_rsrc_t rd = pi_rsrc(V + (size_t)vtile(k - 1, k1, k1) * 4, PI_TILE);
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) acc[bj] = pi_load(rd, (4 * w + bj) * 64 + lane);
+      }
+      __syncthreads();
+      f4v t[4];
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) t[bj] = f4v{0.f, 0.f, 0.f, 0.f};
+      tile_gemm(sm.cm, sB, w, i, q, t, 1.0f);                        // T = P_k X_{k,k+1}
+      __syncthreads();
+      acc_to_bt(sB, t, w, i, q);
+      __syncthreads();
+      tile_gemm(sX, sB, w, i, q, acc, -1.0f);                        // X_{k+1,k+1} - X_{k+1,k} T
+      __syncthreads();                                               // every wave is done with cm (A of T)
+      acc_to_a(sm.cm, acc, w, i, q);
+      __syncthreads();
+    }
+  } else {
+    // ---- one tile of X ---------------------------------------------------------------------------
+    const int t = blockIdx.x - 1, ti = t / NB, tj = t % NB;
+    float (*sA)[LDT] = lds[0];
+    float (*sB)[LDT] = lds[1];
+    float (*sX)[LDT] = lds[2];
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i];
+    for (int k = 0; k < NB; ++k) {
+      if (ti == tj && k == ti - 1) continue;       // X_kk^(k-1) is the chain's; nobody reads this one
+      pi_wait(&pflag[k], dead);
+      const __amdgpu_buffer_rsrc_t rp = pi_rsrc(Pt + (size_t)ptile(k) * 4, PI_TILE);
+      if (ti == k && tj == k) {                                      // X_kk <- P_k
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) acc[bj] = pi_load(rp, (4 * w + bj) * 64 + lane);
+      } else if (tj == k) {                                          // X_ik <- -X_ik P_k
+        acc_to_a(sA, acc, w, i, q);
+        pi_to_bt(sB, rp);
+        __syncthreads();
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
+        tile_gemm(sA, sB, w, i, q, acc, -1.0f);
+      } else if (ti == k) {                                          // X_kj <- P_k X_kj
+        pi_to_a(sA, rp);
+        acc_to_bt(sB, acc, w, i, q);
+        __syncthreads();
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
+        tile_gemm(sA, sB, w, i, q, acc, 1.0f);
+      } else {                                                       // X_ij - X_ik (P_k X_kj)
+        pi_to_a(sA, rp);
+        if (k == 0) {
+          tile_load(sB, in + tj * PB, n, true);                      // X_0j, column-major
+          tile_load(sX, in + (int64_t)ti * PB * n, n, false);        // X_i0
+        } else {
+          pi_wait(&tflag[((k - 1) * NB + k) * NB + tj], dead);
+          pi_wait(&tflag[((k - 1) * NB + ti) * NB + k], dead);
+          pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, tj) * 4, PI_TILE));
+          pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, ti, k) * 4, PI_TILE));
+        }
+        __syncthreads();
+        f4v r4[4];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) r4[bj] = f4v{0.f, 0.f, 0.f, 0.f};
+        tile_gemm(sA, sB, w, i, q, r4, 1.0f);                        // R_kj = P_k X_kj
+        __syncthreads();                                             // every wave is done reading sB
+        acc_to_bt(sB, r4, w, i, q);
+        __syncthreads();
+        tile_gemm(sX, sB, w, i, q, acc, -1.0f);
+      }
+      // publish version k where step k + 1 or the chain reads it
+      const bool rowcol = (ti == k + 1) != (tj == k + 1);
+      if (k + 1 < NB && (rowcol || (ti == tj && ti == k + 2))) {
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) pi_store(rV, vtile(k, ti, tj) + (4 * w + bj) * 64 + lane, acc[bj]);
+        pi_signal(&tflag[(k * NB + ti) * NB + tj]);
+      }
+      __syncthreads();                                               // LDS images reused next step
+    }
+    const float poison = dead ? __builtin_nanf("") : 0.f;
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i] = acc[bj][r] + poison;
+  }
+  // the last workgroup to finish leaves every flag zero for the next call
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add((gu32_t*)arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)(gridDim.x - 1)) {
+      for (int f = 0; f < NB * NB * NB + NB; ++f)
+        __hip_atomic_store((gu32_t*)&tflag[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32_t*)arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int NB>
+void launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, float* out, float* ws, int64_t wstride,
+                 const int32_t* skip) {
+  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(256), 0, st, in, in_stride, out, ws, wstride, skip);
+}
+
 }  // namespace
 
 extern "C" int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch, int32_t n, const void* in,
@@ -269,8 +530,13 @@ extern "C" int fiode_batched_inverse(void* stream, int32_t dtype, int32_t batch,
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
 
+namespace {
+bool pinv_shape(int n) { return n % PB == 0 && n / PB >= 2 && n / PB <= 8; }
+}  // namespace
+
 extern "C" size_t fiode_block_inverse_workspace_bytes(int32_t n) {
   if (n < 1) return 0;
+  if (pinv_shape(n)) return PinvWs::total_floats(n / PB) * sizeof(float);   // flags + tile versions + pivots
   const size_t np = (size_t)((n + PB - 1) / PB) * PB;
   return (2 * np * np + 2 * (size_t)PB * PB) * sizeof(float);   // ping-pong matrices + two pivot inverses
 }
@@ -283,6 +549,28 @@ extern "C" int fiode_block_inverse_cond(void* stream, int32_t batch, int32_t n, 
   hipStream_t st = (hipStream_t)stream;
   const int np = (n + PB - 1) / PB * PB, nb = np / PB;
   const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
+  if (pinv_shape(n)) {
+    float* ws = (float*)workspace;
+    int64_t in_stride = (int64_t)n * n;
+    if (in == out) {        // the tile workgroups write `out` while others may still read `in`: copy it
+      float* cp = ws + PinvWs::copy_offset(nb);
+      FIODE_HIP_CHECK(hipMemcpy2DAsync(cp, (size_t)wstride * sizeof(float), in, (size_t)n * n * sizeof(float),
+                                       (size_t)n * n * sizeof(float), (size_t)batch, hipMemcpyDeviceToDevice, st));
+      in = cp;
+      in_stride = wstride;
+    }
+    switch (nb) {
+      case 2: launch_pinv<2>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 3: launch_pinv<3>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 4: launch_pinv<4>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 5: launch_pinv<5>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 6: launch_pinv<6>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 7: launch_pinv<7>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      default: launch_pinv<8>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+  }
   float* A = (float*)workspace;
   float* B = A + (size_t)np * np;
   float* Pb[2] = {B + (size_t)np * np, B + (size_t)np * np + (size_t)PB * PB};

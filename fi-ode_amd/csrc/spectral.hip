@@ -667,8 +667,8 @@ __global__ void __launch_bounds__(TL * TL) k_spec_gv(SpecArgs a) {
 // fg + FG, ...  Few pairs (the 3 -> 32 first conv: 96 pairs over 544 frequencies) take FG = 64, so
 // the grid has 24 blocks and each thread 9 frequencies instead of 3 blocks with 68 each (44 us ->
 // a few us on the step's chain); the others keep FG = 8.  The root index of tap (da, db) at (ka, kb)
-// is ka da + kb db in (-1.5 n, 1.5 n): one conditional add / subtract instead of an integer modulo
-// by the runtime n per tap.
+// is ka da + kb db in (-1.5 n, 1.5 n): conditional adds / subtracts instead of an integer modulo by
+// the runtime n per tap.
 constexpr int TAPS_THREADS = 256;
 template <int FG>
 __global__ void __launch_bounds__(TAPS_THREADS) k_spec_taps(SpecArgs a) {
@@ -701,8 +701,9 @@ __global__ void __launch_bounds__(TAPS_THREADS) k_spec_taps(SpecArgs a) {
       c32 wf = make_float2(0.f, 0.f);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
-        int m = ka * (t / KS + SH) + kb * (t % KS + SH);
+        int m = ka * (t / KS + SH) + kb * (t % KS + SH);            // in (-1.5 n, 1.5 n)
         m = m < 0 ? m + n : (m >= n ? m - n : m);
+        m = m < 0 ? m + n : m;
         e[t] = roots[m];
         wf.x = fmaf(w[t], e[t].x, wf.x);
         wf.y = fmaf(w[t], e[t].y, wf.y);

@@ -61,11 +61,14 @@ class _Workspace:
     _cache: Dict[tuple, torch.Tensor] = {}
 
     @classmethod
-    def get(cls, dev: torch.device, nbytes: int, tag: str) -> torch.Tensor:
+    def get(cls, dev: torch.device, nbytes: int, tag: str, zero: bool = False) -> torch.Tensor:
+        """A cached device buffer of at least ``nbytes`` per (device, tag); ``zero``: a new buffer
+        starts zeroed (for kernels whose flag words must be zero on first use)."""
         key = (dev.index, tag)
         buf = cls._cache.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            alloc = torch.zeros if zero else torch.empty
+            buf = alloc(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
             cls._cache[key] = buf
         return buf
 
@@ -505,7 +508,9 @@ def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None,
         out = torch.empty_like(M)
     lib = L.lib()
     nb = lib.fiode_block_inverse_workspace_bytes(n) * b
-    ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}")
+    # zeroed when new: the one-launch inverse (n = 128 .. 512) keeps its hand-off flags in the workspace
+    # and leaves them zero after every call
+    ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}", zero=True)
     if skip is not None:
         skip = _need(skip.reshape(1), "skip", (1,), torch.int32, M.device)
     L.check(lib.fiode_block_inverse_cond(_stream(M.device), b, n, M.data_ptr(), out.data_ptr(), ws.data_ptr(),

@@ -94,7 +94,9 @@ def test_spectral_cayley_host_checks():
 def test_block_inverse_host_checks():
     from fiode_amd import _lib
     lib = _lib.lib()
-    assert lib.fiode_block_inverse_workspace_bytes(512) == (2 * 512 * 512 + 2 * 64 * 64) * 4
+    # n = 128 .. 512 in 64-steps: the one-launch inverse (flags, 8 versions of the 64 tiles, 8 pivot
+    # inverses, an input copy for in == out)
+    assert lib.fiode_block_inverse_workspace_bytes(512) == (576 + 8 * 64 * 4096 + 8 * 4096 + 64 * 4096) * 4
     assert lib.fiode_block_inverse_workspace_bytes(65) == (2 * 128 * 128 + 2 * 64 * 64) * 4
     assert lib.fiode_block_inverse(None, 0, None, None, None, 0) == 1
     dummy = ct.c_void_p(1)
