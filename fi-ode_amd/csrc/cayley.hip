@@ -267,10 +267,10 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
 //   * per step the chain's inputs are tiles of version k-2, so the tile workgroups have a whole
 //     pivot inversion of slack: the step's critical path is the chain's two products + one 64 x 64
 //     inversion + one hand-off of P_k, with no kernel boundary.
-// Hand-offs follow MI355X_MICROARCH.md's valid form (row 1): payload tiles are 16-B sc1 (write-
-// through) buffer stores, every storing wave drains vmcnt before the workgroup barrier, one lane
-// stores the flag (agent-scope atomic); the consumer polls it relaxed from one lane, the others
-// wait at a barrier, and every load of handed-off bytes is a 16-B sc1 buffer load.  Correctness does
+// Hand-offs follow cdna_hip_programming.md Guideline 16: payload tiles are 16-B sc1 (write-through)
+// buffer stores, every storing wave drains vmcnt before the workgroup barrier, one lane stores the
+// flag (agent-scope atomic); the consumer polls the phase's flags relaxed from one lane, takes ONE
+// agent-scope acquire, drains it before the barrier, and loads (16-B sc1 buffer loads).  Correctness does
 // not depend on placement or residency order (a workgroup that waits only ever waits for data of
 // earlier steps, which depend on nothing later); every spin is bounded (~0.5 s: the output turns
 // NaN).  The flags start at zero (the caller zeroes a new workspace) and the last workgroup to
@@ -307,8 +307,12 @@ __device__ __forceinline__ void pi_signal(unsigned* flag) {
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store((gu32_t*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// one lane polls, the workgroup waits at the barrier; false (and *dead set) after the spin limit
-__device__ __forceinline__ void pi_wait(const unsigned* flag, int& dead) {
+// one lane polls (relaxed, bounded: *dead set after the spin limit); after the last poll of a phase,
+// pi_acquire: that lane's agent-scope acquire (invalidates this CU's L1 and the L2 lines that are
+// not coherent) drained before the workgroup barrier, so no wave loads a handed-off byte from a
+// stale copy.  (sc1 loads alone were measured stale here: the n = 128 inverse read one published
+// pivot inverse as zeros, tools/probes/pinv_probe.py -- the consumer's L2 held an old copy.)
+__device__ __forceinline__ void pi_poll(const unsigned* flag, int& dead) {
   if (threadIdx.x == 0 && !dead) {
     unsigned spins = 0;
     while (__hip_atomic_load((gu32_t*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
@@ -319,7 +323,17 @@ __device__ __forceinline__ void pi_wait(const unsigned* flag, int& dead) {
       __builtin_amdgcn_s_sleep(1);
     }
   }
+}
+__device__ __forceinline__ void pi_acquire() {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
+}
+__device__ __forceinline__ void pi_wait(const unsigned* flag, int& dead) {
+  pi_poll(flag, dead);
+  pi_acquire();
 }
 // a published tile -> LDS, column-major (B operand: dst[col][row]) or row-major (A operand)
 __device__ __forceinline__ void pi_to_bt(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
@@ -348,6 +362,15 @@ __device__ __forceinline__ void acc_to_a(float (*dst)[LDT], const f4v (&acc)[4],
 __device__ __forceinline__ void acc_to_bt(float (*dst)[LDT], const f4v (&acc)[4], int w, int i, int q) {
 #pragma unroll
   for (int bj = 0; bj < 4; ++bj) *reinterpret_cast<f4v*>(&dst[16 * bj + i][16 * w + 4 * q]) = acc[bj];
+}
+
+// MFMA results consumed across control flow: hipcc (ROCm 7.2, gfx950) was seen moving an MFMA's
+// accumulator (v_accvgpr_mov) at a branch join without the wait states the dependent read needs
+// (k_pinv<2>: acc[3][3] of the column tiles read before the last 16x16x4 MFMA had written it,
+// tools/probes/pinv_probe.py).  Pinning the accumulators in AGPRs through an asm that holds the
+// SIMD for the MFMA's full latency keeps every later copy behind the write.
+__device__ __forceinline__ void mfma_settle(f4v (&acc)[4]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
 }
 
 template <int NB>
@@ -406,9 +429,10 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(k1 * PB + 16 * w + 4 * q + r) * n + k1 * PB + 16 * bj + i];
       } else {
-        pi_wait(&tflag[((k - 1) * NB + k) * NB + k1], dead);
-        pi_wait(&tflag[((k - 1) * NB + k1) * NB + k], dead);
-        pi_wait(&tflag[((k - 1) * NB + k1) * NB + k1], dead);
+        pi_poll(&tflag[((k - 1) * NB + k) * NB + k1], dead);
+        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k], dead);
+        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k1], dead);
+        pi_acquire();
         pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, k1) * 4, PI_TILE));
         pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, k1, k) * 4, PI_TILE));
         const __amdgpu_buffer_rsrc_t rd = pi_rsrc(V + (size_t)vtile(k - 1, k1, k1) * 4, PI_TILE);
@@ -420,10 +444,12 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 #pragma unroll
       for (int bj = 0; bj < 4; ++bj) t[bj] = f4v{0.f, 0.f, 0.f, 0.f};
       tile_gemm(sm.cm, sB, w, i, q, t, 1.0f);                        // T = P_k X_{k,k+1}
+      mfma_settle(t);
       __syncthreads();
       acc_to_bt(sB, t, w, i, q);
       __syncthreads();
       tile_gemm(sX, sB, w, i, q, acc, -1.0f);                        // X_{k+1,k+1} - X_{k+1,k} T
+      mfma_settle(acc);
       __syncthreads();                                               // every wave is done with cm (A of T)
       acc_to_a(sm.cm, acc, w, i, q);
       __syncthreads();
@@ -440,7 +466,13 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
       for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i];
     for (int k = 0; k < NB; ++k) {
       if (ti == tj && k == ti - 1) continue;       // X_kk^(k-1) is the chain's; nobody reads this one
-      pi_wait(&pflag[k], dead);
+      const bool generic = ti != k && tj != k;
+      pi_poll(&pflag[k], dead);
+      if (generic && k > 0) {                      // this step's operands of version k - 1
+        pi_poll(&tflag[((k - 1) * NB + k) * NB + tj], dead);
+        pi_poll(&tflag[((k - 1) * NB + ti) * NB + k], dead);
+      }
+      pi_acquire();
       const __amdgpu_buffer_rsrc_t rp = pi_rsrc(Pt + (size_t)ptile(k) * 4, PI_TILE);
       if (ti == k && tj == k) {                                      // X_kk <- P_k
 #pragma unroll
@@ -452,6 +484,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
         tile_gemm(sA, sB, w, i, q, acc, -1.0f);
+        mfma_settle(acc);
       } else if (ti == k) {                                          // X_kj <- P_k X_kj
         pi_to_a(sA, rp);
         acc_to_bt(sB, acc, w, i, q);
@@ -459,14 +492,13 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
         tile_gemm(sA, sB, w, i, q, acc, 1.0f);
+        mfma_settle(acc);
       } else {                                                       // X_ij - X_ik (P_k X_kj)
         pi_to_a(sA, rp);
         if (k == 0) {
           tile_load(sB, in + tj * PB, n, true);                      // X_0j, column-major
           tile_load(sX, in + (int64_t)ti * PB * n, n, false);        // X_i0
         } else {
-          pi_wait(&tflag[((k - 1) * NB + k) * NB + tj], dead);
-          pi_wait(&tflag[((k - 1) * NB + ti) * NB + k], dead);
           pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, tj) * 4, PI_TILE));
           pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, ti, k) * 4, PI_TILE));
         }
@@ -475,10 +507,12 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj) r4[bj] = f4v{0.f, 0.f, 0.f, 0.f};
         tile_gemm(sA, sB, w, i, q, r4, 1.0f);                        // R_kj = P_k X_kj
+        mfma_settle(r4);
         __syncthreads();                                             // every wave is done reading sB
         acc_to_bt(sB, r4, w, i, q);
         __syncthreads();
         tile_gemm(sX, sB, w, i, q, acc, -1.0f);
+        mfma_settle(acc);
       }
       // publish version k where step k + 1 or the chain reads it
       const bool rowcol = (ti == k + 1) != (tj == k + 1);

@@ -5,6 +5,8 @@
 set -u
 R=$PWD; O=$R/gpurun_out/r05c; mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 120 python -u tools/probes/pinv_probe.py 128 192 256 512 > $O/pinv.log 2>&1 || { echo probe failed; exit 1; }
+grep -E "^n=|us per call" $O/pinv.log
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_cayley.py \
     > $O/cayley.log 2>&1 || { echo "cayley tests failed"; tail -30 $O/cayley.log; exit 1; }
 tail -2 $O/cayley.log
