@@ -102,6 +102,6 @@ print("bad elements", bad.shape[0], "first", bad[:8].tolist())
 rows = sorted({int(r) for r, c in bad.tolist()})
 print("bad rows", rows)
 m = err > 1e-4
-for k in ("correct", "(P0 in01) P1", "P0 in01", "-(P0 in01)"):
+for k in ([] if not bool(m.any()) else ("correct", "(P0 in01) P1", "P0 in01", "-(P0 in01)")):
     print(f"  at the bad elements vs {k}: {float((o[m] - cands[k][m]).abs().max()):.3e}")
 print("  values", o[3, 48:52].tolist(), "correct", cands["correct"][3, 48:52].tolist())
