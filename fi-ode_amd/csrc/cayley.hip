@@ -273,15 +273,16 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
 // agent-scope acquire, drains it before the barrier, and loads (16-B sc1 buffer loads).  Correctness does
 // not depend on placement or residency order (a workgroup that waits only ever waits for data of
 // earlier steps, which depend on nothing later); every spin is bounded (~0.5 s: the output turns
-// NaN).  The flags start at zero (the caller zeroes a new workspace) and the last workgroup to
-// finish zeroes them again, so no call leaves state for the next.
+// NaN).  The flags are zeroed by a memset node in front of every launch (cdna_hip_programming.md
+// Guideline 16, "Re-initialise every call"): nothing carries over between calls, whatever else
+// the caller's workspace was used for.
 // Tiles travel in the MFMA accumulator layout: f4 e = (4 w + bj) 64 + lane holds rows 16 w + 4 q
 // + (0..3), column 16 bj + i of the tile (lane = 16 q + i).
 constexpr int PI_TILE = PB * PB;                   // floats per tile
 constexpr unsigned PI_SPIN_LIMIT = 1u << 22;
 
 struct PinvWs {                                    // per-system workspace layout (floats / words)
-  static __host__ __device__ size_t flag_words(int nb) { return (size_t)nb * nb * nb + nb + 1; }
+  static __host__ __device__ size_t flag_words(int nb) { return (size_t)nb * nb * nb + nb; }
   static __host__ __device__ size_t flag_floats(int nb) { return (flag_words(nb) + 63) / 64 * 64; }
   static __host__ __device__ size_t total_floats(int nb) {      // + an n x n copy of the input for in == out
     return flag_floats(nb) + (size_t)nb * nb * nb * PI_TILE + (size_t)nb * PI_TILE + (size_t)nb * nb * PI_TILE;
@@ -386,7 +387,6 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
   float* ws = ws_all + (int64_t)m * wstride;
   unsigned* tflag = reinterpret_cast<unsigned*>(ws);                 // [NB][NB][NB]
   unsigned* pflag = tflag + NB * NB * NB;                            // [NB]
-  unsigned* arrive = pflag + NB;
   float* V = ws + PinvWs::flag_floats(NB);                           // [NB versions][NB][NB] tiles
   float* Pt = V + (size_t)NB * NB * NB * PI_TILE;                    // [NB] tiles
   const size_t vfloats = (size_t)NB * NB * NB * PI_TILE;
@@ -530,22 +530,16 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
       for (int r = 0; r < 4; ++r)
         out[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i] = acc[bj][r] + poison;
   }
-  // the last workgroup to finish leaves every flag zero for the next call
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add((gu32_t*)arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (unsigned)(gridDim.x - 1)) {
-      for (int f = 0; f < NB * NB * NB + NB; ++f)
-        __hip_atomic_store((gu32_t*)&tflag[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32_t*)arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 template <int NB>
-void launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, float* out, float* ws, int64_t wstride,
-                 const int32_t* skip) {
+int launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, float* out, float* ws, int64_t wstride,
+                const int32_t* skip) {
+  // the flag block of every system: its first flag_floats(NB) floats (a multiple of 16 bytes)
+  FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
+                                   (size_t)batch, st));
   hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(256), 0, st, in, in_stride, out, ws, wstride, skip);
+  return FIODE_OK;
 }
 
 }  // namespace
@@ -593,15 +587,17 @@ extern "C" int fiode_block_inverse_cond(void* stream, int32_t batch, int32_t n, 
       in = cp;
       in_stride = wstride;
     }
+    int rc = FIODE_OK;
     switch (nb) {
-      case 2: launch_pinv<2>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      case 3: launch_pinv<3>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      case 4: launch_pinv<4>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      case 5: launch_pinv<5>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      case 6: launch_pinv<6>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      case 7: launch_pinv<7>(st, batch, in, in_stride, out, ws, wstride, skip); break;
-      default: launch_pinv<8>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 2: rc = launch_pinv<2>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 3: rc = launch_pinv<3>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 4: rc = launch_pinv<4>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 5: rc = launch_pinv<5>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 6: rc = launch_pinv<6>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      case 7: rc = launch_pinv<7>(st, batch, in, in_stride, out, ws, wstride, skip); break;
+      default: rc = launch_pinv<8>(st, batch, in, in_stride, out, ws, wstride, skip); break;
     }
+    if (rc) return rc;
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
   }

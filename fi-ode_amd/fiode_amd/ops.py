@@ -508,9 +508,7 @@ def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None,
         out = torch.empty_like(M)
     lib = L.lib()
     nb = lib.fiode_block_inverse_workspace_bytes(n) * b
-    # zeroed when new: the one-launch inverse (n = 128 .. 512) keeps its hand-off flags in the workspace
-    # and leaves them zero after every call
-    ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}", zero=True)
+    ws = _Workspace.get(M.device, nb, f"blockinv{torch.cuda.current_stream(M.device).cuda_stream}")
     if skip is not None:
         skip = _need(skip.reshape(1), "skip", (1,), torch.int32, M.device)
     L.check(lib.fiode_block_inverse_cond(_stream(M.device), b, n, M.data_ptr(), out.data_ptr(), ws.data_ptr(),

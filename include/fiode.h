@@ -317,9 +317,9 @@ FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64
  * 512 x 512 backbone CayleyLinears and the 128 x 128 dynamics map): block Gauss-Jordan over
  * 64-wide panels, no pivot search, no host sync.  n = 128, 192, ..., 512: ONE persistent launch
  * (cayley.hip k_pinv: a chain workgroup inverts every pivot block, one workgroup per 64 x 64 tile
- * applies the panel steps, hand-offs through flags in the workspace); other n: one update launch
- * per panel (the next pivot block is inverted inside it).  The workspace must be zeroed before its
- * first use (the kernel leaves its flag words zero after every call).  in may equal out. */
+ * applies the panel steps, hand-offs through flags in the workspace, zeroed by a memset in front of
+ * the launch); other n: one update launch per panel (the next pivot block is inverted inside it).
+ * in may equal out. */
 #define FIODE_BLOCK_INV_MAX_N 4096
 FIODE_API size_t fiode_block_inverse_workspace_bytes(int32_t n);
 FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
