@@ -41,11 +41,30 @@ import torch
 
 
 
+# The HIP runtime of this image (ROCm 7.x, torch's libamdhip64) dereferences a null internal stream in
+# its graph executor when a captured graph has more parallel branches than it can place on
+# GPU_MAX_HW_QUEUES < 4 hardware queues: a host SIGSEGV at the first replay (tools/probes/
+# hwq_branch_probe.py: any K-branch graph, K >= 2 at 1 queue, K >= 3 at 2, K = 6 / 12 at 3; none
+# up to K = 12 at the default 4).  The training step's graph has more branches than that (map
+# prefetch, the ODE solve, the conv maps computed ahead), so the capture is refused up front.
+MIN_HW_QUEUES = 4
+
+
+def _check_runtime_queues() -> None:
+    import os
+    q = os.environ.get("GPU_MAX_HW_QUEUES")
+    if q is not None and q.strip().isdigit() and int(q) < MIN_HW_QUEUES:
+        raise RuntimeError(f"GraphTrainStep: GPU_MAX_HW_QUEUES={q} < {MIN_HW_QUEUES}: this HIP runtime's graph "
+                           "executor segfaults replaying a multi-branch graph with fewer hardware queues "
+                           "(DESIGN.md section 6); unset it or use >= 4")
+
+
 class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
                  comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False,
                  guard: bool = True, placement_trials: int = 1):
+        _check_runtime_queues()
         dev = x.device
         if dev.type != "cuda":
             raise ValueError("GraphTrainStep needs ROCm device tensors")

@@ -223,3 +223,16 @@ def test_validation_metrics_synced_two_ranks():
     assert abs(l0["validation_loss"] - (a0 + a1) / 2) < 1e-6
     assert abs(l0["validation_error"] - (e0 + e1) / 2) < 1e-6
     assert l0["validation_adv_error"] == l0["validation_error"]
+
+
+def test_graph_step_refuses_too_few_hw_queues(monkeypatch):
+    """GPU_MAX_HW_QUEUES < 4: the HIP runtime's graph executor segfaults replaying a multi-branch graph
+    (tools/probes/hwq_branch_probe.py), so GraphTrainStep refuses before capturing anything."""
+    import torch
+    from fiode_amd.graph_step import GraphTrainStep
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    with pytest.raises(RuntimeError, match="GPU_MAX_HW_QUEUES=2"):
+        GraphTrainStep(None, None, torch.zeros(1), torch.zeros(1))
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    with pytest.raises(ValueError, match="ROCm device"):       # passes the queue check, then needs a GPU
+        GraphTrainStep(None, None, torch.zeros(1), torch.zeros(1))

@@ -44,7 +44,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "child":
         child(int(sys.argv[2]))
         sys.exit(0)
-    for q in ("2", "4"):
+    for q in [a for a in sys.argv[1:]] or ("2", "4"):
         for k in (2, 3, 4, 6, 8, 12):
             env = dict(os.environ, GPU_MAX_HW_QUEUES=q)
             p = subprocess.run([sys.executable, __file__, "child", str(k)], env=env, capture_output=True, text=True,
