@@ -117,12 +117,20 @@ struct GJB {
   }
 
   // Invert the NP x NP matrix X in sm.cm (column-major).  All NT threads.
-  static __device__ void invert(Smem& sm) {
+  struct NoHook {
+    __device__ void operator()() const {}
+  };
+  static __device__ void invert(Smem& sm) { invert(sm, NoHook{}, -1); }
+  // ... calling hook() (all threads, between two workgroup barriers) after round hook_round: a caller
+  // with other work for the same workgroup (e.g. issuing loads it consumes after the inversion)
+  template <class Hook>
+  static __device__ void invert(Smem& sm, Hook hook, int hook_round) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
     if (w == 0) invert_block(sm, 0, c, q);
     __syncthreads();
     for (int kb = 0; kb < NB; ++kb) {
+      if (kb == hook_round) hook();
       // (c) R = P X[K, j] for j-blocks != kb (one block per wave), and the old column panel -> cb
       for (int jb = w; jb < NB; jb += NW) {
         if (jb == kb) continue;
