@@ -375,7 +375,7 @@ __device__ __forceinline__ void mfma_settle(f4v (&acc)[4]) {
 template <int NB>
 __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int64_t in_stride, float* __restrict__ out,
                                               float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
-                                              int acq) {
+                                              int acq, unsigned long long* prof) {
   if (skip && *skip) return;                  // (uniform)
   constexpr int n = NB * PB;
   __shared__ __attribute__((aligned(16))) float lds[4][PB][LDT + 0];
@@ -394,6 +394,12 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
   auto ptile = [&](int k) { return k * (PI_TILE / 4); };
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
   if (threadIdx.x == 0) dead = 0;
+  // diagnostic timestamps (fiode_debug_pinv_profile; null in the product): prof[1024 + wg] start,
+  // chain prof[8 k + 0..3], tile t's step k end prof[256 + t NB + k]
+  auto mark = [&](int slot) {
+    if (prof && threadIdx.x == 0 && m == 0) prof[slot] = wall_clock64();
+  };
+  mark(1024 + blockIdx.x);
   __syncthreads();
   f4v acc[4];
 
@@ -428,7 +434,9 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
           nxt_d[u] = pi_load(r2, (4 * w + u) * 64 + lane);
         }
       };
+      mark(8 * k + 0);
       CG::invert(sm, fetch, 1);                                      // cm: P_k (row-major)
+      mark(8 * k + 1);
 #pragma unroll
       for (int bj = 0; bj < 4; ++bj) {
         f4v v;
@@ -437,6 +445,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
         pi_store(rP, ptile(k) + (4 * w + bj) * 64 + lane, v);
       }
       pi_signal(&pflag[k]);
+      mark(8 * k + 2);
       if (k1 == NB) break;
       // X_{k+1,k+1}^(k) = X_{k+1,k+1}^(k-1) - X_{k+1,k}^(k-1) (P_k X_{k,k+1}^(k-1))
       if (k == 0) {                                                  // version -1 = the input
@@ -470,6 +479,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
       __syncthreads();                                               // every wave is done with cm (A of T)
       acc_to_a(sm.cm, acc, w, i, q);
       __syncthreads();
+      mark(8 * k + 3);
     }
   } else {
     // ---- one tile of X ---------------------------------------------------------------------------
@@ -538,6 +548,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
         for (int bj = 0; bj < 4; ++bj) pi_store(rV, vtile(k, ti, tj) + (4 * w + bj) * 64 + lane, acc[bj]);
         pi_signal(&tflag[(k * NB + ti) * NB + tj]);
       }
+      mark(256 + t * NB + k);
       __syncthreads();                                               // LDS images reused next step
     }
     const float poison = dead ? __builtin_nanf("") : 0.f;
@@ -551,7 +562,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
 
 template <int NB>
 int launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, float* out, float* ws, int64_t wstride,
-                const int32_t* skip) {
+                const int32_t* skip, unsigned long long* prof = nullptr) {
   // the flag block of every system: its first flag_floats(NB) floats (a multiple of 16 bytes)
   FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
                                    (size_t)batch, st));
@@ -559,7 +570,7 @@ int launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, f
     const char* e = getenv("FIODE_PINV_ACQUIRE");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(256), 0, st, in, in_stride, out, ws, wstride, skip, acq);
+  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(256), 0, st, in, in_stride, out, ws, wstride, skip, acq, prof);
   return FIODE_OK;
 }
 
@@ -659,4 +670,13 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
 extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                    size_t workspace_bytes) {
   return fiode_block_inverse_batched(stream, 1, n, in, out, workspace, workspace_bytes);
+}
+
+// Diagnostic (not in fiode.h): the one-launch inverse of one n = 512 system with phase timestamps
+// (wall clock, 100 MHz) -- tools/probes/pinv_probe.py.
+extern "C" int fiode_debug_pinv_profile(void* stream, int32_t n, const float* in, float* out, void* workspace,
+                                        unsigned long long* prof) {
+  if (n != 512 || !in || !out || !workspace || !prof || in == out) return FIODE_EINVAL;
+  const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
+  return launch_pinv<8>((hipStream_t)stream, 1, in, (int64_t)n * n, out, (float*)workspace, wstride, nullptr, prof);
 }

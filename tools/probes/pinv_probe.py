@@ -105,3 +105,32 @@ m = err > 1e-4
 for k in ([] if not bool(m.any()) else ("correct", "(P0 in01) P1", "P0 in01", "-(P0 in01)")):
     print(f"  at the bad elements vs {k}: {float((o[m] - cands[k][m]).abs().max()):.3e}")
 print("  values", o[3, 48:52].tolist(), "correct", cands["correct"][3, 48:52].tolist())
+
+# phase timestamps of the n = 512 chain (fiode_debug_pinv_profile)
+import ctypes as ct  # noqa: E402
+n = 512
+g = torch.Generator().manual_seed(n)
+A = torch.randn(n, n, generator=g, dtype=torch.float64) * (1.0 / n ** 0.5)
+M = (torch.eye(n, dtype=torch.float64) + (A - A.T) + 0.3 * A.T @ A).float().to(dev)
+out = torch.empty_like(M)
+nbytes = L.lib().fiode_block_inverse_workspace_bytes(n)
+ws = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
+prof = torch.zeros(2048, dtype=torch.int64, device=dev)
+fn = L.lib().fiode_debug_pinv_profile
+fn.argtypes = [ct.c_void_p, ct.c_int32, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p]
+for _ in range(3):
+    L.lib().fiode_block_inverse(ops._stream(dev), n, M.data_ptr(), out.data_ptr(), ws.data_ptr(), nbytes)
+torch.cuda.synchronize()
+assert fn(ops._stream(dev), n, M.data_ptr(), out.data_ptr(), ws.data_ptr(), prof.data_ptr()) == 0
+torch.cuda.synchronize()
+p = prof.cpu().tolist()
+t0 = min(p[1024:1024 + 65])
+us = lambda v: (v - t0) / 100.0
+print("WG start spread (us): first", us(min(p[1024:1089])), "last", us(max(p[1024:1089])))
+for k in range(8):
+    print(f"chain k={k}: invert {us(p[8*k]):7.2f} -> {us(p[8*k+1]):7.2f}  published {us(p[8*k+2]):7.2f}  "
+          f"next D ready {us(p[8*k+3]) if k < 7 else float('nan'):7.2f}")
+ends = [[us(p[256 + t * 8 + k]) for k in range(8)] for t in range(64)]
+for k in range(8):
+    col = [ends[t][k] for t in range(64) if p[256 + t * 8 + k]]
+    print(f"tiles step {k}: first end {min(col):7.2f} last end {max(col):7.2f}")
