@@ -674,7 +674,7 @@ extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, flo
 
 // Diagnostic (not in fiode.h): the one-launch inverse of one n = 512 system with phase timestamps
 // (wall clock, 100 MHz) -- tools/probes/pinv_probe.py.
-extern "C" int fiode_debug_pinv_profile(void* stream, int32_t n, const float* in, float* out, void* workspace,
+extern "C" FIODE_API int fiode_debug_pinv_profile(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                         unsigned long long* prof) {
   if (n != 512 || !in || !out || !workspace || !prof || in == out) return FIODE_EINVAL;
   const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
