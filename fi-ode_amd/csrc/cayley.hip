@@ -277,8 +277,12 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
 // NaN).  The flags are zeroed by a memset node in front of every launch (cdna_hip_programming.md
 // Guideline 16, "Re-initialise every call"): nothing carries over between calls, whatever else
 // the caller's workspace was used for.
-// Tiles travel in the MFMA accumulator layout: f4 e = (4 w + bj) 64 + lane holds rows 16 w + 4 q
-// + (0..3), column 16 bj + i of the tile (lane = 16 q + i).
+// Tiles travel in the MFMA accumulator layout: f4 e = (4 rw + bj) 64 + lane holds rows 16 rw + 4 q
+// + (0..3), column 16 bj + i of the tile (lane = 16 q + i).  Round-5 phase timestamps of the 512
+// inverse with 4-wave workgroups (fiode_debug_pinv_profile): per step the 64 x 64 inversion 8.5 us,
+// the two products 2.8 us, the hand-off 0.7 us, the tile workgroups done ~4.5 us after P_k -- so the
+// workgroups are 8 waves: the inversion's rank-16 updates and the products spread over twice the
+// SIMDs (the tile workgroups use them too).
 constexpr int PI_TILE = PB * PB;                   // floats per tile
 constexpr unsigned PI_SPIN_LIMIT = 1u << 22;
 
@@ -334,48 +338,82 @@ __device__ __forceinline__ void pi_acquire(bool acq) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     // (no instruction: keeps the loads below)
   __syncthreads();
 }
+// 512-thread workgroups (8 waves): wave w owns rows 16 (w & 3) .. + 15 and the column blocks
+// bj = 2 (w >> 2) + b, b = 0, 1 of a tile, i.e. acc[b][r] = X[16 rw + 4 q + r][16 (2 ch + b) + i]
+// (rw = w & 3, ch = w >> 2, lane = 16 q + i) -- a 64^3 product is 32 MFMAs per wave.
+constexpr int PI_NT = 512;
 // a published tile -> LDS, column-major (B operand: dst[col][row]) or row-major (A operand)
 __device__ __forceinline__ void pi_to_bt(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = threadIdx.x + 256 * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+  for (int u = 0; u < 1024 / PI_NT; ++u) {
+    const int e = threadIdx.x + PI_NT * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
     *reinterpret_cast<f4v*>(&dst[16 * bj + (ln & 15)][16 * w + 4 * (ln >> 4)]) = pi_load(r, e);
   }
 }
 __device__ __forceinline__ void pi_to_a(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = threadIdx.x + 256 * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+  for (int u = 0; u < 1024 / PI_NT; ++u) {
+    const int e = threadIdx.x + PI_NT * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
     const f4v v = pi_load(r, e);
 #pragma unroll
     for (int k = 0; k < 4; ++k) dst[16 * w + 4 * (ln >> 4) + k][16 * bj + (ln & 15)] = v[k];
   }
 }
-// this thread's accumulator registers <-> LDS (row-major A image / column-major B image)
-__device__ __forceinline__ void acc_to_a(float (*dst)[LDT], const f4v (&acc)[4], int w, int i, int q) {
+// a 64 x 64 block of a row-major matrix (row stride ld) -> LDS, row-major or transposed
+__device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const float* __restrict__ src, int64_t ld,
+                                             bool transpose) {
 #pragma unroll
-  for (int bj = 0; bj < 4; ++bj)
+  for (int u = 0; u < PB * PB / 4 / PI_NT; ++u) {
+    const int t = threadIdx.x + PI_NT * u;
+    const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
+    const f4v v = *reinterpret_cast<const f4v*>(src + (int64_t)r * ld + c4);
+    if (transpose) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dst[16 * w + 4 * q + k][16 * bj + i] = acc[bj][k];
+      for (int e = 0; e < 4; ++e) dst[c4 + e][r] = v[e];
+    } else {
+      *reinterpret_cast<f4v*>(&dst[r][c4]) = v;
+    }
+  }
 }
-__device__ __forceinline__ void acc_to_bt(float (*dst)[LDT], const f4v (&acc)[4], int w, int i, int q) {
+// this thread's accumulator registers <-> LDS (row-major A image / column-major B image)
+__device__ __forceinline__ void acc_to_a(float (*dst)[LDT], const f4v (&acc)[2], int rw, int ch, int i, int q) {
 #pragma unroll
-  for (int bj = 0; bj < 4; ++bj) *reinterpret_cast<f4v*>(&dst[16 * bj + i][16 * w + 4 * q]) = acc[bj];
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[16 * rw + 4 * q + k][16 * (2 * ch + b) + i] = acc[b][k];
+}
+__device__ __forceinline__ void acc_to_bt(float (*dst)[LDT], const f4v (&acc)[2], int rw, int ch, int i, int q) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) *reinterpret_cast<f4v*>(&dst[16 * (2 * ch + b) + i][16 * rw + 4 * q]) = acc[b];
+}
+// acc[b] += sign A[16 rw + i][:] . BT[16 (2 ch + b) + i][:]  (the k order permuted as tile_gemm's)
+__device__ __forceinline__ void pi_gemm(const float (*A)[LDT], const float (*BT)[LDT], int rw, int ch, int i, int q,
+                                        f4v (&acc)[2], float sign) {
+#pragma unroll
+  for (int kc = 0; kc < PB / 16; ++kc) {
+    const f4v a4 = *reinterpret_cast<const f4v*>(&A[16 * rw + i][16 * kc + 4 * q]) * sign;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const f4v b4 = *reinterpret_cast<const f4v*>(&BT[16 * (2 * ch + b) + i][16 * kc + 4 * q]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[b] = fiode_gjb::mfma(a4[s], b4[s], acc[b]);
+    }
+  }
 }
 
 // MFMA results consumed across control flow: hipcc (ROCm 7.2, gfx950) was seen moving an MFMA's
 // accumulator (v_accvgpr_mov) at a branch join without the wait states the dependent read needs
-// (k_pinv<2>: acc[3][3] of the column tiles read before the last 16x16x4 MFMA had written it,
-// tools/probes/pinv_probe.py).  Pinning the accumulators in AGPRs through an asm that holds the
-// SIMD for the MFMA's full latency keeps every later copy behind the write.
-__device__ __forceinline__ void mfma_settle(f4v (&acc)[4]) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+// (k_pinv<2>: one accumulator register of the column tiles read before the last 16x16x4 MFMA had
+// written it, tools/probes/pinv_probe.py).  Pinning the accumulators in AGPRs through an asm that
+// holds the SIMD for the MFMA's full latency keeps every later copy behind the write.
+__device__ __forceinline__ void mfma_settle(f4v (&acc)[2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(acc[0]), "+a"(acc[1]));
 }
 
 template <int NB>
-__global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int64_t in_stride, float* __restrict__ out,
-                                              float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
-                                              int acq, unsigned long long* prof) {
+__global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, int64_t in_stride, float* __restrict__ out,
+                                                float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
+                                                int acq, unsigned long long* prof) {
   if (skip && *skip) return;                  // (uniform)
   constexpr int n = NB * PB;
   __shared__ __attribute__((aligned(16))) float lds[4][PB][LDT + 0];
@@ -393,6 +431,8 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
   auto vtile = [&](int ver, int ti, int tj) { return ((ver * NB + ti) * NB + tj) * (PI_TILE / 4); };   // f4 index
   auto ptile = [&](int k) { return k * (PI_TILE / 4); };
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, q = lane >> 4;
+  const int rw = w & 3, ch = w >> 2;
+  auto own_e = [&](int b) { return (4 * rw + 2 * ch + b) * 64 + lane; };   // f4 index of acc[b]
   if (threadIdx.x == 0) dead = 0;
   // diagnostic timestamps (fiode_debug_pinv_profile; null in the product): prof[1024 + wg] start,
   // chain prof[8 k + 0..3], tile t's step k end prof[256 + t NB + k]
@@ -401,11 +441,17 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
   };
   mark(1024 + blockIdx.x);
   __syncthreads();
-  f4v acc[4];
+  f4v acc[2];
+  auto load_in = [&](int r0, int c0) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[b][r] = in[(int64_t)(r0 + 16 * rw + 4 * q + r) * n + c0 + 16 * (2 * ch + b) + i];
+  };
 
   if (blockIdx.x == 0) {
     // ---- the chain: every pivot block and its inverse --------------------------------------------
-    typedef fiode_gjb::GJB<PB, 4> CG;
+    typedef fiode_gjb::GJB<PB, PI_NT / 64> CG;
     static_assert(sizeof(CG::Smem) <= 2 * sizeof(float) * PB * LDT, "pivot scratch fits two LDS tiles");
     CG::Smem& sm = *reinterpret_cast<CG::Smem*>(&lds[0][0][0]);     // cm = lds[0] (row stride LDT)
     float (*sX)[LDT] = lds[2];
@@ -415,7 +461,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
     __syncthreads();
     // the next pivot's three operand tiles (version k - 1 for step k + 1), fetched into registers
     // while the current pivot block is inverted: polled and loaded from the inversion's hook
-    f4v nxt_b[4], nxt_a[4], nxt_d[4];
+    f4v nxt_b[2], nxt_a[2], nxt_d[2];
     for (int k = 0;; ++k) {
       const int k1 = k + 1;
       auto fetch = [&]() {
@@ -428,37 +474,34 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
         const __amdgpu_buffer_rsrc_t r1 = pi_rsrc(V + (size_t)vtile(k - 1, k1, k) * 4, PI_TILE);
         const __amdgpu_buffer_rsrc_t r2 = pi_rsrc(V + (size_t)vtile(k - 1, k1, k1) * 4, PI_TILE);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          nxt_b[u] = pi_load(r0, threadIdx.x + 256 * u);
-          nxt_a[u] = pi_load(r1, threadIdx.x + 256 * u);
-          nxt_d[u] = pi_load(r2, (4 * w + u) * 64 + lane);
+        for (int u = 0; u < 2; ++u) {
+          nxt_b[u] = pi_load(r0, threadIdx.x + PI_NT * u);
+          nxt_a[u] = pi_load(r1, threadIdx.x + PI_NT * u);
+          nxt_d[u] = pi_load(r2, own_e(u));
         }
       };
       mark(8 * k + 0);
       CG::invert(sm, fetch, 1);                                      // cm: P_k (row-major)
       mark(8 * k + 1);
 #pragma unroll
-      for (int bj = 0; bj < 4; ++bj) {
+      for (int b = 0; b < 2; ++b) {
         f4v v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = sm.cm[16 * w + 4 * q + r][16 * bj + i];
-        pi_store(rP, ptile(k) + (4 * w + bj) * 64 + lane, v);
+        for (int r = 0; r < 4; ++r) v[r] = sm.cm[16 * rw + 4 * q + r][16 * (2 * ch + b) + i];
+        pi_store(rP, ptile(k) + own_e(b), v);
       }
       pi_signal(&pflag[k]);
       mark(8 * k + 2);
       if (k1 == NB) break;
       // X_{k+1,k+1}^(k) = X_{k+1,k+1}^(k-1) - X_{k+1,k}^(k-1) (P_k X_{k,k+1}^(k-1))
       if (k == 0) {                                                  // version -1 = the input
-        tile_load(sB, in + k1 * PB, n, true);                        // X_01 (column-major)
-        tile_load(sX, in + (int64_t)k1 * PB * n, n, false);          // X_10
-#pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(k1 * PB + 16 * w + 4 * q + r) * n + k1 * PB + 16 * bj + i];
+        pi_tile_load(sB, in + k1 * PB, n, true);                     // X_01 (column-major)
+        pi_tile_load(sX, in + (int64_t)k1 * PB * n, n, false);       // X_10
+        load_in(k1 * PB, k1 * PB);
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {                                // the prefetched tiles -> LDS / acc
-          const int e = threadIdx.x + 256 * u, we = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+        for (int u = 0; u < 2; ++u) {                                // the prefetched tiles -> LDS / acc
+          const int e = threadIdx.x + PI_NT * u, we = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
           *reinterpret_cast<f4v*>(&sB[16 * bj + (ln & 15)][16 * we + 4 * (ln >> 4)]) = nxt_b[u];
 #pragma unroll
           for (int r = 0; r < 4; ++r) sX[16 * we + 4 * (ln >> 4) + r][16 * bj + (ln & 15)] = nxt_a[u][r];
@@ -466,18 +509,16 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
         }
       }
       __syncthreads();
-      f4v t[4];
-#pragma unroll
-      for (int bj = 0; bj < 4; ++bj) t[bj] = f4v{0.f, 0.f, 0.f, 0.f};
-      tile_gemm(sm.cm, sB, w, i, q, t, 1.0f);                        // T = P_k X_{k,k+1}
+      f4v t[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+      pi_gemm(sm.cm, sB, rw, ch, i, q, t, 1.0f);                     // T = P_k X_{k,k+1}
       mfma_settle(t);
       __syncthreads();
-      acc_to_bt(sB, t, w, i, q);
+      acc_to_bt(sB, t, rw, ch, i, q);
       __syncthreads();
-      tile_gemm(sX, sB, w, i, q, acc, -1.0f);                        // X_{k+1,k+1} - X_{k+1,k} T
+      pi_gemm(sX, sB, rw, ch, i, q, acc, -1.0f);                     // X_{k+1,k+1} - X_{k+1,k} T
       mfma_settle(acc);
       __syncthreads();                                               // every wave is done with cm (A of T)
-      acc_to_a(sm.cm, acc, w, i, q);
+      acc_to_a(sm.cm, acc, rw, ch, i, q);
       __syncthreads();
       mark(8 * k + 3);
     }
@@ -487,10 +528,7 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
     float (*sA)[LDT] = lds[0];
     float (*sB)[LDT] = lds[1];
     float (*sX)[LDT] = lds[2];
-#pragma unroll
-    for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[bj][r] = in[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i];
+    load_in(ti * PB, tj * PB);
     for (int k = 0; k < NB; ++k) {
       if (ti == tj && k == ti - 1) continue;       // X_kk^(k-1) is the chain's; nobody reads this one
       const bool generic = ti != k && tj != k;
@@ -503,49 +541,47 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
       const __amdgpu_buffer_rsrc_t rp = pi_rsrc(Pt + (size_t)ptile(k) * 4, PI_TILE);
       if (ti == k && tj == k) {                                      // X_kk <- P_k
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) acc[bj] = pi_load(rp, (4 * w + bj) * 64 + lane);
+        for (int b = 0; b < 2; ++b) acc[b] = pi_load(rp, own_e(b));
       } else if (tj == k) {                                          // X_ik <- -X_ik P_k
-        acc_to_a(sA, acc, w, i, q);
+        acc_to_a(sA, acc, rw, ch, i, q);
         pi_to_bt(sB, rp);
         __syncthreads();
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
-        tile_gemm(sA, sB, w, i, q, acc, -1.0f);
+        for (int b = 0; b < 2; ++b) acc[b] = f4v{0.f, 0.f, 0.f, 0.f};
+        pi_gemm(sA, sB, rw, ch, i, q, acc, -1.0f);
         mfma_settle(acc);
       } else if (ti == k) {                                          // X_kj <- P_k X_kj
         pi_to_a(sA, rp);
-        acc_to_bt(sB, acc, w, i, q);
+        acc_to_bt(sB, acc, rw, ch, i, q);
         __syncthreads();
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) acc[bj] = f4v{0.f, 0.f, 0.f, 0.f};
-        tile_gemm(sA, sB, w, i, q, acc, 1.0f);
+        for (int b = 0; b < 2; ++b) acc[b] = f4v{0.f, 0.f, 0.f, 0.f};
+        pi_gemm(sA, sB, rw, ch, i, q, acc, 1.0f);
         mfma_settle(acc);
       } else {                                                       // X_ij - X_ik (P_k X_kj)
         pi_to_a(sA, rp);
         if (k == 0) {
-          tile_load(sB, in + tj * PB, n, true);                      // X_0j, column-major
-          tile_load(sX, in + (int64_t)ti * PB * n, n, false);        // X_i0
+          pi_tile_load(sB, in + tj * PB, n, true);                   // X_0j, column-major
+          pi_tile_load(sX, in + (int64_t)ti * PB * n, n, false);     // X_i0
         } else {
           pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, tj) * 4, PI_TILE));
           pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, ti, k) * 4, PI_TILE));
         }
         __syncthreads();
-        f4v r4[4];
-#pragma unroll
-        for (int bj = 0; bj < 4; ++bj) r4[bj] = f4v{0.f, 0.f, 0.f, 0.f};
-        tile_gemm(sA, sB, w, i, q, r4, 1.0f);                        // R_kj = P_k X_kj
+        f4v r4[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+        pi_gemm(sA, sB, rw, ch, i, q, r4, 1.0f);                     // R_kj = P_k X_kj
         mfma_settle(r4);
         __syncthreads();                                             // every wave is done reading sB
-        acc_to_bt(sB, r4, w, i, q);
+        acc_to_bt(sB, r4, rw, ch, i, q);
         __syncthreads();
-        tile_gemm(sX, sB, w, i, q, acc, -1.0f);
+        pi_gemm(sX, sB, rw, ch, i, q, acc, -1.0f);
         mfma_settle(acc);
       }
       // publish version k where step k + 1 or the chain reads it
       const bool rowcol = (ti == k + 1) != (tj == k + 1);
       if (k + 1 < NB && (rowcol || (ti == tj && ti == k + 2))) {
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) pi_store(rV, vtile(k, ti, tj) + (4 * w + bj) * 64 + lane, acc[bj]);
+        for (int b = 0; b < 2; ++b) pi_store(rV, vtile(k, ti, tj) + own_e(b), acc[b]);
         pi_signal(&tflag[(k * NB + ti) * NB + tj]);
       }
       mark(256 + t * NB + k);
@@ -553,10 +589,10 @@ __global__ void __launch_bounds__(256) k_pinv(const float* __restrict__ in, int6
     }
     const float poison = dead ? __builtin_nanf("") : 0.f;
 #pragma unroll
-    for (int bj = 0; bj < 4; ++bj)
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        out[(int64_t)(ti * PB + 16 * w + 4 * q + r) * n + tj * PB + 16 * bj + i] = acc[bj][r] + poison;
+        out[(int64_t)(ti * PB + 16 * rw + 4 * q + r) * n + tj * PB + 16 * (2 * ch + b) + i] = acc[b][r] + poison;
   }
 }
 
@@ -570,7 +606,8 @@ int launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, f
     const char* e = getenv("FIODE_PINV_ACQUIRE");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(256), 0, st, in, in_stride, out, ws, wstride, skip, acq, prof);
+  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(PI_NT), 0, st, in, in_stride, out, ws, wstride, skip, acq,
+                     prof);
   return FIODE_OK;
 }
 
