@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(PivotGJ::NT) k_panel_pivot(int np, int k0, con
 // out tile (ib, jb) of the next buffer: 256 threads, MFMA 16x16x4 (wave w: output rows 16w..16w+15,
 // all 4 column blocks), operands in LDS as row-major A / column-major B so every k-chunk of 4 is
 // one ds_read_b128 (k order permuted: step s of chunk kc uses k = 16 kc + 4q + s at lane q).
-constexpr int LDT = PB + 4;
+constexpr int LDT = PB + 8;     // = 8 mod 64: every ds_read_b128 lane group of the products hits 64 distinct banks
 typedef fiode_gjb::f4v f4v;
 
 // acc[bj] += A[16w + i][:] . B^T[16bj + j][:]  (A row-major, BT = B column-major, both [PB][LDT])

@@ -80,7 +80,7 @@ template <int NP, int NW>
 struct GJB {
   static constexpr int NB = NP / 16;          // blocks per side
   static constexpr int NT = 64 * NW;
-  static constexpr int LDM = NP + 4;          // cm row stride (floats; 16-byte aligned rows)
+  static constexpr int LDM = NP + 8;          // cm row stride (floats; = 8 mod 64: the b128 lane groups conflict-free)
   static constexpr int LDP = 20;              // panel buffers' row stride
   struct Smem {
     float cm[NP][LDM];                        // cm[col][row] of X
