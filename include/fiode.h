@@ -330,9 +330,8 @@ FIODE_API int fiode_block_inverse(void* stream, int32_t n, const float* in, floa
 FIODE_API int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t n, const float* in, float* out,
                                           void* workspace, size_t workspace_bytes);
 /* The same, skipped on the device when *skip != 0 (device int32; NULL = never): every launch of the
- * sequence returns at once and `out` keeps its contents -- for a caller that has already refined an
- * inverse from the previous step's (fiode_amd/cayley.py _warm_inverse) and falls back to the exact
- * elimination only when that did not converge, without a host sync. */
+ * sequence returns at once and `out` keeps its contents -- for a caller that decides on the device
+ * whether an inverse it already holds is still exact (no host sync). */
 FIODE_API int fiode_block_inverse_cond(void* stream, int32_t batch, int32_t n, const float* in, float* out,
                                        void* workspace, size_t workspace_bytes, const int32_t* skip);
 
