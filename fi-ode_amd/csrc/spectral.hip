@@ -24,6 +24,7 @@
 //                 g = dL/dRe + i dL/dIm, so a real w with z = c w gets Re(conj(c) g)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "common.h"
 #include "fiode.h"
@@ -810,9 +811,19 @@ extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_
     hipLaunchKernelGGL(k_spec_gram, dim3(a.nf, nt * nt), dim3(TL * TL), 0, st, a);
     if (a.K == 32)
       hipLaunchKernelGGL((k_spec_inv_re<64, 8>), dim3(a.nf), dim3(512), sizeof(fiode_gjb::GJB<64, 8>::Smem), st, a);
-    else if (a.K == 64)
-      hipLaunchKernelGGL((k_spec_inv_re<128, 16>), dim3(a.nf), dim3(1024), sizeof(fiode_gjb::GJB<128, 16>::Smem), st,
-                         a);
+    else if (a.K == 64) {
+      static const int nw = [] {
+        const char* e = getenv("FIODE_SPEC_NW");            // (probe knob: waves of the K = 64 inverse)
+        return e ? atoi(e) : 16;
+      }();
+      if (nw == 8)
+        hipLaunchKernelGGL((k_spec_inv_re<128, 8>), dim3(a.nf), dim3(512), sizeof(fiode_gjb::GJB<128, 8>::Smem), st, a);
+      else if (nw == 4)
+        hipLaunchKernelGGL((k_spec_inv_re<128, 4>), dim3(a.nf), dim3(256), sizeof(fiode_gjb::GJB<128, 4>::Smem), st, a);
+      else
+        hipLaunchKernelGGL((k_spec_inv_re<128, 16>), dim3(a.nf), dim3(1024), sizeof(fiode_gjb::GJB<128, 16>::Smem), st,
+                           a);
+    }
     else if (a.K <= 32) hipLaunchKernelGGL((k_spec_inv<32, 2, 2, 256>), dim3(a.nf), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
     if (a.R > a.K) hipLaunchKernelGGL(k_spec_qbot, dim3(a.nf, ((a.R - a.K) / TL) * nt), dim3(TL * TL), 0, st, a);
