@@ -76,6 +76,11 @@ __device__ __forceinline__ void gj16(float (&x)[4], int c, int q) {
   }
 }
 
+#ifndef GJB_PRIO_DEFAULT
+#define GJB_PRIO_DEFAULT 1
+#endif
+constexpr bool GJB_PRIO = GJB_PRIO_DEFAULT != 0;
+
 template <int NP, int NW>
 struct GJB {
   static constexpr int NB = NP / 16;          // blocks per side
@@ -93,10 +98,14 @@ struct GJB {
     return reinterpret_cast<f4v*>(&sm.cm[16 * bj + c][16 * bi + 4 * q]);
   }
 
+  // (the pivot block's elimination is the round's critical path: while it runs the wave takes the
+  // SIMD's issue slots ahead of the co-resident waves doing the rank-16 updates, s_setprio)
   static __device__ __forceinline__ void invert_block(Smem& sm, int b, int c, int q) {
     f4v v = *blk(sm, b, b, c, q);
     float x[4] = {v[0], v[1], v[2], v[3]};
+    if constexpr (GJB_PRIO) __builtin_amdgcn_s_setprio(3);
     gj16(x, c, q);
+    if constexpr (GJB_PRIO) __builtin_amdgcn_s_setprio(0);
     *blk(sm, b, b, c, q) = f4v{x[0], x[1], x[2], x[3]};
   }
 
