@@ -359,14 +359,58 @@ __device__ __forceinline__ void pi_to_a(float (*dst)[LDT], __amdgpu_buffer_rsrc_
     for (int k = 0; k < 4; ++k) dst[16 * w + 4 * (ln >> 4) + k][16 * bj + (ln & 15)] = v[k];
   }
 }
+// Where the matrix to invert comes from: a row-major n x n array (PlainSrc), or built on load from a
+// dense Cayley map's weight (DenseSrc: M = I + s (U' - U'^T) + s^2 G with s = alpha / ||W||, the
+// arithmetic of dense.hip k_dense_prep element for element -- the same M bit for bit, so the fused
+// map forward needs no prep launch and no M buffer).  bind(m): the batch entry; all threads call it.
+struct PlainSrc {
+  const float* in;
+  int64_t stride;
+  int n;
+  __device__ void bind(int m, float*) { in += (int64_t)m * stride; }
+  __device__ float at(int r, int c) const { return in[(int64_t)r * n + c]; }
+  __device__ f4v row4(int r, int c4) const { return *reinterpret_cast<const f4v*>(in + (int64_t)r * n + c4); }
+};
+struct DenseSrc {
+  const float* W;        // [b][cout][cin]
+  const float* G;        // [b][k][k] or null (square maps)
+  const float* alpha;    // [b]
+  const float* part;     // [b][256] squared-norm partials (fiode_dense_norm_partials*)
+  float* nrm_out;        // [b]
+  int cout, cin, k, wide;
+  float s;
+  __device__ void bind(int m, float* slot) {
+    W += (int64_t)m * cout * cin;
+    if (G) G += (int64_t)m * k * k;
+    if (threadIdx.x < 64) {               // dense.hip dense_norm: the same fixed order
+      const float* pb = part + m * 256 + 4 * threadIdx.x;
+      float v = (pb[0] + pb[1]) + (pb[2] + pb[3]);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (threadIdx.x == 0) {
+        *slot = sqrtf(v);
+        if (nrm_out && blockIdx.x == 0) nrm_out[m] = *slot;
+      }
+    }
+    __syncthreads();
+    s = alpha[m] / *slot;
+  }
+  __device__ float wx(int r, int c) const { return wide ? W[(int64_t)c * cin + r] : W[(int64_t)r * cin + c]; }
+  __device__ float at(int r, int c) const {
+    float v = s * (wx(r, c) - wx(c, r));
+    if (G) v = fmaf(s * s, G[(int64_t)r * k + c], v);
+    if (r == c) v += 1.0f;
+    return v;
+  }
+  __device__ f4v row4(int r, int c4) const { return f4v{at(r, c4), at(r, c4 + 1), at(r, c4 + 2), at(r, c4 + 3)}; }
+};
 // a 64 x 64 block of a row-major matrix (row stride ld) -> LDS, row-major or transposed
-__device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const float* __restrict__ src, int64_t ld,
-                                             bool transpose) {
+template <class Src>
+__device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const Src& src, int r0, int c0, bool transpose) {
 #pragma unroll
   for (int u = 0; u < PB * PB / 4 / PI_NT; ++u) {
     const int t = threadIdx.x + PI_NT * u;
     const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
-    const f4v v = *reinterpret_cast<const f4v*>(src + (int64_t)r * ld + c4);
+    const f4v v = src.row4(r0 + r, c0 + c4);
     if (transpose) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) dst[c4 + e][r] = v[e];
@@ -410,17 +454,19 @@ __device__ __forceinline__ void mfma_settle(f4v (&acc)[2]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(acc[0]), "+a"(acc[1]));
 }
 
-template <int NB>
-__global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, int64_t in_stride, float* __restrict__ out,
+template <int NB, class Src>
+__global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out, float* __restrict__ qout,
                                                 float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
                                                 int acq, unsigned long long* prof) {
   if (skip && *skip) return;                  // (uniform)
   constexpr int n = NB * PB;
   __shared__ __attribute__((aligned(16))) float lds[4][PB][LDT + 0];
   __shared__ int dead;
+  __shared__ float slot;
   const int m = blockIdx.y;
-  in += (int64_t)m * in_stride;
+  src.bind(m, &slot);
   out += (int64_t)m * n * n;
+  if (qout) qout += (int64_t)m * n * n;
   float* ws = ws_all + (int64_t)m * wstride;
   unsigned* tflag = reinterpret_cast<unsigned*>(ws);                 // [NB][NB][NB]
   unsigned* pflag = tflag + NB * NB * NB;                            // [NB]
@@ -446,7 +492,7 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, in
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[b][r] = in[(int64_t)(r0 + 16 * rw + 4 * q + r) * n + c0 + 16 * (2 * ch + b) + i];
+      for (int r = 0; r < 4; ++r) acc[b][r] = src.at(r0 + 16 * rw + 4 * q + r, c0 + 16 * (2 * ch + b) + i);
   };
 
   if (blockIdx.x == 0) {
@@ -457,7 +503,10 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, in
     float (*sX)[LDT] = lds[2];
     float (*sB)[LDT] = lds[3];
     static_assert(CG::LDM == LDT, "the pivot image doubles as the product's A operand");
-    CG::load(sm, in, PB, n);
+    for (int t = threadIdx.x; t < PB * PB / 4; t += PI_NT) {         // X_00 (gjb.h load's layout)
+      const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
+      *reinterpret_cast<f4v*>(&sm.cm[r][c4]) = src.row4(r, c4);
+    }
     __syncthreads();
     // the next pivot's three operand tiles (version k - 1 for step k + 1), fetched into registers
     // while the current pivot block is inverted: polled and loaded from the inversion's hook
@@ -495,8 +544,8 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, in
       if (k1 == NB) break;
       // X_{k+1,k+1}^(k) = X_{k+1,k+1}^(k-1) - X_{k+1,k}^(k-1) (P_k X_{k,k+1}^(k-1))
       if (k == 0) {                                                  // version -1 = the input
-        pi_tile_load(sB, in + k1 * PB, n, true);                     // X_01 (column-major)
-        pi_tile_load(sX, in + (int64_t)k1 * PB * n, n, false);       // X_10
+        pi_tile_load(sB, src, 0, k1 * PB, true);                     // X_01 (column-major)
+        pi_tile_load(sX, src, k1 * PB, 0, false);                    // X_10
         load_in(k1 * PB, k1 * PB);
       } else {
 #pragma unroll
@@ -561,8 +610,8 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, in
       } else {                                                       // X_ij - X_ik (P_k X_kj)
         pi_to_a(sA, rp);
         if (k == 0) {
-          pi_tile_load(sB, in + tj * PB, n, true);                   // X_0j, column-major
-          pi_tile_load(sX, in + (int64_t)ti * PB * n, n, false);     // X_i0
+          pi_tile_load(sB, src, 0, tj * PB, true);                   // X_0j, column-major
+          pi_tile_load(sX, src, ti * PB, 0, false);                  // X_i0
         } else {
           pi_to_bt(sB, pi_rsrc(V + (size_t)vtile(k - 1, k, tj) * 4, PI_TILE));
           pi_to_a(sX, pi_rsrc(V + (size_t)vtile(k - 1, ti, k) * 4, PI_TILE));
@@ -591,24 +640,43 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(const float* __restrict__ in, in
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out[(int64_t)(ti * PB + 16 * rw + 4 * q + r) * n + tj * PB + 16 * (2 * ch + b) + i] = acc[b][r] + poison;
+      for (int r = 0; r < 4; ++r) {
+        const int gi = ti * PB + 16 * rw + 4 * q + r, gj = tj * PB + 16 * (2 * ch + b) + i;
+        const float v = acc[b][r] + poison;
+        out[(int64_t)gi * n + gj] = v;
+        if (qout) {                           // a square dense map's Q = 2 inv - I (k_dense_finish's arithmetic)
+          float qv = 2.0f * v;
+          if (gi == gj) qv -= 1.0f;
+          qout[(int64_t)gi * n + gj] = qv;
+        }
+      }
   }
+}
+
+int pinv_acquire_knob() {
+  static const int acq = [] {
+    const char* e = getenv("FIODE_PINV_ACQUIRE");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return acq;
+}
+
+template <int NB, class Src>
+int launch_pinv_src(hipStream_t st, int batch, Src src, float* out, float* qout, float* ws, int64_t wstride,
+                    const int32_t* skip, bool clear_flags, unsigned long long* prof = nullptr) {
+  // the flag block of every system: its first flag_floats(NB) floats (a multiple of 16 bytes)
+  if (clear_flags)
+    FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
+                                     (size_t)batch, st));
+  hipLaunchKernelGGL((k_pinv<NB, Src>), dim3(1 + NB * NB, batch), dim3(PI_NT), 0, st, src, out, qout, ws, wstride, skip,
+                     pinv_acquire_knob(), prof);
+  return FIODE_OK;
 }
 
 template <int NB>
 int launch_pinv(hipStream_t st, int batch, const float* in, int64_t in_stride, float* out, float* ws, int64_t wstride,
                 const int32_t* skip, unsigned long long* prof = nullptr) {
-  // the flag block of every system: its first flag_floats(NB) floats (a multiple of 16 bytes)
-  FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
-                                   (size_t)batch, st));
-  static const int acq = [] {
-    const char* e = getenv("FIODE_PINV_ACQUIRE");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  hipLaunchKernelGGL(k_pinv<NB>, dim3(1 + NB * NB, batch), dim3(PI_NT), 0, st, in, in_stride, out, ws, wstride, skip, acq,
-                     prof);
-  return FIODE_OK;
+  return launch_pinv_src<NB>(st, batch, PlainSrc{in, in_stride, NB * PB}, out, nullptr, ws, wstride, skip, true, prof);
 }
 
 }  // namespace
@@ -716,4 +784,47 @@ extern "C" FIODE_API int fiode_debug_pinv_profile(void* stream, int32_t n, const
   if (n != 512 || !in || !out || !workspace || !prof || in == out) return FIODE_EINVAL;
   const int64_t wstride = (int64_t)(fiode_block_inverse_workspace_bytes(n) / sizeof(float));
   return launch_pinv<8>((hipStream_t)stream, 1, in, (int64_t)n * n, out, (float*)workspace, wstride, nullptr, prof);
+}
+
+// ---- the dense Cayley map's inverse, its M built on load ----------------------------------------
+// fiode_dense_cayley_inverse: for each [cout][cin] matrix b of the batch (k = min(cout, cin) = 128 ..
+// 512 in steps of 64): s = alpha[b] / ||W_b|| from the 256 norm partials (fiode_dense_norm_partials*),
+// M = I + s (U' - U'^T) + s^2 G (G = V'^T V' for tall / wide maps, null for square ones) -- built by
+// the inverse's own loads, so no prep launch and no M buffer -- and inv = M^-1 -> inv_out [b][k][k],
+// ||W_b|| -> nrm_out [b]; for a square map also Q = 2 inv - I -> q_out (the whole map: no finish
+// launch; tall / wide maps keep fiode_dense_cayley_finish for Q).  The workspace's flag words (the
+// first fiode_dense_inverse_flag_bytes(k) bytes of each matrix's fiode_block_inverse_workspace_bytes(k)
+// stride) must be zero: fiode_dense_norm_partials_clear zeroes them in the same launch as the partials.
+extern "C" FIODE_API size_t fiode_dense_inverse_flag_bytes(int32_t k) {
+  return pinv_shape(k) ? PinvWs::flag_floats(k / PB) * sizeof(float) : 0;
+}
+
+extern "C" FIODE_API int fiode_dense_cayley_inverse(void* stream, const fiode_dense_config* cfg, const float* W,
+                                                    const float* alpha, const float* part, const float* G,
+                                                    float* nrm_out, float* inv_out, float* q_out, void* workspace,
+                                                    size_t workspace_bytes) {
+  if (!cfg || cfg->batch < 1 || cfg->batch > 65535 || cfg->cout < 1 || cfg->cin < 1) return FIODE_EINVAL;
+  const int k = cfg->cout < cfg->cin ? cfg->cout : cfg->cin, R = cfg->cout < cfg->cin ? cfg->cin : cfg->cout;
+  if (!pinv_shape(k)) return FIODE_ESHAPE;
+  if (!W || !alpha || !part || !nrm_out || !inv_out || !workspace || (R > k && !G) || (q_out && R > k))
+    return FIODE_EINVAL;
+  const size_t per = fiode_block_inverse_workspace_bytes(k);
+  if (workspace_bytes < (size_t)cfg->batch * per) return FIODE_EWORKSPACE;
+  DenseSrc src{W, R > k ? G : nullptr, alpha, part, nrm_out, cfg->cout, cfg->cin, k, cfg->cin > cfg->cout ? 1 : 0, 0.f};
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  const int64_t wstride = (int64_t)(per / sizeof(float));
+  int rc = FIODE_OK;
+  switch (k / PB) {
+    case 2: rc = launch_pinv_src<2>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    case 3: rc = launch_pinv_src<3>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    case 4: rc = launch_pinv_src<4>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    case 5: rc = launch_pinv_src<5>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    case 6: rc = launch_pinv_src<6>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    case 7: rc = launch_pinv_src<7>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+    default: rc = launch_pinv_src<8>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
+  }
+  if (rc) return rc;
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

@@ -49,9 +49,14 @@ __device__ __forceinline__ int64_t wpos(const DArgs& a, int r, int c) {   // X (
 // read over NPART x batch workgroups in place of torch's vector_norm reduction (~10 us on the dense
 // maps' forward chain).
 constexpr int NPART = 256;      // 8 float4 per thread of the 4096 x 512 map: two load round trips
-__global__ void __launch_bounds__(NT) k_dense_sumsq(DArgs a, float* __restrict__ part) {
+__global__ void __launch_bounds__(NT) k_dense_sumsq(DArgs a, float* __restrict__ part, unsigned* __restrict__ clear,
+                                                    int clear_words, int64_t clear_stride) {
   __shared__ float red[NT / 64];
   const int b = blockIdx.y;
+  // (optional) zero the next kernel's hand-off flags: the one-launch inverse of this map
+  // (fiode_dense_cayley_inverse) runs two launches later on the same stream
+  if (clear && blockIdx.x == 0)
+    for (int t = threadIdx.x; t < clear_words; t += NT) clear[(int64_t)b * clear_stride + t] = 0u;
   const int64_t n = (int64_t)a.cout * a.cin;
   const float* Wb = a.W + (int64_t)b * n;
   float acc = 0.f;
@@ -412,7 +417,24 @@ extern "C" int fiode_dense_norm_partials(void* stream, const fiode_dense_config*
   if (!W || !workspace) return FIODE_EINVAL;
   if (workspace_bytes < fiode_dense_norm_workspace_bytes(cfg)) return FIODE_EWORKSPACE;
   a.W = W;
-  hipLaunchKernelGGL(k_dense_sumsq, dim3(NPART, batch), dim3(NT), 0, (hipStream_t)stream, a, (float*)workspace);
+  hipLaunchKernelGGL(k_dense_sumsq, dim3(NPART, batch), dim3(NT), 0, (hipStream_t)stream, a, (float*)workspace,
+                     (unsigned*)nullptr, 0, (int64_t)0);
+  DENSE_RET();
+}
+
+extern "C" int fiode_dense_norm_partials_clear(void* stream, const fiode_dense_config* cfg, const float* W,
+                                               void* workspace, size_t workspace_bytes, void* clear,
+                                               size_t clear_words, size_t clear_stride_bytes) {
+  DArgs a;
+  int batch, rc = mk(cfg, a, batch);
+  if (rc) return rc;
+  if (!W || !workspace || (clear_words && !clear) || clear_words > (1u << 20) || clear_stride_bytes % 4)
+    return FIODE_EINVAL;
+  if (workspace_bytes < fiode_dense_norm_workspace_bytes(cfg)) return FIODE_EWORKSPACE;
+  a.W = W;
+  hipLaunchKernelGGL(k_dense_sumsq, dim3(NPART, batch), dim3(NT), 0, (hipStream_t)stream, a, (float*)workspace,
+                     clear_words ? (unsigned*)clear : (unsigned*)nullptr, (int)clear_words,
+                     (int64_t)(clear_stride_bytes / 4));
   DENSE_RET();
 }
 

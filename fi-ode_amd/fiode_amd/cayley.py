@@ -242,16 +242,61 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     return gW.reshape(wshape), ga.reshape(ashape)
 
 
+def _dense_fused_ok(W: torch.Tensor) -> bool:
+    from . import _lib as L
+    k = min(W.shape[-2], W.shape[-1])
+    return DENSE_FUSED_INVERSE and W.is_cuda and L.lib().fiode_dense_inverse_flag_bytes(k) > 0
+
+
+def _dense_forward_fused(W: torch.Tensor, alpha: torch.Tensor):
+    """The map forward with the one-launch inverse building M on load (fiode_dense_cayley_inverse):
+    norm partials (+ the inverse's flag words zeroed in the same launch), [G GEMM], the inverse (+ Q
+    for a square map), [P GEMM + k_dense_finish].  The same M, inverse and Q as _dense_prep ->
+    _block_inverse -> _dense_finish, bit for bit (dense.hip k_dense_prep's arithmetic on load)."""
+    from . import ops, _lib as L
+    Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
+    al = alpha.detach().reshape(-1).contiguous().float()
+    b, cout, cin = Wb.shape
+    wide = cin > cout
+    k = cout if wide else cin
+    cfg = L.DenseConfig(b, cout, cin)
+    lib, stream = L.lib(), ops._stream(W.device)
+    per = lib.fiode_block_inverse_workspace_bytes(k)
+    ws = ops._Workspace.get(W.device, b * per, f"denseinv{torch.cuda.current_stream(W.device).cuda_stream}")
+    part = torch.empty(lib.fiode_dense_norm_workspace_bytes(ct.byref(cfg)) // 4, dtype=torch.float32, device=W.device)
+    L.check(lib.fiode_dense_norm_partials_clear(stream, ct.byref(cfg), Wb.data_ptr(), part.data_ptr(), part.numel() * 4,
+                                                ws.data_ptr(), lib.fiode_dense_inverse_flag_bytes(k) // 4, per),
+            "fiode_dense_norm_partials_clear")
+    Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
+    G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
+    nrm = torch.empty(b, dtype=torch.float32, device=W.device)
+    inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
+    Q = torch.empty_like(Wb) if Vp is None else None
+    L.check(lib.fiode_dense_cayley_inverse(stream, ct.byref(cfg), Wb.data_ptr(), al.data_ptr(), part.data_ptr(),
+                                           ops._ptr(G), nrm.data_ptr(), inv.data_ptr(), ops._ptr(Q), ws.data_ptr(),
+                                           ws.numel()), "fiode_dense_cayley_inverse")
+    st = dict(Wb=Wb, al=al, nrm=nrm, wide=wide, k=k, Vp=Vp, cfg=cfg)
+    if Q is None:
+        Q = _dense_finish(st, inv)
+    return st, inv, Q
+
+
 class _DenseCayleyFn(torch.autograd.Function):
     """cayley(alpha W / ||W||) for a batch of real [cout, cin] matrices (per-matrix norm and alpha):
     the same forward / analytic backward as _CayleyScaledFn, with the GEMMs as library GEMMs and
-    every elementwise stage between them one HIP kernel (fiode_dense_cayley_*; dense.hip)."""
+    every elementwise stage between them one HIP kernel (fiode_dense_cayley_*; dense.hip).  For
+    k = min(cout, cin) = 128 .. 512 (the backbone's 512 maps, the dynamics' 128 x 128) the inverse is
+    one launch that builds M on load (_dense_forward_fused): 2 launches for a square map's forward,
+    5 for a wide one (norm partials, G GEMM, inverse, P GEMM, finish)."""
 
     @staticmethod
     def forward(ctx, W, alpha):
-        st, M = _dense_prep(W, alpha)
-        inv = _block_inverse(M)
-        Q = _dense_finish(st, inv)
+        if _dense_fused_ok(W):
+            st, inv, Q = _dense_forward_fused(W, alpha)
+        else:
+            st, M = _dense_prep(W, alpha)
+            inv = _block_inverse(M)
+            Q = _dense_finish(st, inv)
         ctx.save_for_backward(st["Wb"], st["al"], st["nrm"], inv)
         ctx.shapes = (W.shape, alpha.shape)
         ctx.step_stream = STEP_STREAM
@@ -327,6 +372,7 @@ def cayley_scaled(W: torch.Tensor, alpha: torch.Tensor, per_matrix: bool = False
 
 DENSE_FUSED = True
 SMALL_FUSED = True
+DENSE_FUSED_INVERSE = True   # the one-launch inverse builds M itself (tests compare it with the staged path)
 
 
 def cayley(W: torch.Tensor) -> torch.Tensor:

@@ -367,6 +367,21 @@ FIODE_API int fiode_dense_norm_partials(void* stream, const fiode_dense_config* 
 FIODE_API int fiode_dense_cayley_prep_normed(void* stream, const fiode_dense_config* cfg, const float* W,
                                              const float* alpha, const void* workspace, float* nrm_out,
                                              const float* G, float* M);
+/* The norm partials, zeroing `clear_words` 32-bit words at clear + b * clear_stride_bytes for every
+ * matrix b in the same launch (the flag words of fiode_dense_cayley_inverse's workspace). */
+FIODE_API int fiode_dense_norm_partials_clear(void* stream, const fiode_dense_config* cfg, const float* W,
+                                              void* workspace, size_t workspace_bytes, void* clear,
+                                              size_t clear_words, size_t clear_stride_bytes);
+/* The dense map's inverse in ONE launch with M built on load (no prep launch, no M buffer):
+ * k = min(cout, cin) = 128 .. 512 in steps of 64; s = alpha / ||W|| from the norm partials,
+ * M = I + s (U' - U'^T) + s^2 G (G = V'^T V' when cout != cin, else NULL), inv_out [b][k][k] = M^-1,
+ * nrm_out [b] = ||W||; q_out (square maps only, else NULL): Q = 2 inv - I.  Workspace: batch x
+ * fiode_block_inverse_workspace_bytes(k), whose first fiode_dense_inverse_flag_bytes(k) bytes per
+ * matrix must be zero (fiode_dense_norm_partials_clear). */
+FIODE_API size_t fiode_dense_inverse_flag_bytes(int32_t k);
+FIODE_API int fiode_dense_cayley_inverse(void* stream, const fiode_dense_config* cfg, const float* W,
+                                         const float* alpha, const float* part, const float* G, float* nrm_out,
+                                         float* inv_out, float* q_out, void* workspace, size_t workspace_bytes);
 FIODE_API int fiode_dense_cayley_finish(void* stream, const fiode_dense_config* cfg, const float* alpha,
                                         const float* nrm, const float* inv, const float* P, float* Q);
 FIODE_API int fiode_dense_cayley_ginv(void* stream, const fiode_dense_config* cfg, const float* alpha,

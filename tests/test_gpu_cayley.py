@@ -480,3 +480,34 @@ def test_dense_gemm_matches_float64(n, batch):
     assert L.lib().fiode_dense_gemm(ops._stream(dev), 1, 96, 0, 0, A.data_ptr(), B.data_ptr(), A.data_ptr()) == \
         2      # FIODE_ESHAPE (include/fiode.h)
 
+
+
+@pytest.mark.parametrize("shape", [(512, 512), (512, 4096), (128, 128), (1024, 256), (2, 256, 256)])
+def test_dense_fused_inverse_equals_staged(shape):
+    """The dense map forward with the one-launch inverse building M on load (fiode_dense_cayley_
+    inverse: no prep launch, Q of a square map written by the inverse) = the staged path (prep
+    kernel -> M -> fiode_block_inverse -> finish), bit for bit: Q, and dL/dW, dL/dalpha."""
+    from fiode_amd import cayley as CY
+    dev = _dev()
+    g = torch.Generator().manual_seed(sum(shape))
+    W = (torch.randn(*shape, generator=g) / shape[-1] ** 0.5).to(dev)
+    alpha = (W.reshape(-1, shape[-2], shape[-1]).norm(dim=(-2, -1)) * 1.5).reshape(-1 if len(shape) == 3 else 1)
+    gQ = torch.randn(*shape, generator=g).to(dev)
+    out = {}
+    for fused in (True, False):
+        CY.DENSE_FUSED_INVERSE = fused
+        try:
+            Wl, al = W.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+            assert CY._dense_fused_ok(Wl) == fused
+            Q = CY._DenseCayleyFn.apply(Wl, al)
+            (Q * gQ).sum().backward()
+            torch.cuda.synchronize()
+            out[fused] = (Q.detach().clone(), Wl.grad.clone(), al.grad.clone())
+        finally:
+            CY.DENSE_FUSED_INVERSE = True
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+    Qt = out[True][0].reshape(-1, shape[-2], shape[-1])
+    Qt = Qt if shape[-2] >= shape[-1] else Qt.mT
+    eye = torch.eye(Qt.shape[-1], device=dev)
+    assert float((Qt.mT @ Qt - eye).abs().max()) < 5e-5
