@@ -199,6 +199,8 @@ def _load():
         "fiode_abi_version": (ct.c_int, []),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name) and "FIODE_LIB" in os.environ:
+            continue        # an older build under an A/B (tools/gpu_lib_ab.sh): callers check hasattr
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -245,7 +245,9 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
 def _dense_fused_ok(W: torch.Tensor) -> bool:
     from . import _lib as L
     k = min(W.shape[-2], W.shape[-1])
-    return DENSE_FUSED_INVERSE and W.is_cuda and L.lib().fiode_dense_inverse_flag_bytes(k) > 0
+    lib = L.lib()
+    return (DENSE_FUSED_INVERSE and W.is_cuda and hasattr(lib, "fiode_dense_cayley_inverse")
+            and lib.fiode_dense_inverse_flag_bytes(k) > 0)
 
 
 def _dense_forward_fused(W: torch.Tensor, alpha: torch.Tensor):
