@@ -77,7 +77,7 @@ __device__ __forceinline__ void gj16(float (&x)[4], int c, int q) {
 }
 
 #ifndef GJB_PRIO_DEFAULT
-#define GJB_PRIO_DEFAULT 1
+#define GJB_PRIO_DEFAULT 0
 #endif
 constexpr bool GJB_PRIO = GJB_PRIO_DEFAULT != 0;
 
@@ -98,8 +98,8 @@ struct GJB {
     return reinterpret_cast<f4v*>(&sm.cm[16 * bj + c][16 * bi + 4 * q]);
   }
 
-  // (the pivot block's elimination is the round's critical path: while it runs the wave takes the
-  // SIMD's issue slots ahead of the co-resident waves doing the rank-16 updates, s_setprio)
+  // (GJB_PRIO=1 raises the pivot wave's issue priority during the elimination: measured no gain on
+  // the spectral inverses and +2-3 us on the 512 block inverse, so off)
   static __device__ __forceinline__ void invert_block(Smem& sm, int b, int c, int q) {
     f4v v = *blk(sm, b, b, c, q);
     float x[4] = {v[0], v[1], v[2], v[3]};

@@ -812,17 +812,21 @@ extern "C" int fiode_spectral_cayley_forward(void* stream, const fiode_spectral_
     if (a.K == 32)
       hipLaunchKernelGGL((k_spec_inv_re<64, 8>), dim3(a.nf), dim3(512), sizeof(fiode_gjb::GJB<64, 8>::Smem), st, a);
     else if (a.K == 64) {
+      // the real embedding measured no faster at K = 64 (54 vs 51 us: its 8 serial 16-wide rounds
+      // bound it), so the complex kernel stays the default; the knob selects the embedding's waves
       static const int nw = [] {
-        const char* e = getenv("FIODE_SPEC_NW");            // (probe knob: waves of the K = 64 inverse)
-        return e ? atoi(e) : 16;
+        const char* e = getenv("FIODE_SPEC_NW");            // (probe knob: 4 / 8 / 16 waves)
+        return e ? atoi(e) : 0;
       }();
       if (nw == 8)
         hipLaunchKernelGGL((k_spec_inv_re<128, 8>), dim3(a.nf), dim3(512), sizeof(fiode_gjb::GJB<128, 8>::Smem), st, a);
       else if (nw == 4)
         hipLaunchKernelGGL((k_spec_inv_re<128, 4>), dim3(a.nf), dim3(256), sizeof(fiode_gjb::GJB<128, 4>::Smem), st, a);
-      else
+      else if (nw == 16)
         hipLaunchKernelGGL((k_spec_inv_re<128, 16>), dim3(a.nf), dim3(1024), sizeof(fiode_gjb::GJB<128, 16>::Smem), st,
                            a);
+      else
+        hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
     }
     else if (a.K <= 32) hipLaunchKernelGGL((k_spec_inv<32, 2, 2, 256>), dim3(a.nf), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_spec_inv<64, 2, 4, 512>), dim3(a.nf), dim3(512), 0, st, a);
