@@ -129,7 +129,8 @@ __device__ __forceinline__ Rng rng_of(const OTArgs& a) {
 #endif
 struct OtShared {
   float zpart[4][64][4];      // [part][lane][layer-3 accumulator registers]
-  float mu_rec[4][64][33];    // [wave][lane][bisection iteration] (padded): every lane its own
+  float mu_rec[4][48][33];    // [wave][row j < 16][bisection iteration] (the row's lanes of the wave share it);
+                              // [wave][32 + j][0..1]: the tree bisection's bracket hand-over
   float z1x[8][64][4];        // layer-1 blocks, one pair per wave (mlp16_part)
   int K;
   int Kprev;                  // previous eval's exit iteration (speculation for the next)
@@ -189,8 +190,8 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
     }
   }
   OT_MARK(5);
-  float* rec = &sh.mu_rec[p][lane][0];
-  qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec,
+  float* rec = &sh.mu_rec[p][j][0];
+  qp16_exit<TR>(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, q, lane, rec, &sh.mu_rec[p][32 + j][0],
             a.xslots + (size_t)(e % OT_XRING) * 2 * gridDim.x, (unsigned)e + 1u, a.stats + 3, sh.K, sh.dead,
             a.drop_block,
 #ifdef OT_PROFILE
@@ -201,7 +202,7 @@ __device__ void ot_eval(const OTArgs& a, const T16W& w, OtShared& sh, int e, int
   );
   OT_MARK(3);
   const int K = sh.K;
-  const float mu = sh.mu_rec[p][lane][K];
+  const float mu = rec[K];
 #pragma unroll
   for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);
   if (p == 0 && valid && q == 0) {
@@ -340,7 +341,8 @@ constexpr int FIODE_OT4_MAX_TILES = 256;     // one persistent workgroup per CU 
 constexpr int OT4_XSTRIDE = 16;              // u64 words per exit granule: one 128-byte line per tile
 struct OtShared4 {
   Mlp4Shared mlp;
-  float mu_rec[4][64][33];    // [wave][lane][bisection iteration] (padded): every lane its own
+  float mu_rec[4][48][33];    // [wave][row j < 16][bisection iteration] (the row's lanes of the wave share it);
+                              // [wave][32 + j][0..1]: the tree bisection's bracket hand-over
   int K;
   int Kprev;
   int dead;
@@ -348,7 +350,7 @@ struct OtShared4 {
 };
 
 // end_barrier: the trailing workgroup barrier, which k_ot_fwd4 leaves out -- every LDS word this
-// eval reads is either the lane's own (mu_rec) or is next written only behind a barrier of the next
+// eval reads is either written by its own wave (mu_rec) or is next written only behind a barrier of the next
 // eval that every wave reaches after its last read here: a1s / zpart behind the next layer-1
 // barrier, K / Kprev by lane 0 of wave 0 behind it too, a2s by the owning wave only.  The dopri5
 // solve keeps it (its caller shares the workgroup's LDS between evals).
@@ -384,8 +386,9 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
     }
   }
   OT_MARK(5);
-  float* rec = &sh.mu_rec[p][lane][0];
-  const int K = qp16_exit(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
+  float* rec = &sh.mu_rec[p][j][0];
+  const int K = qp16_exit<TR4>(lower, nominal, a.d.tol, a.d.max_iter, sh.Kprev, valid, p, 0, lane, rec,
+            &sh.mu_rec[p][32 + j][0],
             a.xslots + (size_t)(e % OT_XRING) * 2 * gridDim.x * OT4_XSTRIDE, (unsigned)e + 1u, a.stats + 3, sh.K,
             sh.dead,
             a.drop_block,
@@ -396,7 +399,7 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
 #endif
             OT4_XSTRIDE, gridDim.x <= 64);
   OT_MARK(3);
-  const float mu = sh.mu_rec[p][lane][K];
+  const float mu = rec[K];
 #pragma unroll
   for (int i = 0; i < C; ++i) k[i] = fmaxf(nominal[i] - mu, lower[i]);
   if (writer) {
@@ -1013,6 +1016,9 @@ template <int NV>
 __device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& ep, const double (&mine)[NV],
                              double (&out)[NV]) {
   const int lane = threadIdx.x & 63;
+#ifdef OT_PROFILE
+  const uint64_t tp0 = wall_clock64();
+#endif
   if (threadIdx.x < 64) {
     double w[NV];
 #pragma unroll
@@ -1085,6 +1091,9 @@ __device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& 
 #pragma unroll
   for (int v = 0; v < NV; ++v) out[v] = red[v];
   __syncthreads();
+#ifdef OT_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.prof + 9, (unsigned long long)(wall_clock64() - tp0));
+#endif
 }
 
 template <bool T4>
@@ -1244,6 +1253,9 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
   for (int c = 0; c < C; ++c) yprev[c] = y[c];
   float dt32L = 0.f;
   while (tmax > tnext) {
+#ifdef OT_PROFILE
+    const uint64_t ta0 = wall_clock64();
+#endif
     if (n >= a.A || !(tcur + dt > tcur)) {
       status = n >= a.A ? 2 : 3;           // attempt capacity exhausted / dt underflow
       break;
@@ -1325,6 +1337,9 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       dt = dt * fmin(DP_IFACTOR, fmax(DP_SAFETY / pow((double)ratio, 1.0 / 5.0), df));
     }
     ++n;
+#ifdef OT_PROFILE
+    if (lead) atomicAdd(a.prof + 2, (unsigned long long)(wall_clock64() - ta0));
+#endif
   }
   // ---- dense output at t1 (torchdiffeq _interp_evaluate of the last accepted step) -----------
   float out[C];

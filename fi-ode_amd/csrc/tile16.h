@@ -168,10 +168,9 @@ __device__ __forceinline__ float qp_eps(const float (&lower)[C], const float (&n
 // above 2^-125), the per-lane open bits are OR-reduced over the wave once per call (a ballot per
 // iteration measured slower: its scalar test waits on the compare), and mu_rec (nullable) is
 // written by every lane (rec: the caller's per-lane slot) with no exec-mask branch.
-__device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const float (&nom)[C], int from, int to,
-                                                  float tol, float& lo, float& hi, float* mu_rec, bool rec,
-                                                  bool valid) {
-  if (from > to) return 0u;
+__device__ __forceinline__ uint32_t qp_open_seq(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                float tol, float& lo, float& hi, float* mu_rec, bool rec,
+                                                bool valid) {
   uint32_t open = 0;
   for (int it = from; it <= to; ++it) {
     const float mu = __fmaf_rn(hi - lo, 0.5f, lo);
@@ -181,11 +180,93 @@ __device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const
     lo = eps > 0.f ? mu : lo;
     hi = eps < 0.f ? mu : hi;
   }
+  return open;
+}
+__device__ __forceinline__ uint32_t qp_span(int from, int to) {
   const int n = to - from + 1;
-  const uint32_t span = (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << from;
-  return ~wave_or16(open) & span;
+  return (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << from;
+}
+__device__ __forceinline__ uint32_t qp_bisect_seq(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                  float tol, float& lo, float& hi, float* mu_rec, bool rec,
+                                                  bool valid) {
+  if (from > to) return 0u;
+  const uint32_t open = qp_open_seq(lower, nom, from, to, tol, lo, hi, mu_rec, rec, valid);
+  return ~wave_or16(open) & qp_span(from, to);
 }
 
+// The same iterations, LV at a time, on the lanes that replicate a row.  A wave holding R rows has
+// 64 / R copies of each (lane = m R + j: row j, copy m); copy m < 2^LV - 1 evaluates node m of the
+// depth-LV tree of bisection states the next LV iterations can reach (node n's children 2n + 1 /
+// 2n + 2 follow eps > 0 (lo = mu) / eps < 0 (hi = mu)), so one eps per lane replaces LV dependent
+// ones.  Every node's mu is computed from the round's (lo, hi) by the sequential recurrence along
+// its path, so the mus, the convergence bits and the final bracket are bit-identical to
+// qp_bisect_seq's.  One ballot of the signs gives each node its place on the path (all ancestors'
+// signs lead to it); the path nodes record their mu (rec: the row's shared record) and open bit, and
+// the last one publishes the next bracket through LDS (bc, same wave: LDS order suffices).  A round
+// in which any node's eps is 0 or NaN (the bracket would not move there) runs sequentially.
+template <int R>
+struct QpTree {
+  static constexpr int REP = 64 / R;
+  static constexpr int LV = REP >= 16 ? 4 : (REP >= 4 ? 2 : 1);
+  static constexpr int NN = (1 << LV) - 1;
+};
+
+template <int R>
+__device__ __forceinline__ uint32_t qp_bisect_tree(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                   float tol, float& lo, float& hi, float* rec, float* bc,
+                                                   bool valid) {
+  if (from > to) return 0u;
+  constexpr int LV = QpTree<R>::LV;
+  uint32_t open = 0;
+  int it = from;
+  if constexpr (LV > 1) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane % R, m = lane / R;
+    const bool owner = m < QpTree<R>::NN;
+    const int n1 = (owner ? m : 0) + 1;       // heap index + 1 = binary 1 d_0 .. d_{L-1} (d = 1: eps < 0)
+    const int L = 31 - __builtin_clz(n1);     // the node's level
+    bool use[LV - 1], right[LV - 1];
+    int pos[LV - 1];
+#pragma unroll
+    for (int l = 0; l < LV - 1; ++l) {
+      use[l] = l < L;
+      right[l] = use[l] && ((n1 >> (L - 1 - l)) & 1);
+      pos[l] = (use[l] ? (n1 >> (L - l)) - 1 : 0) * R + j;       // lane of the level-l ancestor
+    }
+    for (; it + LV - 1 <= to; it += LV) {
+      float lo_ = lo, hi_ = hi;
+#pragma unroll
+      for (int l = 0; l < LV - 1; ++l) {
+        const float mu_l = __fmaf_rn(hi_ - lo_, 0.5f, lo_);
+        lo_ = (use[l] && !right[l]) ? mu_l : lo_;
+        hi_ = right[l] ? mu_l : hi_;
+      }
+      const float mu = __fmaf_rn(hi_ - lo_, 0.5f, lo_);
+      const float eps = qp_eps(lower, nom, mu);
+      if (__any(!(eps > 0.f) && !(eps < 0.f))) {       // (uniform) a node the bracket would not leave
+        open |= qp_open_seq(lower, nom, it, it + LV - 1, tol, lo, hi, rec, true, valid);
+        continue;
+      }
+      const unsigned long long P = __ballot(eps > 0.f);
+      uint32_t bad = 0;
+#pragma unroll
+      for (int l = 0; l < LV - 1; ++l)
+        bad |= use[l] ? (((uint32_t)(P >> pos[l]) & 1u) ^ (right[l] ? 0u : 1u)) : 0u;
+      if (owner && bad == 0u) {
+        rec[it + L] = mu;
+        open |= ((valid && !(fabsf(eps) < tol)) ? 1u : 0u) << (it + L);
+        if (L == LV - 1) {
+          bc[0] = eps > 0.f ? mu : lo_;
+          bc[1] = eps > 0.f ? hi_ : mu;
+        }
+      }
+      lo = bc[0];
+      hi = bc[1];
+    }
+  }
+  if (it <= to) open |= qp_open_seq(lower, nom, it, to, tol, lo, hi, rec, true, valid);
+  return ~wave_or16(open) & qp_span(from, to);
+}
 
 // The weights one wave (hidden part p) reads in the MLP of a tile, held in registers for the whole
 // persistent kernel (108 VGPRs; the kernels run one wave per SIMD, 512 registers): no LDS reads on
@@ -331,8 +412,25 @@ __device__ __forceinline__ void ft16_sum(const float (*zpart)[64][4], int j, flo
 // all compute the same masks and the same K): no workgroup barrier and no LDS round trip for K;
 // wave 0 still publishes, shK is left untouched.  With more tiles the 4x polling costs more than
 // the barrier (B = 1024: exchange wait 2.35 -> 2.83 us per eval), so those keep the broadcast.
+// R: rows per wave (16 or 4); rec: the row's mu record (shared by the row's lanes of this wave),
+// bc: 2 LDS floats per (wave, row) for the tree bisection's bracket hand-over (FIODE_QP_TREE=0: the
+// sequential bisection on every lane).
+#ifndef FIODE_QP_TREE
+#define FIODE_QP_TREE 1
+#endif
+template <int R>
+__device__ __forceinline__ uint32_t qp_bisect_rows(const float (&lower)[C], const float (&nom)[C], int from, int to,
+                                                   float tol, float& lo, float& hi, float* rec, float* bc,
+                                                   bool valid) {
+  // (the depth-2 tree of 16-row waves measured slower than the sequential loop: 341 -> 348 us for the
+  // B = 2048 rk4 forward; depth 4 on 4-row waves: 234 -> 224 us at B = 128, dopri5 1263 -> 1171 us)
+  if constexpr (FIODE_QP_TREE != 0 && QpTree<R>::LV >= 4) return qp_bisect_tree<R>(lower, nom, from, to, tol, lo, hi, rec, bc, valid);
+  else return qp_bisect_seq(lower, nom, from, to, tol, lo, hi, rec, true, valid);
+}
+
+template <int R>
 __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&nominal)[C], float tol, int max_iter,
-                                         int kprev, bool valid, int p, int q, int lane, float* mu_rec_row,
+                                         int kprev, bool valid, int p, int q, int lane, float* mu_rec_row, float* bc,
                                          unsigned long long* slots, unsigned epoch, int32_t* status, int& shK,
                                          int& dead, int drop_block = -1,
                                          unsigned long long* prof = nullptr, int stride = 1, bool allg = false) {
@@ -342,7 +440,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
   const bool pr = prof && blockIdx.x == 0 && threadIdx.x == 0;      // phase timing (diagnostic builds)
   const uint64_t t0 = prof ? wall_clock64() : 0;
   qp_bracket(lower, nominal, lo, hi);
-  uint32_t conv = qp_bisect_seq(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, true, valid);
+  uint32_t conv = qp_bisect_rows<R>(lower, nominal, 0, kspec, tol, lo, hi, mu_rec_row, bc, valid);
   const uint64_t t1 = prof ? wall_clock64() : 0;
   if (pr) atomicAdd(prof + 6, (unsigned long long)(t1 - t0));
   const int ntiles = gridDim.x;
@@ -367,7 +465,7 @@ __device__ __forceinline__ int qp16_exit(const float (&lower)[C], const float (&
     if (kw < 0) atomicAdd(prof + 8, 1ull);
   }
   if (kw < 0) {                         // block-uniform: every tile saw the same masks
-    conv |= qp_bisect_seq(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, true, valid);
+    conv |= qp_bisect_rows<R>(lower, nominal, kspec + 1, last, tol, lo, hi, mu_rec_row, bc, valid);
     if (allg || p == 0) {
       unsigned long long* s2 = slots + (size_t)ntiles * stride;
       if (p == 0 && lane == 0) publish_mask(s2 + (size_t)blockIdx.x * stride, epoch, conv);

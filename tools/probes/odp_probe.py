@@ -51,3 +51,7 @@ for method, A in (("rk4", 0), ("dopri5", 64), ("dopri5", ops.odetrain_default_at
           f"{fwd / max(nfe, 1):.2f} us/eval, backward {e1.elapsed_time(e2) * 1e3:.0f} us; per eval (block 0): "
           f"mlp {t[1]:.2f}  nominal {t[5]:.2f}  QP+exit {t[3]:.2f} (bisection {t[6]:.2f}, exchange wait {t[7]:.2f})  "
           f"finalize {t[4]:.2f}  -> in-eval {t[1] + t[5] + t[3] + t[4]:.2f}", flush=True)
+    if method == "dopri5":
+        na = max(s[6], 1)
+        print(f"    per attempt ({na}): loop {prof[2] / na * 0.01:.2f} us, batch sums {prof[9] / na * 0.01:.2f} us "
+              f"(all {prof[9] * 0.01:.1f} us), evals {(t[1] + t[5] + t[3] + t[4]) * nfe / na:.2f} us", flush=True)
