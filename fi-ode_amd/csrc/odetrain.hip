@@ -40,13 +40,15 @@ using namespace fiode_dp;
 // set is never overwritten while it is read; 4 sets leave a margin.  The cleared region no longer
 // grows with the eval count (dopri5: the attempt capacity).
 constexpr int OT_XRING = 4;
+constexpr int FIODE_OT_KW_PRE = 256;      // dopri5: evals whose keep words k_ot_masks draws ahead
 
 struct OTArgs {
   int B, E, niters;
   int nslots;               // u64 words of xslots zeroed by k_ot_masks before the forward
-  int kw_lazy;              // dopri5, Philox p = 0.5: the forward draws each eval's keep words itself
-                            // (and stores them for the backward) instead of k_ot_masks drawing the
-                            // whole eval capacity up front
+  int kw_lazy;              // dopri5, Philox p = 0.5: the forward draws the keep words of evals >= kw_pre
+                            // itself (and stores them for the backward) instead of k_ot_masks drawing
+                            // the whole eval capacity up front
+  int kw_pre;               // evals whose keep words k_ot_masks draws (E unless kw_lazy)
   float t0, t1, hstep;
   int dropout_mode, bit_mode;
   uint32_t thr8;
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void k_ot_masks(OTArgs a) {
   if (q < a.nslots) a.xslots[q] = 0ull;
   if (q < 8) a.stats[q] = 0;
   if (q < 8) a.imeta[q] = 0;       // the solve's status word (saved [12]) and the dopri5 counters
-  if (a.dropout_mode == FIODE_DROPOUT_OFF || a.kw_lazy || q >= a.E * a.B) return;
+  if (a.dropout_mode == FIODE_DROPOUT_OFF || q >= a.kw_pre * a.B) return;
   const int e = q / a.B, b = q - e * a.B;
   const Rng rng = rng_of(a);
 #pragma unroll
@@ -1157,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       w2 = 0xFFFFFFFFu;
       return;
     }
-    if (a.kw_lazy) {          // the draws k_ot_masks would make (same stream, index, offset)
+    if (a.kw_lazy && e >= a.kw_pre) {   // the draws k_ot_masks would make (same stream, index, offset)
       const uint4 r0 = krng.draw((uint32_t)bb, RNG_STREAM_ODE_DROP + ((uint32_t)e << 5));
       const uint4 r1 = krng.draw((uint32_t)bb, RNG_STREAM_ODE_DROP + ((uint32_t)e << 5) + (1u << 4));
       w1[0] = r0.x; w1[1] = r0.y; w1[2] = r0.z; w1[3] = r0.w;
@@ -1185,9 +1187,18 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
   int e = 0;
   uint32_t kc1[4], kc2;
   fetch(0, kc1, kc2);
+#ifdef OT_PROFILE
+#define ODP_T0(V) const uint64_t V = wall_clock64();
+#define ODP_T1(SLOT, V) if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.prof + (SLOT), (unsigned long long)(wall_clock64() - V));
+#else
+#define ODP_T0(V)
+#define ODP_T1(SLOT, V)
+#endif
   auto eval = [&](const float (&h)[C], float (&k)[C]) {
     uint32_t kn1[4] = {0u, 0u, 0u, 0u}, kn2 = 0u;
+    ODP_T0(tf0)
     if (e + 1 < a.E) fetch(e + 1, kn1, kn2);
+    ODP_T1(10, tf0)
     if constexpr (T4) ot_eval4(a, w, sh, e, p, b, valid, lane, j, uacc, kc1[p], kc2, h, k);
     else ot_eval(a, w, sh, e, p, b, valid, lane, q, j, uacc, kc1, kc2, h, k);
 #pragma unroll
@@ -1269,28 +1280,35 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
     kput(0, fcur);
     float hin[C];
     for (int i = 0; i < 6; ++i) {
+      ODP_T0(ts0)
       float acc[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) acc[c] = 0.f;
-      for (int jj = 0; jj <= i; ++jj) {
-        float f[C];
-        kget(jj, f);
-        const float co = DP_BETA[i][jj] * dt32;
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
+      for (int jj = 0; jj < 6; ++jj) {
+        if (jj <= i) {          // (uniform; unrolled so the LDS reads of all terms issue together)
+          float f[C];
+          kget(jj, f);
+          const float co = DP_BETA[i][jj] * dt32;
+#pragma unroll
+          for (int c = 0; c < C; ++c) acc[c] = acc[c] + f[c] * co;
+        }
       }
 #pragma unroll
       for (int c = 0; c < C; ++c) hin[c] = y[c] + acc[c];
+      ODP_T1(11, ts0)
       float kn[C];
       eval(hin, kn);
       kput(i + 1, kn);
     }
     // y_new = the stage-5 input (FSAL); batch-global RMS error ratio
+    ODP_T0(te0)
     double ps[1] = {0.0};
     if (own) {
       float err[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) err[c] = 0.f;
+#pragma unroll
       for (int jj = 0; jj < 7; ++jj) {
         float f[C];
         kget(jj, f);
@@ -1305,7 +1323,9 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
         ps[0] += (double)qv * qv;
       }
     }
+    ODP_T1(12, te0)
     ot_batch_sum<1>(a, S.red, sh.dead, rep, ps, ps);
+    ODP_T0(tc0)
     const float ratio = (float)rms_of(ps[0], NBC);
     const bool accept = ratio <= 1.0f;
     if (lead) {
@@ -1337,6 +1357,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       dt = dt * fmin(DP_IFACTOR, fmax(DP_SAFETY / pow((double)ratio, 1.0 / 5.0), df));
     }
     ++n;
+    ODP_T1(13, tc0)
 #ifdef OT_PROFILE
     if (lead) atomicAdd(a.prof + 2, (unsigned long long)(wall_clock64() - ta0));
 #endif
@@ -1348,6 +1369,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
     float acc[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) acc[c] = 0.f;
+#pragma unroll
     for (int jj = 0; jj < 7; ++jj) {
       float f[C];
       kget(jj, f);
@@ -1392,12 +1414,15 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
     a.imeta[3] = (int32_t)rep;       // next unused reduction epoch: the backward continues from it
   }
 }
+#undef ODP_T0
+#undef ODP_T1
 
 // ---- backward: the reverse sweep of oracle/dopri5_train.py dopri5_adjoint ---------------------
 template <bool T4>
 struct OdpBwdShared {
   std::conditional_t<T4, OtBwdShared4, OtBwdShared> ot;
   float gk[4][7][T4 ? TR4 : TR][C];       // [wave][stage][row][c]: adjoints of the attempt's k_0..k_6
+  float kst[4][7][T4 ? TR4 : TR][C];      // [wave][stage][row][c]: the attempt's saved k_0..k_6
   double red[OT_XV];
   int dead;
 };
@@ -1454,6 +1479,22 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
     for (int c = 0; c < C; ++c) v[c] = gks[s][j][c];
   };
   auto krow = [&](int e, float (&v)[C]) { load_row10(a.vw + ((size_t)bb * a.E + e) * C, v); };
+  // the attempt's stage derivatives, staged in LDS once per attempt (loads issued together): read
+  // from global memory term by term they cost one dependent L2 round trip each, ~28 per attempt
+  float (*kss)[TRX][C] = S.kst[p];
+  auto kstage = [&](int fidx, int e0) {
+    float t[7][C];
+#pragma unroll
+    for (int jj = 0; jj < 7; ++jj) krow(jj == 0 ? fidx : e0 + jj - 1, t[jj]);
+#pragma unroll
+    for (int jj = 0; jj < 7; ++jj)
+#pragma unroll
+      for (int c = 0; c < C; ++c) kss[jj][j][c] = t[jj][c];
+  };
+  auto kget = [&](int s, float (&v)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] = kss[s][j][c];
+  };
   float gout[C];
   if (valid) load_row10(a.g_y + (size_t)b * C, gout);
   else
@@ -1479,7 +1520,15 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   else load_vjp_in(a, p, ecur, b, valid, q, cur);
   vjp_row_math<SN>(a, cur, crw);
   // evals visited nfe-1, nfe-2, ..., 0 (attempts in reverse, stages 5..0; then evals 1, 0)
+#ifdef OT_PROFILE
+#define ODB_T0(V) const uint64_t V = wall_clock64();
+#define ODB_T1(SLOT, V) if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.prof + (SLOT), (unsigned long long)(wall_clock64() - V));
+#else
+#define ODB_T0(V)
+#define ODB_T1(SLOT, V)
+#endif
   auto vjp = [&](const float (&g)[C], float (&gY)[C]) {
+    ODB_T0(tv0)
     if constexpr (T4) {
       load_vjp_in4(a, p, ecur - 1, b, valid, lane, nxt);
       ot_vjp4<SN>(a, wv, S.ot, buf, p, ecur, b, valid, lane, j, cur, crw, g, gY);
@@ -1493,18 +1542,24 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
     }
     buf ^= 1;
     --ecur;
+    ODB_T1(1, tv0)
   };
   float gy[C], gf[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) gy[c] = gf[c] = 0.f;
   double g_dt_next = 0.0, g_t_next = 0.0;
   for (int n = A - 1; n >= 0; --n) {
+#ifdef OT_PROFILE
+    const uint64_t tb0 = wall_clock64();
+#endif
     const double* lg = a.alog + (size_t)n * ALOG_W;
     const double tn = lg[ALOG_T], dtn = lg[ALOG_DT];
     const float ratio = (float)lg[ALOG_RATIO];
     const bool accept = lg[ALOG_ACCEPT] != 0.0;
     const int fidx = (int)lg[ALOG_FIDX], e0 = (int)lg[ALOG_E0];
     const float dts = (float)dtn;
+    ODB_T0(tk0)
+    kstage(fidx, e0);
     // controller: dt_{n+1} = dt_n * factor(ratio_n)
     double fac, dfac = 0.0;
     if (ratio == 0.f) {
@@ -1544,13 +1599,13 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
       for (int c = 0; c < C; ++c) ym[c] = 0.f;
       for (int jj = 0; jj < 7; ++jj) {
         float f[C];
-        krow(jj == 0 ? fidx : e0 + jj - 1, f);
+        kget(jj, f);
         const float co = DP_CMID[jj] * dts;
 #pragma unroll
         for (int c = 0; c < C; ++c) ym[c] = ym[c] + f[c] * co;
       }
-      krow(fidx, fa);
-      krow(e0 + 5, fb);
+      kget(0, fa);
+      kget(6, fb);
       const float x2 = x * x, x3 = x2 * x, x4 = x3 * x;
       float g_ym[C], gfa[C], gfb[C];
 #pragma unroll
@@ -1573,7 +1628,7 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
       }
       for (int jj = 0; jj < 7; ++jj) {
         float f[C], t[C];
-        krow(jj == 0 ? fidx : e0 + jj - 1, f);
+        kget(jj, f);
         const float co = DP_CMID[jj] * dts;
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -1585,13 +1640,15 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
       gadd(0, gfa);
       gadd(6, gfb);
     }
+    ODB_T1(5, tk0)
+    ODB_T0(tr0)
     if (g_ratio != 0.0) {            // ratio = rms(err / etol), etol = atol + rtol max(|y_n|, |y_new|)
       float err[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) err[c] = 0.f;
       float kk[7][C];
       for (int jj = 0; jj < 7; ++jj) {
-        krow(jj == 0 ? fidx : e0 + jj - 1, kk[jj]);
+        kget(jj, kk[jj]);
         const float co = DP_CERR[jj] * dts;
 #pragma unroll
         for (int c = 0; c < C; ++c) err[c] = err[c] + kk[jj][c] * co;
@@ -1618,27 +1675,33 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
         gadd(jj, t);
       }
     }
+    ODB_T1(4, tr0)
     // stages in reverse: k_{i+1} = f(Y_i), Y_i = y_n + sum_{j <= i} k_j beta_ij dt; y_new = Y_5
     for (int i = 5; i >= 0; --i) {
       float g[C], gY[C];
       gget(i + 1, g);
       vjp(g, gY);
+      ODB_T0(tj0)
       if (i == 5)
 #pragma unroll
         for (int c = 0; c < C; ++c) gY[c] += g_ynew[c];
 #pragma unroll
       for (int c = 0; c < C; ++c) g_yn[c] += gY[c];
-      for (int jj = 0; jj <= i; ++jj) {
-        float f[C], t[C];
-        krow(jj == 0 ? fidx : e0 + jj - 1, f);
-        const float co = DP_BETA[i][jj] * dts;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          t[c] = gY[c] * co;
-          pdt += (double)gY[c] * f[c] * DP_BETA[i][jj];
+      for (int jj = 0; jj < 6; ++jj) {
+        if (jj <= i) {          // (uniform)
+          float f[C], t[C];
+          kget(jj, f);
+          const float co = DP_BETA[i][jj] * dts;
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            t[c] = gY[c] * co;
+            pdt += (double)gY[c] * f[c] * DP_BETA[i][jj];
+          }
+          gadd(jj, t);
         }
-        gadd(jj, t);
       }
+      ODB_T1(3, tj0)
     }
     double red[2] = {own ? pdt : 0.0, own ? px : 0.0};
     ot_batch_sum<2>(a, S.red, S.dead, rep, red, red);
@@ -1656,6 +1719,9 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
 #pragma unroll
     for (int c = 0; c < C; ++c) gy[c] = g_yn[c];
     gget(0, gf);
+#ifdef OT_PROFILE
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.prof + 0, (unsigned long long)(wall_clock64() - tb0));
+#endif
   }
   // ---- the initial step: dt_0 = min(100 h0, h1) -----------------------------------------------
   const double d1 = a.meta[META_D1], d2 = a.meta[META_D2], h0 = a.meta[META_H0], h1 = a.meta[META_H1];
@@ -1715,6 +1781,8 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && !S.dead) a.imeta[3] = (int32_t)rep;
   if (threadIdx.x == 0 && S.dead) atomicMax(a.imeta + 3, (int32_t)(rep + 65536u));
 }
+#undef ODB_T0
+#undef ODB_T1
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1901,7 +1969,10 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
   const OtLayout L = ot_layout(a.B, a.E, a.A);
   a.nslots = (int)((L.kw - L.xs) / 8);
   a.kw_lazy = a.method == FIODE_ODE_DOPRI5 && a.dropout_mode == FIODE_DROPOUT_PHILOX && a.bit_mode;
-  const int nthreads = (a.kw_lazy || a.nslots > a.E * a.B) ? a.nslots : a.E * a.B;
+  // a dopri5 solve's first evals (a B = 128 step takes ~150) are drawn up front, off the solve's
+  // dependent chain (the lazy draw cost 0.4 us per eval there); the rest of the capacity lazily
+  a.kw_pre = a.kw_lazy ? std::min(a.E, FIODE_OT_KW_PRE) : a.E;
+  const int nthreads = std::max(a.nslots, a.kw_pre * a.B);
   hipLaunchKernelGGL(k_ot_masks, dim3((nthreads + 255) / 256), dim3(256), 0, st, a);
   FIODE_HIP_CHECK(hipGetLastError());
   if (a.method == FIODE_ODE_DOPRI5) {

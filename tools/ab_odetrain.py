@@ -33,5 +33,20 @@ for B, sn in ((128, False), (300, True), (37, False)):
     gy = torch.from_numpy(rng.normal(size=(B, 10)).astype(np.float32)).to(dev)
     grads, _ = ops.odetrain_backward(gy, x, w, ops.DynCfg(scale_nominal=sn), cfg, ws)
     out.update({f"g{k}{B}": v.cpu() for k, v in grads.items()})
+# the dopri5 train solve (bench configs[2] dynamics: scale_nominal, Philox dropout p = 0.5)
+for B in (128, 300):
+    P = make_params(seed=B + 1)
+    rng = np.random.default_rng(B + 1)
+    x = torch.from_numpy(rng.normal(size=(B, 10)).astype(np.float32)).to(dev)
+    h0 = torch.full((B, 10), 0.1, device=dev)
+    w = {k: torch.from_numpy(np.ascontiguousarray(getattr(P, k))).to(dev) for k in ops.WEIGHT_KEYS}
+    dyn = ops.DynCfg(scale_nominal=True, dropout=0.5)
+    cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=5, offset=7, method="dopri5",
+                              max_attempts=ops.odetrain_default_attempts(B))
+    y, st, ws = ops.odetrain_forward(x, h0, w, dyn, cfg)
+    out.update({f"dp_y{B}": y.cpu(), f"dp_stats{B}": st.cpu()})
+    gy = torch.from_numpy(rng.normal(size=(B, 10)).astype(np.float32)).to(dev)
+    grads, _ = ops.odetrain_backward(gy, x, w, dyn, cfg, ws)
+    out.update({f"dp_g{k}{B}": v.cpu() for k, v in grads.items()})
 torch.save(out, sys.argv[1])
 print("saved", sys.argv[1])

@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 5, pass p: dopri5 attempt loops (keep words drawn ahead, stage rows staged in LDS in the
+# backward): bit identity against the previous commit's library, the solve tests, phases, timings
+set -u
+R=$PWD; O=$R/gpurun_out/r05p; mkdir -p $O
+FIODE_LIB=tools/libfiode_base.so timeout -k 10 120 python -u tools/ab_odetrain.py $O/base.pt > $O/ab.log 2>&1 || { cat $O/ab.log; exit 1; }
+timeout -k 10 120 python -u tools/ab_odetrain.py $O/new.pt >> $O/ab.log 2>&1 || { cat $O/ab.log; exit 1; }
+python tools/ab_odetrain.py --cmp $O/base.pt $O/new.pt >> $O/ab.log 2>&1; echo "cmp rc=$?" >> $O/ab.log
+grep -c identical $O/ab.log; grep DIFFER $O/ab.log | head; tail -1 $O/ab.log
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_odetrain.py tests/test_gpu_odetrain_dp.py \
+    > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 120 python -u tools/probes/odp_probe.py > $O/odp_probe.log 2>&1 || { tail $O/odp_probe.log; exit 1; }
+grep -v amdgpu.ids $O/odp_probe.log
+FIODE_LIB=tools/libfiode_base.so timeout -k 10 120 python -u tools/probes/solve_ab.py > $O/solve_base.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/probes/solve_ab.py > $O/solve_new.log 2>&1 || exit 1
+for f in $O/solve_*.log; do echo "== $f"; grep -v "amdgpu.ids" $f; done

@@ -43,6 +43,7 @@ for method, A in (("rk4", 0), ("dopri5", 64), ("dopri5", ops.odetrain_default_at
         ops.odetrain_backward(torch.ones_like(y), x, w, dyn, cfg, ws)
         e2.record()
         torch.cuda.synchronize()
+        pb = ws[base: base + 16 * 8].view(torch.int64).cpu().numpy().astype(np.float64) - prof
     s = st.cpu().tolist()
     nfe = s[0]
     t = prof / max(nfe, 1) * 0.01          # us per eval
@@ -54,4 +55,10 @@ for method, A in (("rk4", 0), ("dopri5", 64), ("dopri5", ops.odetrain_default_at
     if method == "dopri5":
         na = max(s[6], 1)
         print(f"    per attempt ({na}): loop {prof[2] / na * 0.01:.2f} us, batch sums {prof[9] / na * 0.01:.2f} us "
-              f"(all {prof[9] * 0.01:.1f} us), evals {(t[1] + t[5] + t[3] + t[4]) * nfe / na:.2f} us", flush=True)
+              f"(all {prof[9] * 0.01:.1f} us), evals {(t[1] + t[5] + t[3] + t[4]) * nfe / na:.2f} us; keep-word fetch "
+              f"{prof[10] / na * 0.01:.2f}, stage inputs {prof[11] / na * 0.01:.2f}, error {prof[12] / na * 0.01:.2f}, "
+              f"controller {prof[13] / na * 0.01:.2f} us", flush=True)
+        print(f"    backward per attempt: loop {pb[0] / na * 0.01:.2f} us, batch sums {pb[9] / na * 0.01:.2f} us, "
+              f"VJP phases {pb[10:16].sum() / na * 0.01:.2f} us ({pb[10:16].sum() / max(nfe, 1) * 0.01:.2f} per VJP), "
+              f"vjp calls {pb[1] / na * 0.01:.2f}, stage-term loops {pb[3] / na * 0.01:.2f}, error adjoint "
+              f"{pb[4] / na * 0.01:.2f}, prologue {pb[5] / na * 0.01:.2f} us", flush=True)

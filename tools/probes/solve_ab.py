@@ -22,15 +22,19 @@ for method, B, sn in (("rk4", 128, False), ("rk4", 2048, False), ("dopri5", 128,
     dyn = ops.DynCfg(scale_nominal=sn, dropout=0.5)
     kw = {} if method == "rk4" else {"method": "dopri5", "max_attempts": ops.odetrain_default_attempts(B)}
     cfg = ops.odetrain_config(B, 0.0, 1.0, 0.1, L.FIODE_DROPOUT_PHILOX, seed=3, **kw)
-    ts = []
+    ts, tb = [], []
+    gy = torch.ones(B, 10, device=dev)
     for rep in range(25):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
         y, st, ws = ops.odetrain_forward(x, h0, w, dyn, cfg)
         e1.record()
+        grads, _ = ops.odetrain_backward(gy, x, w, dyn, cfg, ws)
+        e2.record()
         torch.cuda.synchronize()
         if rep >= 5:
             ts.append(e0.elapsed_time(e1) * 1e3)
+            tb.append(e1.elapsed_time(e2) * 1e3)
     stv = st.cpu().numpy().tolist()
-    print(f"{method} B={B}: forward median {np.median(ts):.1f} us (min {min(ts):.1f})  stats {stv}  "
-          f"y sum {float(y.double().sum()):.9e}", flush=True)
+    print(f"{method} B={B}: forward median {np.median(ts):.1f} us (min {min(ts):.1f}), backward median "
+          f"{np.median(tb):.1f} us  stats {stv}  y sum {float(y.double().sum()):.9e}", flush=True)
