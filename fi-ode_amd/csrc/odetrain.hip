@@ -1012,10 +1012,120 @@ constexpr int OT_XV = 4;          // float64 values per reduction exchange (at m
 enum { ALOG_T = 0, ALOG_DT, ALOG_RATIO, ALOG_ACCEPT, ALOG_FIDX, ALOG_E0, ALOG_W = 8 };
 enum { META_D0 = 0, META_D1, META_D2, META_H0, META_H1, META_CLAMP0, META_CLAMP1, META_DT0, META_R2, META_N = 16 };
 
+// float64 sum over the 64 lanes, the same value in every lane (fixed order): a DPP prefix scan
+// within each 16-lane row (VALU; the shuffle butterfly was 6 dependent LDS-crossbar round trips
+// per value), then the four row totals added in row order
+template <int N>
+__device__ __forceinline__ double dpp_row_shr(double x) {
+  const long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xFFFFFFFF), 0x110 + N, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x110 + N, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xFFFFFFFF), l);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+  return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+#ifndef FIODE_BSUM_DPP
+#define FIODE_BSUM_DPP 1
+#endif
+__device__ __forceinline__ double wave_dsum(double x) {
+  if constexpr (FIODE_BSUM_DPP == 0) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+    return x;
+  }
+  x += dpp_row_shr<1>(x);
+  x += dpp_row_shr<2>(x);
+  x += dpp_row_shr<4>(x);
+  x += dpp_row_shr<8>(x);
+  return ((readlane_d(x, 15) + readlane_d(x, 31)) + readlane_d(x, 47)) + readlane_d(x, 63);
+}
+
 // sum over all rows (every workgroup gets the same float64 values): the caller's per-lane values
-// count only on wave 0's owner lanes (q = 0, valid rows: the caller zeroes the others)
+// count only on owner lanes (the caller zeroes the others; every wave holds the same rows, so every
+// wave forms the same partial).  Wave 0 publishes the partial; every wave gathers the granules
+// itself and adds them in tile order, so the result needs no LDS broadcast and no barrier (the
+// dopri5 forward: 1146 -> 1123 us at B = 128).
 template <int NV>
-__device__ void ot_batch_sum(const OTArgs& a, double* red, int& dead, unsigned& ep, const double (&mine)[NV],
+__device__ void ot_batch_sum(const OTArgs& a, int& dead, unsigned& ep, const double (&mine)[NV],
+                             double (&out)[NV]) {
+  const int lane = threadIdx.x & 63;
+#ifdef OT_PROFILE
+  const uint64_t tp0 = wall_clock64();
+#endif
+  double w[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) w[i] = wave_dsum(mine[i]);
+  const int G = gridDim.x;
+  unsigned long long* buf = a.xr + (size_t)(ep & 1u) * G * 2 * OT_XV;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(w[v]);
+      publish_mask(buf + (size_t)blockIdx.x * 2 * OT_XV + 2 * v, ep, (uint32_t)(bits >> 32));
+      publish_mask(buf + (size_t)blockIdx.x * 2 * OT_XV + 2 * v + 1, ep, (uint32_t)bits);
+    }
+  }
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  bool timed_out = false;
+  for (int base = 0; base < G; base += 64) {
+    const int t = base + lane;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      unsigned long long x[2 * NV];
+#pragma unroll
+      for (int g = 0; g < 2 * NV; ++g) {
+        x[g] = 0;
+        if (t < G) {
+          x[g] = __hip_atomic_load((gu64_t*)(buf + (size_t)t * 2 * OT_XV + g), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          ok = ok && (unsigned)(x[g] >> 32) == ep;
+        }
+      }
+      if (__all(ok)) {
+        if (t < G) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v)
+            acc[v] += __longlong_as_double((long long)(((x[2 * v] & 0xFFFFFFFFull) << 32) | (x[2 * v + 1] & 0xFFFFFFFFull)));
+        }
+        break;
+      }
+      if (dead || ++spins > (1u << 22)) {     // ~0.5 s: a workgroup is not resident
+        timed_out = true;
+        if (lane == 0) {
+          atomicMax(a.stats ? a.stats + 3 : a.imeta + 2, 4);
+          dead = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  // a timed-out exchange summed only the granules that arrived: NaN, so everything computed from
+  // it (y_out in the forward; g_dt and every stage adjoint upstream of it in the backward) is
+  // poisoned instead of silently wrong
+  const bool poisoned = timed_out || dead;       // (a sticky earlier timeout poisons every later sum)
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double tot = wave_dsum(acc[v]);
+    out[v] = poisoned ? __builtin_nan("") : tot;
+  }
+  ++ep;
+#ifdef OT_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.prof + 9, (unsigned long long)(wall_clock64() - tp0));
+#endif
+}
+
+// The backward keeps the round-4 form: wave 0 gathers, LDS broadcast behind barriers (the form
+// above measured 35 us slower there at B = 128).
+template <int NV>
+__device__ void ot_batch_sum_bwd(const OTArgs& a, double* red, int& dead, unsigned& ep, const double (&mine)[NV],
                              double (&out)[NV]) {
   const int lane = threadIdx.x & 63;
 #ifdef OT_PROFILE
@@ -1102,7 +1212,6 @@ template <bool T4>
 struct OdpShared {
   std::conditional_t<T4, OtShared4, OtShared> ot;
   float kst[4][7][T4 ? TR4 : TR][C];      // [wave][stage][row][c]: the current attempt's k_0..k_6
-  double red[OT_XV];
 };
 
 __device__ __forceinline__ double rms_of(double sumsq, double n) { return sqrt(sumsq / n); }
@@ -1224,7 +1333,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       s01[1] += (double)qq * qq;
     }
   }
-  ot_batch_sum<2>(a, S.red, sh.dead, rep, s01, s01);
+  ot_batch_sum<2>(a, sh.dead, rep, s01, s01);
   const float d0 = (float)rms_of(s01[0], NBC), d1 = (float)rms_of(s01[1], NBC);
   const bool clamp0 = d0 < 1e-5f || d1 < 1e-5f;
   const float h0s = clamp0 ? 1e-6f : (0.01f * d0) / d1;
@@ -1243,7 +1352,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
         s2[0] += (double)qv * qv;
       }
     }
-    ot_batch_sum<1>(a, S.red, sh.dead, rep, s2, s2);
+    ot_batch_sum<1>(a, sh.dead, rep, s2, s2);
     const float r2 = (float)rms_of(s2[0], NBC);
     const float d2 = r2 / h0s;
     const bool clamp1 = d1 <= 1e-15f && d2 <= 1e-15f;
@@ -1324,7 +1433,7 @@ __global__ __launch_bounds__(256) void k_odp_fwd(OTArgs a) {
       }
     }
     ODP_T1(12, te0)
-    ot_batch_sum<1>(a, S.red, sh.dead, rep, ps, ps);
+    ot_batch_sum<1>(a, sh.dead, rep, ps, ps);
     ODP_T0(tc0)
     const float ratio = (float)rms_of(ps[0], NBC);
     const bool accept = ratio <= 1.0f;
@@ -1704,7 +1813,7 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
       ODB_T1(3, tj0)
     }
     double red[2] = {own ? pdt : 0.0, own ? px : 0.0};
-    ot_batch_sum<2>(a, S.red, S.dead, rep, red, red);
+    ot_batch_sum_bwd<2>(a, S.red, S.dead, rep, red, red);
     g_dt += red[0];
     double g_t;
     if (last) {
@@ -1762,7 +1871,7 @@ __global__ __launch_bounds__(256) void k_odp_bwd(OTArgs a) {
     sh0 += (double)gyi[c] * f0[c];
   }
   double red1[1] = {own ? sh0 : 0.0};
-  ot_batch_sum<1>(a, S.red, S.dead, rep, red1, red1);
+  ot_batch_sum_bwd<1>(a, S.red, S.dead, rep, red1, red1);
   g_h0 += red1[0];
   if (!clamp0) g_d1 += -g_h0 * h0 / d1;   // h0 = 0.01 d0 / d1
 #pragma unroll
