@@ -409,7 +409,9 @@ __device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const Src& src, 
 #pragma unroll
   for (int u = 0; u < PB * PB / 4 / PI_NT; ++u) {
     const int t = threadIdx.x + PI_NT * u;
-    const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
+    // transposed: lanes on consecutive rows r, so the b32 stores of one column hit 32 distinct banks
+    // (row-fastest lanes put 16 lanes of a group on one bank)
+    const int r = transpose ? t % PB : t / (PB / 4), c4 = transpose ? (t / PB) * 4 : (t % (PB / 4)) * 4;
     const f4v v = src.row4(r0 + r, c0 + c4);
     if (transpose) {
 #pragma unroll

@@ -86,7 +86,9 @@ struct GJB {
   static constexpr int NB = NP / 16;          // blocks per side
   static constexpr int NT = 64 * NW;
   static constexpr int LDM = NP + 8;          // cm row stride (floats; = 8 mod 64: the b128 lane groups conflict-free)
-  static constexpr int LDP = 20;              // panel buffers' row stride
+  static constexpr int LDP = 24;              // panel buffers' row stride (ds_read_b128 of lane (c, q) at
+                                              // 24 c + 4 q: every 16-lane group of the table's grouping
+                                              // covers the 64 banks; 20 was 2-way)
   struct Smem {
     float cm[NP][LDM];                        // cm[col][row] of X
     float cb[NP][LDP];                        // cb[i][k] = X[i][K0 + k] before the round's update
@@ -154,7 +156,8 @@ struct GJB {
         *reinterpret_cast<f4v*>(&sm.rt[16 * jb + c][4 * q]) = acc;              // rt[j][4q + r] = R[4q + r][j]
       }
       for (int t = threadIdx.x; t < NP * 4; t += NT) {
-        const int i = t >> 2, k4 = (t & 3) * 4;
+        const int i = t % NP, k4 = (t / NP) * 4;      // lanes on consecutive rows i: the b32 reads of one
+                                                      // column hit 32 distinct banks (4-way before)
         *reinterpret_cast<f4v*>(&sm.cb[i][k4]) =
             f4v{sm.cm[16 * kb + k4][i], sm.cm[16 * kb + k4 + 1][i], sm.cm[16 * kb + k4 + 2][i], sm.cm[16 * kb + k4 + 3][i]};
       }

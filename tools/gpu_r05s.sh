@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 5, pass s: profile pass at HEAD (kernel stats, PMC passes) and the step's critical chain
+set -u
+R=$PWD
+bash tools/gpu_profile.sh r05s --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+cd $R/tools && python critical_chain.py $R/gpurun_out/r05s/trace/run_kernel_trace.csv > $R/gpurun_out/r05s/chain.txt 2>&1 || true
+head -2 $R/gpurun_out/r05s/chain.txt
