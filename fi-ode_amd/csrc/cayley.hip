@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256) k_panel_update(int np, int k0, const floa
 #pragma unroll
     for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sm.cm[16 * w + 4 * q + r][16 * bj + i] = acc[bj][r];
+      for (int r = 0; r < 4; ++r) UpdGJ::at(sm, 16 * w + 4 * q + r, 16 * bj + i) = acc[bj][r];
     __syncthreads();
     UpdGJ::invert(sm);
     UpdGJ::store(sm, P_next, PB, PB);
@@ -342,22 +342,33 @@ __device__ __forceinline__ void pi_acquire(bool acq) {
 // bj = 2 (w >> 2) + b, b = 0, 1 of a tile, i.e. acc[b][r] = X[16 rw + 4 q + r][16 (2 ch + b) + i]
 // (rw = w & 3, ch = w >> 2, lane = 16 q + i) -- a 64^3 product is 32 MFMAs per wave.
 constexpr int PI_NT = 512;
+// k_pinv's LDS tiles: 64 x 64, no padding, XOR-swizzled like gjb.h's image (element (a, b) of a tile at
+// [a][b ^ 4 (a & 15)]): the b128 operand reads, the b128 / b32 stores of the accumulators and of the
+// published tiles, and the b32 reads all conflict-free (the padded stride 72 left the stores and
+// b32 accesses 2-way: bank-conflict share 0.28, r05u)
+constexpr int LDTS = PB;
+__device__ __forceinline__ int tsw(int a, int b) { return b ^ ((a & 15) << 2); }
 // a published tile -> LDS, column-major (B operand: dst[col][row]) or row-major (A operand)
-__device__ __forceinline__ void pi_to_bt(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
+__device__ __forceinline__ void pi_put_bt(float (*dst)[LDTS], int e, f4v v) {   // f4 e of a tile, column-major
+  const int w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
+  const int a = 16 * bj + (ln & 15);
+  *reinterpret_cast<f4v*>(&dst[a][tsw(a, 16 * w + 4 * (ln >> 4))]) = v;
+}
+__device__ __forceinline__ void pi_put_a(float (*dst)[LDTS], int e, f4v v) {    // f4 e of a tile, row-major
+  const int w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
 #pragma unroll
-  for (int u = 0; u < 1024 / PI_NT; ++u) {
-    const int e = threadIdx.x + PI_NT * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
-    *reinterpret_cast<f4v*>(&dst[16 * bj + (ln & 15)][16 * w + 4 * (ln >> 4)]) = pi_load(r, e);
+  for (int k = 0; k < 4; ++k) {
+    const int a = 16 * w + 4 * (ln >> 4) + k;
+    dst[a][tsw(a, 16 * bj + (ln & 15))] = v[k];
   }
 }
-__device__ __forceinline__ void pi_to_a(float (*dst)[LDT], __amdgpu_buffer_rsrc_t r) {
+__device__ __forceinline__ void pi_to_bt(float (*dst)[LDTS], __amdgpu_buffer_rsrc_t r) {
 #pragma unroll
-  for (int u = 0; u < 1024 / PI_NT; ++u) {
-    const int e = threadIdx.x + PI_NT * u, w = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
-    const f4v v = pi_load(r, e);
+  for (int u = 0; u < 1024 / PI_NT; ++u) pi_put_bt(dst, threadIdx.x + PI_NT * u, pi_load(r, threadIdx.x + PI_NT * u));
+}
+__device__ __forceinline__ void pi_to_a(float (*dst)[LDTS], __amdgpu_buffer_rsrc_t r) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dst[16 * w + 4 * (ln >> 4) + k][16 * bj + (ln & 15)] = v[k];
-  }
+  for (int u = 0; u < 1024 / PI_NT; ++u) pi_put_a(dst, threadIdx.x + PI_NT * u, pi_load(r, threadIdx.x + PI_NT * u));
 }
 // Where the matrix to invert comes from: a row-major n x n array (PlainSrc), or built on load from a
 // dense Cayley map's weight (DenseSrc: M = I + s (U' - U'^T) + s^2 G with s = alpha / ||W||, the
@@ -405,7 +416,7 @@ struct DenseSrc {
 };
 // a 64 x 64 block of a row-major matrix (row stride ld) -> LDS, row-major or transposed
 template <class Src>
-__device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const Src& src, int r0, int c0, bool transpose) {
+__device__ __forceinline__ void pi_tile_load(float (*dst)[LDTS], const Src& src, int r0, int c0, bool transpose) {
 #pragma unroll
   for (int u = 0; u < PB * PB / 4 / PI_NT; ++u) {
     const int t = threadIdx.x + PI_NT * u;
@@ -415,32 +426,40 @@ __device__ __forceinline__ void pi_tile_load(float (*dst)[LDT], const Src& src, 
     const f4v v = src.row4(r0 + r, c0 + c4);
     if (transpose) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dst[c4 + e][r] = v[e];
+      for (int e = 0; e < 4; ++e) dst[c4 + e][tsw(c4 + e, r)] = v[e];
     } else {
-      *reinterpret_cast<f4v*>(&dst[r][c4]) = v;
+      *reinterpret_cast<f4v*>(&dst[r][tsw(r, c4)]) = v;
     }
   }
 }
 // this thread's accumulator registers <-> LDS (row-major A image / column-major B image)
-__device__ __forceinline__ void acc_to_a(float (*dst)[LDT], const f4v (&acc)[2], int rw, int ch, int i, int q) {
+__device__ __forceinline__ void acc_to_a(float (*dst)[LDTS], const f4v (&acc)[2], int rw, int ch, int i, int q) {
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dst[16 * rw + 4 * q + k][16 * (2 * ch + b) + i] = acc[b][k];
+    for (int k = 0; k < 4; ++k) {
+      const int a = 16 * rw + 4 * q + k;
+      dst[a][tsw(a, 16 * (2 * ch + b) + i)] = acc[b][k];
+    }
 }
-__device__ __forceinline__ void acc_to_bt(float (*dst)[LDT], const f4v (&acc)[2], int rw, int ch, int i, int q) {
+__device__ __forceinline__ void acc_to_bt(float (*dst)[LDTS], const f4v (&acc)[2], int rw, int ch, int i, int q) {
 #pragma unroll
-  for (int b = 0; b < 2; ++b) *reinterpret_cast<f4v*>(&dst[16 * (2 * ch + b) + i][16 * rw + 4 * q]) = acc[b];
+  for (int b = 0; b < 2; ++b) {
+    const int a = 16 * (2 * ch + b) + i;
+    *reinterpret_cast<f4v*>(&dst[a][tsw(a, 16 * rw + 4 * q)]) = acc[b];
+  }
 }
 // acc[b] += sign A[16 rw + i][:] . BT[16 (2 ch + b) + i][:]  (the k order permuted as tile_gemm's)
-__device__ __forceinline__ void pi_gemm(const float (*A)[LDT], const float (*BT)[LDT], int rw, int ch, int i, int q,
+__device__ __forceinline__ void pi_gemm(const float (*A)[LDTS], const float (*BT)[LDTS], int rw, int ch, int i, int q,
                                         f4v (&acc)[2], float sign) {
 #pragma unroll
   for (int kc = 0; kc < PB / 16; ++kc) {
-    const f4v a4 = *reinterpret_cast<const f4v*>(&A[16 * rw + i][16 * kc + 4 * q]) * sign;
+    const int aa = 16 * rw + i;
+    const f4v a4 = *reinterpret_cast<const f4v*>(&A[aa][tsw(aa, 16 * kc + 4 * q)]) * sign;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const f4v b4 = *reinterpret_cast<const f4v*>(&BT[16 * (2 * ch + b) + i][16 * kc + 4 * q]);
+      const int ab = 16 * (2 * ch + b) + i;
+      const f4v b4 = *reinterpret_cast<const f4v*>(&BT[ab][tsw(ab, 16 * kc + 4 * q)]);
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc[b] = fiode_gjb::mfma(a4[s], b4[s], acc[b]);
     }
@@ -462,7 +481,7 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
                                                 int acq, unsigned long long* prof) {
   if (skip && *skip) return;                  // (uniform)
   constexpr int n = NB * PB;
-  __shared__ __attribute__((aligned(16))) float lds[4][PB][LDT + 0];
+  __shared__ __attribute__((aligned(16))) float lds[4][PB][LDTS];
   __shared__ int dead;
   __shared__ float slot;
   const int m = blockIdx.y;
@@ -500,14 +519,14 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
   if (blockIdx.x == 0) {
     // ---- the chain: every pivot block and its inverse --------------------------------------------
     typedef fiode_gjb::GJB<PB, PI_NT / 64> CG;
-    static_assert(sizeof(CG::Smem) <= 2 * sizeof(float) * PB * LDT, "pivot scratch fits two LDS tiles");
-    CG::Smem& sm = *reinterpret_cast<CG::Smem*>(&lds[0][0][0]);     // cm = lds[0] (row stride LDT)
-    float (*sX)[LDT] = lds[2];
-    float (*sB)[LDT] = lds[3];
-    static_assert(CG::LDM == LDT, "the pivot image doubles as the product's A operand");
+    static_assert(sizeof(CG::Smem) <= 2 * sizeof(float) * PB * LDTS, "pivot scratch fits two LDS tiles");
+    CG::Smem& sm = *reinterpret_cast<CG::Smem*>(&lds[0][0][0]);     // cm = lds[0] (same swizzle as the tiles)
+    float (*sX)[LDTS] = lds[2];
+    float (*sB)[LDTS] = lds[3];
+    static_assert(CG::LDM == LDTS, "the pivot image doubles as the product's A operand");
     for (int t = threadIdx.x; t < PB * PB / 4; t += PI_NT) {         // X_00 (gjb.h load's layout)
       const int r = t / (PB / 4), c4 = (t % (PB / 4)) * 4;
-      *reinterpret_cast<f4v*>(&sm.cm[r][c4]) = src.row4(r, c4);
+      *CG::at4(sm, r, c4) = src.row4(r, c4);
     }
     __syncthreads();
     // the next pivot's three operand tiles (version k - 1 for step k + 1), fetched into registers
@@ -538,7 +557,7 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
       for (int b = 0; b < 2; ++b) {
         f4v v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = sm.cm[16 * rw + 4 * q + r][16 * (2 * ch + b) + i];
+        for (int r = 0; r < 4; ++r) v[r] = CG::at(sm, 16 * rw + 4 * q + r, 16 * (2 * ch + b) + i);
         pi_store(rP, ptile(k) + own_e(b), v);
       }
       pi_signal(&pflag[k]);
@@ -552,10 +571,9 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
       } else {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {                                // the prefetched tiles -> LDS / acc
-          const int e = threadIdx.x + PI_NT * u, we = e >> 8, bj = (e >> 6) & 3, ln = e & 63;
-          *reinterpret_cast<f4v*>(&sB[16 * bj + (ln & 15)][16 * we + 4 * (ln >> 4)]) = nxt_b[u];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sX[16 * we + 4 * (ln >> 4) + r][16 * bj + (ln & 15)] = nxt_a[u][r];
+          const int e = threadIdx.x + PI_NT * u;
+          pi_put_bt(sB, e, nxt_b[u]);
+          pi_put_a(sX, e, nxt_a[u]);
           acc[u] = nxt_d[u];
         }
       }
@@ -576,9 +594,9 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
   } else {
     // ---- one tile of X ---------------------------------------------------------------------------
     const int t = blockIdx.x - 1, ti = t / NB, tj = t % NB;
-    float (*sA)[LDT] = lds[0];
-    float (*sB)[LDT] = lds[1];
-    float (*sX)[LDT] = lds[2];
+    float (*sA)[LDTS] = lds[0];
+    float (*sB)[LDTS] = lds[1];
+    float (*sX)[LDTS] = lds[2];
     load_in(ti * PB, tj * PB);
     for (int k = 0; k < NB; ++k) {
       if (ti == tj && k == ti - 1) continue;       // X_kk^(k-1) is the chain's; nobody reads this one

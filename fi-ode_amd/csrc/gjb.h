@@ -85,7 +85,13 @@ template <int NP, int NW>
 struct GJB {
   static constexpr int NB = NP / 16;          // blocks per side
   static constexpr int NT = 64 * NW;
-  static constexpr int LDM = NP + 8;          // cm row stride (floats; = 8 mod 64: the b128 lane groups conflict-free)
+  // cm is XOR-swizzled, no padding: element (a, b) of cm[a][b] sits at cm[a][b ^ 4 (a & (NP/4 - 1))] (4-float
+  // groups stay contiguous).  Against the lane groups of MI355X_MICROARCH.md's LDS table every access
+  // below is conflict-free: the b128 operand reads (lane (c, q) at row 16 j + c, column 16 i + 4 q: 4-float
+  // slot (4 i + q) ^ c), their b128 stores (8 contiguous lanes c: slot 4 i ^ c) and the b32 column reads
+  // and stores (rows 4 q + r: the row bits flip bit 4 of the column); the padded stride 72 left the b128
+  // stores and the b32 accesses 2-way (LDS bank-conflict share 0.28 in k_pinv, r05u).
+  static constexpr int LDM = NP;
   static constexpr int LDP = 24;              // panel buffers' row stride (ds_read_b128 of lane (c, q) at
                                               // 24 c + 4 q: every 16-lane group of the table's grouping
                                               // covers the 64 banks; 20 was 2-way)
@@ -95,9 +101,19 @@ struct GJB {
     float rt[NP][LDP];                        // rt[j][k] = R[k][j]
   };
 
+  static __device__ __forceinline__ int sw(int a, int b) { return b ^ ((a & (NP / 4 - 1)) << 2); }
+  static __device__ __forceinline__ float& at(Smem& sm, int a, int b) { return sm.cm[a][sw(a, b)]; }
+  static __device__ __forceinline__ float at(const Smem& sm, int a, int b) { return sm.cm[a][sw(a, b)]; }
+  static __device__ __forceinline__ f4v* at4(Smem& sm, int a, int b) {      // b % 4 == 0
+    return reinterpret_cast<f4v*>(&sm.cm[a][sw(a, b)]);
+  }
+  static __device__ __forceinline__ const f4v* at4(const Smem& sm, int a, int b) {
+    return reinterpret_cast<const f4v*>(&sm.cm[a][sw(a, b)]);
+  }
+
   // the 16 x 16 block (bi, bj) of X: lane (c, q) <-> X[16 bi + 4q + r][16 bj + c]
   static __device__ __forceinline__ f4v* blk(Smem& sm, int bi, int bj, int c, int q) {
-    return reinterpret_cast<f4v*>(&sm.cm[16 * bj + c][16 * bi + 4 * q]);
+    return at4(sm, 16 * bj + c, 16 * bi + 4 * q);
   }
 
   // (GJB_PRIO=1 raises the pivot wave's issue priority during the elimination: measured no gain on
@@ -117,7 +133,7 @@ struct GJB {
     f4v acc, b4;
     if (jb == kb) {
       acc = f4v{0.f, 0.f, 0.f, 0.f};
-      b4 = *reinterpret_cast<const f4v*>(&sm.cm[16 * kb + c][16 * kb + 4 * q]);   // P[4q + s][j]
+      b4 = *at4(sm, 16 * kb + c, 16 * kb + 4 * q);                                 // P[4q + s][j]
     } else {
       acc = *blk(sm, ib, jb, c, q);
       b4 = *reinterpret_cast<const f4v*>(&sm.rt[16 * jb + c][4 * q]);            // R[4q + s][j]
@@ -148,8 +164,8 @@ struct GJB {
         // A[i][k] = P[i][k] = cm[K0 + k][K0 + i] (i = c, k = 4q + s); B[k][j] = X[K0 + k][J0 + j] = cm[J0 + j][K0 + k]
         f4v pa;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) pa[s] = sm.cm[16 * kb + 4 * q + s][16 * kb + c];
-        const f4v b4 = *reinterpret_cast<const f4v*>(&sm.cm[16 * jb + c][16 * kb + 4 * q]);
+        for (int s = 0; s < 4; ++s) pa[s] = at(sm, 16 * kb + 4 * q + s, 16 * kb + c);
+        const f4v b4 = *at4(sm, 16 * jb + c, 16 * kb + 4 * q);
         f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma(pa[s], b4[s], acc);
@@ -158,8 +174,8 @@ struct GJB {
       for (int t = threadIdx.x; t < NP * 4; t += NT) {
         const int i = t % NP, k4 = (t / NP) * 4;      // lanes on consecutive rows i: the b32 reads of one
                                                       // column hit 32 distinct banks (4-way before)
-        *reinterpret_cast<f4v*>(&sm.cb[i][k4]) =
-            f4v{sm.cm[16 * kb + k4][i], sm.cm[16 * kb + k4 + 1][i], sm.cm[16 * kb + k4 + 2][i], sm.cm[16 * kb + k4 + 3][i]};
+        *reinterpret_cast<f4v*>(&sm.cb[i][k4]) = f4v{at(sm, 16 * kb + k4, i), at(sm, 16 * kb + k4 + 1, i),
+                                                     at(sm, 16 * kb + k4 + 2, i), at(sm, 16 * kb + k4 + 3, i)};
       }
       __syncthreads();
       // (e) rank-16 update; wave 0 takes the next pivot block alone and inverts it at once
@@ -196,13 +212,13 @@ struct GJB {
         const int cc = c4 + u;
         v[u] = (r < n && cc < n) ? src[(int64_t)r * ld + cc] : (r == cc ? 1.0f : 0.0f);
       }
-      *reinterpret_cast<f4v*>(&sm.cm[r][c4]) = v;      // row r of M = column r of X
+      *at4(sm, r, c4) = v;                              // row r of M = column r of X
     }
   }
   static __device__ __forceinline__ void store(const Smem& sm, float* __restrict__ dst, int n, int64_t ld) {
     for (int t = threadIdx.x; t < NP * NP / 4; t += NT) {
       const int r = t / (NP / 4), c4 = (t % (NP / 4)) * 4;
-      const f4v v = *reinterpret_cast<const f4v*>(&sm.cm[r][c4]);
+      const f4v v = *at4(sm, r, c4);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (r < n && c4 + u < n) dst[(int64_t)r * ld + c4 + u] = v[u];

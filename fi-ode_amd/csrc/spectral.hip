@@ -503,10 +503,10 @@ __global__ void __launch_bounds__(64 * NW) k_spec_inv_re(SpecArgs a) {
   for (int t = threadIdx.x; t < K * K; t += G::NT) {
     const int i = t / K, j = t % K;
     const c32 m = Mf[t];
-    sm.cm[i][j] = m.x;               // cm[r][c] = E[r][c] (gjb.h: row-major in, row-major out)
-    sm.cm[K + i][K + j] = m.x;
-    sm.cm[i][K + j] = -m.y;
-    sm.cm[K + i][j] = m.y;
+    G::at(sm, i, j) = m.x;            // cm[r][c] = E[r][c] (gjb.h: row-major in, row-major out)
+    G::at(sm, K + i, K + j) = m.x;
+    G::at(sm, i, K + j) = -m.y;
+    G::at(sm, K + i, j) = m.y;
   }
   __syncthreads();
   G::invert(sm);
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(64 * NW) k_spec_inv_re(SpecArgs a) {
   c32* If = a.inv + (int64_t)f * K * K;
   for (int t = threadIdx.x; t < K * K; t += G::NT) {
     const int i = t / K, j = t % K;
-    const c32 v = make_float2(sm.cm[i][j], sm.cm[K + i][j]);
+    const c32 v = make_float2(G::at(sm, i, j), G::at(sm, K + i, j));
     If[t] = v;
     c32 q = cscale(v, 2.0f);
     if (i == j) q.x -= 1.0f;
