@@ -55,9 +55,14 @@ struct GJ {
   static constexpr int NT = RT * CT;                 // threads
   static constexpr int U = TR > TC ? TR : TC;        // unroll of the pivot loop
   static_assert(TR % 2 == 0 && TC % 2 == 0 && U % TR == 0 && U % TC == 0, "tile shape");
+  // pivot rows in LDS: with 4 complex columns per thread (32 B), threads tj and tj + 8 of a 16-lane
+  // group would read the same banks (2-way; LDS bank-conflict share 0.54 in k_spec_inv<64>), so every
+  // 32 columns are shifted by 2 complex (4 banks)
+  static constexpr bool ROW_PAD = sizeof(T) == 8 && TC == 4;
+  static __device__ __forceinline__ int rc(int c) { return ROW_PAD ? c + (c >> 5) * 2 : c; }
   struct Smem {
-    T rowk[2][2][NP];   // [parity][pivot row 0/1][col]
-    T colk[2][2][NP];   // [parity][pivot col 0/1][row]
+    T rowk[2][2][ROW_PAD ? NP + NP / 16 : NP];   // [parity][pivot row 0/1][col (rc)]
+    T colk[2][2][NP];                            // [parity][pivot col 0/1][row]
   };
 
   // Invert the n x n (n <= NP, padded with I) matrix held in a[][] by this workgroup's threads.
@@ -77,8 +82,8 @@ struct GJ {
         if (own_r) {
 #pragma unroll
           for (int c = 0; c < TC; ++c) {
-            sm.rowk[b][0][c0 + c] = a[rr][c];
-            sm.rowk[b][1][c0 + c] = a[rr + 1][c];
+            sm.rowk[b][0][rc(c0 + c)] = a[rr][c];
+            sm.rowk[b][1][rc(c0 + c)] = a[rr + 1][c];
           }
         }
         if (own_c) {
@@ -97,11 +102,11 @@ struct GJ {
         }
 #pragma unroll
         for (int c = 0; c < TC; ++c) {
-          x0[c] = sm.rowk[b][0][c0 + c];
-          x1[c] = sm.rowk[b][1][c0 + c];
+          x0[c] = sm.rowk[b][0][rc(c0 + c)];
+          x1[c] = sm.rowk[b][1][rc(c0 + c)];
         }
-        const T q00 = sm.rowk[b][0][k], q01 = sm.rowk[b][0][k + 1];
-        const T q10 = sm.rowk[b][1][k], q11 = sm.rowk[b][1][k + 1];
+        const T q00 = sm.rowk[b][0][rc(k)], q01 = sm.rowk[b][0][rc(k + 1)];
+        const T q10 = sm.rowk[b][1][rc(k)], q11 = sm.rowk[b][1][rc(k + 1)];
         const T idet = Ops::recip(Ops::sub(Ops::mul(q00, q11), Ops::mul(q01, q10)));
         const T p00 = Ops::mul(q11, idet), p11 = Ops::mul(q00, idet);
         const T p01 = Ops::neg(Ops::mul(q01, idet)), p10 = Ops::neg(Ops::mul(q10, idet));
