@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
+import os
 from typing import Optional
 
 import torch
@@ -495,7 +496,8 @@ class CayleyLinear(nn.Linear):
         the layers before it); the next training forward joins it."""
         self._pre = _prefetch(stream, self.effective_weight)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_weight(self) -> torch.Tensor:
+        """The effective weight this forward uses (the prefetched map when one is pending)."""
         if self._pre is not None and self.training:
             Q = _take(self._pre)
             self._pre = None
@@ -506,7 +508,87 @@ class CayleyLinear(nn.Linear):
         # kept detached: a stored Q with its graph would keep the step's autograd nodes (and the
         # parameters' AccumulateGrad nodes) alive into the next step
         self._Q = Q.detach()
-        return F.linear(x, Q if self.training else self._Q, self.bias)
+        return Q if self.training else self._Q
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return F.linear(x, self.forward_weight(), self.bias)
+
+
+# KWLargeConcat's head (Linear -> GroupSort -> Linear -> GroupSort -> Linear) as one autograd node
+# whose backward keeps only the input-gradient chain on the step's stream (see _LinearHeadFn)
+HEAD_WGRAD_SIDE = os.environ.get("FIODE_HEAD_WGRAD_SIDE", "1") != "0"
+_HEAD_STREAMS: dict = {}
+
+
+def _head_stream(dev: torch.device) -> torch.cuda.Stream:
+    key = dev.index
+    if key not in _HEAD_STREAMS:
+        _HEAD_STREAMS[key] = torch.cuda.Stream(dev)
+    return _HEAD_STREAMS[key]
+
+
+class _LinearHeadFn(torch.autograd.Function):
+    """y = L3(gs(L2(gs(L1(h))))) with L_k(x) = x Q_k^T + b_k (F.linear's addmm) and gs the GroupSort
+    kernel.  Autograd's addmm backward runs each layer's input gradient, weight gradient and bias
+    sum in sequence on one stream, so the next layer's input gradient waited for the weight
+    gradient it does not need (the head's backward is on the step's critical path).  Here the
+    weight / bias gradients (the same GEMM g^T x and column sum) of every layer run on a side
+    stream forked as soon as that layer's output gradient exists, beside the input-gradient chain,
+    and join the step's stream once at the end."""
+
+    @staticmethod
+    def forward(ctx, h, Q1, b1, Q2, b2, Q3, b3):
+        from . import ops
+        y1 = torch.addmm(b1, h, Q1.t())
+        z1 = ops.groupsort_forward(y1, 1)
+        y2 = torch.addmm(b2, z1, Q2.t())
+        z2 = ops.groupsort_forward(y2, 1)
+        out = torch.addmm(b3, z2, Q3.t())
+        ctx.save_for_backward(h, Q1, Q2, Q3, y1, z1, y2, z2)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import ops
+        h, Q1, Q2, Q3, y1, z1, y2, z2 = ctx.saved_tensors
+        g = g.contiguous()
+        cur = torch.cuda.current_stream(g.device)
+        side = _head_stream(g.device)
+        wg = {}
+
+        def wgrad(k, gk, x):
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                wg[k] = (gk.t().mm(x), gk.sum(0))
+            gk.record_stream(side)
+            x.record_stream(side)
+
+        wgrad(3, g, z2)
+        g2 = ops.groupsort_backward(y2, g.mm(Q3), 1)
+        wgrad(2, g2, z1)
+        g1 = ops.groupsort_backward(y1, g2.mm(Q2), 1)
+        wgrad(1, g1, h)
+        dh = g1.mm(Q1)
+        cur.wait_stream(side)
+        for dW, db in wg.values():
+            dW.record_stream(cur)
+            db.record_stream(cur)
+        return dh, wg[1][0], wg[1][1], wg[2][0], wg[2][1], wg[3][0], wg[3][1]
+
+
+def linear_head(mods, h: torch.Tensor):
+    """Apply KWLargeConcat's head modules to h: one _LinearHeadFn node when training on ROCm with
+    the GroupSort head, else module by module."""
+    fusable = (HEAD_WGRAD_SIDE and h.is_cuda and len(mods) == 5 and
+               all(isinstance(m, CayleyLinear) and m.training and m.bias is not None for m in mods[0::2]) and
+               all(isinstance(m, GroupSort) for m in mods[1::2]) and torch.is_grad_enabled())
+    if not fusable:
+        for m in mods:
+            h = m(h)
+        return h
+    l1, l2, l3 = mods[0::2]
+    return _LinearHeadFn.apply(h.contiguous(), l1.forward_weight(), l1.bias, l2.forward_weight(), l2.bias,
+                               l3.forward_weight(), l3.bias)
 
 
 class _GroupSortFn(torch.autograd.Function):

@@ -15,7 +15,7 @@ from typing import Optional, Sequence
 import torch
 import torch.nn as nn
 
-from .cayley import CayleyConv, CayleyLinear, GroupSort
+from .cayley import CayleyConv, CayleyLinear, GroupSort, linear_head
 
 
 class Normalize(nn.Module):
@@ -104,9 +104,7 @@ class KWLargeConcat(nn.Module):
                 h = m(h)
             i += 1
         h = h.permute(3, 2, 0, 1).reshape(h.shape[3], -1)
-        for m in mods[i + 1:]:
-            h = m(h)
-        return h
+        return linear_head(mods[i + 1:], h)
 
 
 def make_ortho_KWLarge_Concat(n_in_channels=3, n_outputs=10, mu=(0.485, 0.456, 0.406), std=(0.225, 0.225, 0.225),

@@ -511,3 +511,35 @@ def test_dense_fused_inverse_equals_staged(shape):
     Qt = Qt if shape[-2] >= shape[-1] else Qt.mT
     eye = torch.eye(Qt.shape[-1], device=dev)
     assert float((Qt.mT @ Qt - eye).abs().max()) < 5e-5
+
+
+def test_linear_head_side_stream_wgrad_matches_autograd():
+    """KWLargeConcat's head as one node (_LinearHeadFn: weight / bias gradients on a side stream)
+    against the module-by-module autograd chain (F.linear + GroupSort) on the same inputs: the
+    output and the input gradient bit for bit (same kernels, same stream order), the weight
+    gradients within float32 rounding (the same GEMMs; bias sums may reduce in another order)."""
+    from fiode_amd import cayley as cy
+    from fiode_amd.models import KWLargeConcat
+    dev = _dev()
+    torch.manual_seed(0)
+    net = KWLargeConcat().to(dev).train()
+    mods = list(net.model)[-5:]
+    h0 = torch.randn(128, 4096, device=dev)
+    gout = torch.randn(128, 10, device=dev)
+    res = {}
+    for fused in (False, True):
+        cy.HEAD_WGRAD_SIDE = fused
+        for m in mods:
+            if isinstance(m, cy.CayleyLinear):
+                m.zero_grad(set_to_none=True)
+        h = h0.clone().requires_grad_(True)
+        out = cy.linear_head(mods, h)
+        out.backward(gout)
+        torch.cuda.synchronize()
+        res[fused] = (out.detach().clone(), h.grad.clone(),
+                      [p.grad.clone() for m in mods if isinstance(m, cy.CayleyLinear) for p in (m.weight, m.alpha, m.bias)])
+    cy.HEAD_WGRAD_SIDE = True
+    assert torch.equal(res[False][0], res[True][0])
+    assert torch.equal(res[False][1], res[True][1])
+    for a, b in zip(res[False][2], res[True][2]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), float((a - b).abs().max())
