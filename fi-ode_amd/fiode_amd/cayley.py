@@ -706,22 +706,44 @@ class _SpectralConvFn(torch.autograd.Function):
         else:
             G = ops.sconv_rfft2(gy, n, cout, B)
         gx = gQ = gb = None
-        if ctx.needs_input_grad[0]:
-            gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
-        if ctx.needs_input_grad[1]:
+        need_x, need_q, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], has_bias and ctx.needs_input_grad[2]
+        wq = None
+        if need_q:
             key = (n, str(G.device))
             wq = _SPECTRAL_GRAD_WEIGHTS.get(key)
             if wq is None:
                 kb = torch.arange(n // 2 + 1, device=G.device)
                 w = torch.where((kb == 0) | (kb == n // 2), 1.0, 2.0) / float(n * n)
                 wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
-            gQ = torch.matmul(G, X.mH) * wq
-        if has_bias and ctx.needs_input_grad[2]:
-            gb = G[0].real.sum(-1)
+
+        def wgrad():
+            gq = torch.matmul(G, X.mH) * wq if need_q else None
+            gbias = G[0].real.sum(-1) if need_b else None
+            return gq, gbias
+        # the weight / bias gradients beside the input gradient (which alone is on the backward's
+        # critical chain), on the side stream of the linear head's, joined before returning
+        side = _head_stream(G.device) if (CONV_WGRAD_SIDE and G.is_cuda and need_x and (need_q or need_b)) else None
+        if side is not None:
+            cur = torch.cuda.current_stream(G.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                gQ, gb = wgrad()
+            G.record_stream(side)
+            X.record_stream(side)
+        if need_x:
+            gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
+        if side is not None:
+            cur.wait_stream(side)
+            for t in (gQ, gb):
+                if t is not None:
+                    t.record_stream(cur)
+        else:
+            gQ, gb = wgrad()
         return gx, gQ, gb, None, None, None
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
+CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
 
 # The conv layers' map-ahead work (map backward, early update, refresh) runs on one stream per layer
 # (False) or on one stream shared by all layers (True; tools/ab_step.py conv_one_stream).
