@@ -341,51 +341,17 @@ class _SmallCayleyFn(torch.autograd.Function):
 
     @staticmethod
     def _backward(ctx, gQ):
+        from . import ops, _lib as L
         Wb, al, nrm, inv = ctx.saved_tensors
-        return _small_backward(Wb, al, nrm, inv, gQ, *ctx.shapes)
-
-
-def _small_forward(W: torch.Tensor, alpha: torch.Tensor):
-    """(Q, inv, nrm) of the one-kernel map (fiode_small_cayley_forward), no autograd."""
-    from . import ops, _lib as L
-    Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1]).contiguous()
-    al = alpha.detach().reshape(-1).contiguous().float()
-    b, cout, cin = Wb.shape
-    k = min(cout, cin)
-    Q = torch.empty_like(Wb)
-    inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
-    nrm = torch.empty(b, dtype=torch.float32, device=W.device)
-    L.check(L.lib().fiode_small_cayley_forward(ops._stream(W.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
-                                               Q.data_ptr(), inv.data_ptr(), nrm.data_ptr()),
-            "fiode_small_cayley_forward")
-    return Q, inv, nrm
-
-
-def _small_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
-    from . import ops, _lib as L
-    b, cout, cin = Wb.shape
-    gQb = gQ.reshape(b, cout, cin).contiguous().float()
-    gW = torch.empty_like(Wb)
-    ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
-    L.check(L.lib().fiode_small_cayley_backward(ops._stream(Wb.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
-                                                nrm.data_ptr(), inv.data_ptr(), gQb.data_ptr(), gW.data_ptr(),
-                                                ga.data_ptr()), "fiode_small_cayley_backward")
-    return gW.reshape(wshape), ga.reshape(ashape)
-
-
-def _map_forward_state(W: torch.Tensor, alpha: torch.Tensor):
-    """cayley_scaled(W, alpha) of one real 2-D CayleyLinear weight WITHOUT autograd, with what its
-    backward needs: (Q, inv, nrm, small) -- the same kernels as cayley_scaled's forward."""
-    if SMALL_FUSED and _small_ok(W):
-        Q, inv, nrm = _small_forward(W, alpha)
-        return Q.reshape(W.shape), inv, nrm, True
-    if _dense_fused_ok(W):
-        st, inv, Q = _dense_forward_fused(W, alpha)
-    else:
-        st, M = _dense_prep(W, alpha)
-        inv = _block_inverse(M)
-        Q = _dense_finish(st, inv)
-    return Q.reshape(W.shape), inv, st["nrm"], False
+        wshape, ashape = ctx.shapes
+        b, cout, cin = Wb.shape
+        gQb = gQ.reshape(b, cout, cin).contiguous().float()
+        gW = torch.empty_like(Wb)
+        ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
+        L.check(L.lib().fiode_small_cayley_backward(ops._stream(Wb.device), b, cout, cin, Wb.data_ptr(), al.data_ptr(),
+                                                    nrm.data_ptr(), inv.data_ptr(), gQb.data_ptr(), gW.data_ptr(),
+                                                    ga.data_ptr()), "fiode_small_cayley_backward")
+        return gW.reshape(wshape), ga.reshape(ashape)
 
 
 def _small_ok(W: torch.Tensor) -> bool:
@@ -514,7 +480,6 @@ class CayleyLinear(nn.Linear):
         self.alpha = nn.Parameter(self.weight.detach().norm().reshape(1).clone())
         self._Q = None
         self._pre = None
-        self._store = None              # map computed ahead (pipeline_on), else None
 
     def reset_parameters(self) -> None:
         std = 1.0 / math.sqrt(self.weight.shape[1])
@@ -529,48 +494,10 @@ class CayleyLinear(nn.Linear):
     def prefetch(self, stream: torch.cuda.Stream) -> None:
         """Compute this step's Cayley map on a side stream (its latency-bound inverse overlaps
         the layers before it); the next training forward joins it."""
-        if getattr(self, "_store", None) is not None:
-            return
         self._pre = _prefetch(stream, self.effective_weight)
 
-    # ---- maps computed ahead (GraphTrainStep), as CayleyConv's: the next step's Q right after this
-    # step's update, inside the backward, on the layer's own stream
-    def pipeline_on(self) -> bool:
-        """Keep this layer's map in fixed buffers, computed ahead by refresh_map (now, from the
-        current parameters); returns whether the layer is pipelined (ROCm float32 only)."""
-        if not (self.weight.is_cuda and self.weight.dtype == torch.float32 and DENSE_FUSED and LINEAR_AHEAD):
-            return False
-        Q, inv, nrm, small = _map_forward_state(self.weight, self.alpha)
-        self._store = {"Q": Q, "inv": inv, "nrm": nrm, "small": small, "stream": torch.cuda.Stream(self.weight.device)}
-        return True
-
-    def pipeline_off(self) -> None:
-        self._store = None
-
-    def refresh_map(self) -> None:
-        """Recompute the stored map from the current parameters on the current stream (the same
-        kernels as the step-start map, so the same Q bit for bit)."""
-        st = self._store
-        Q, inv, nrm, _ = _map_forward_state(self.weight, self.alpha)
-        st["Q"].copy_(Q)
-        st["inv"].copy_(inv)
-        st["nrm"].copy_(nrm)
-
     def forward_weight(self) -> torch.Tensor:
-        """The effective weight this forward uses (the map computed ahead, or the prefetched map
-        when one is pending)."""
-        st = getattr(self, "_store", None)
-        if st is not None and self.training and torch.is_grad_enabled():
-            # the node's backward (map backward + the store's hook) runs on the layer's own stream
-            side = st["stream"]
-            main = torch.cuda.current_stream(self.weight.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                Q = _DenseCayleyStoredFn.apply(self.weight, self.alpha, st)
-            main.wait_stream(side)
-            self._pre = None
-            self._Q = Q.detach()
-            return Q
+        """The effective weight this forward uses (the prefetched map when one is pending)."""
         if self._pre is not None and self.training:
             Q = _take(self._pre)
             self._pre = None
@@ -585,42 +512,6 @@ class CayleyLinear(nn.Linear):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return F.linear(x, self.forward_weight(), self.bias)
-
-
-# CayleyLinear maps computed ahead (pipeline_on) when GraphTrainStep turns the pipeline on: measured
-# 115 us SLOWER per step than the maps at the step start (tools/ab_step.py linear_at_start, r05ab:
-# 1.499 vs 1.384 ms) -- the 512 inverses and the wide map's GEMMs inside the backward hold CUs the
-# conv stack's backward chain needs -- so off (FIODE_LINEAR_AHEAD=1 turns it on; bit-identical)
-LINEAR_AHEAD = os.environ.get("FIODE_LINEAR_AHEAD", "0") == "1"
-
-
-class _DenseCayleyStoredFn(torch.autograd.Function):
-    """The Q of a CayleyLinear whose map was computed AHEAD into fixed buffers (pipeline_on /
-    refresh_map), as _SpectralCayleyStoredFn for the conv layers: forward hands out the stored Q;
-    backward is the map's (_dense_backward / _small_backward from the stored inverse and norm, the
-    parameters read in place), then ``store["on_grads"]`` (if set) gets (dL/dW, dL/dalpha) --
-    GraphTrainStep updates the layer there and computes its next map.  Applied on the layer's own
-    stream, so autograd runs this backward there as soon as dL/dQ exists (the head's node), beside
-    the conv stack's backward, instead of on the step's stream after it."""
-
-    @staticmethod
-    def forward(ctx, W, alpha, store: dict):
-        ctx.store = store
-        ctx.save_for_backward(W, alpha)
-        return store["Q"].detach()
-
-    @staticmethod
-    def backward(ctx, gQ):
-        W, alpha = ctx.saved_tensors
-        st = ctx.store
-        Wb = W.detach().reshape(-1, W.shape[-2], W.shape[-1])
-        al = alpha.detach().reshape(-1)
-        bwd = _small_backward if st["small"] else _dense_backward
-        gw, ga = bwd(Wb, al, st["nrm"], st["inv"], gQ, W.shape, alpha.shape)
-        hook = st.get("on_grads")
-        if hook is not None:
-            hook(gw, ga)
-        return gw, ga, None
 
 
 # KWLargeConcat's head (Linear -> GroupSort -> Linear -> GroupSort -> Linear) as one autograd node

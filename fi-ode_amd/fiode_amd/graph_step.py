@@ -271,13 +271,13 @@ class GraphTrainStep:
     # (ode_reuse_features False) each layer has two map nodes per step, so there the maps are
     # refreshed after the optimizer step instead (late refresh, correct for any number of uses).
     def _maps_ahead_on(self):
-        from .cayley import CayleyConv, CayleyLinear
+        from .cayley import CayleyConv
         from .optim import _KernelStepMixin, _kernel_ok_params
         once = getattr(self.module, "ode_reuse_features", True) or not getattr(self.module, "train_ode", False)
         self.early = self.single and once and isinstance(self.opt, _KernelStepMixin)
         root = getattr(self.module, "init_coordinates", self.module)       # the backbone's layers
         for c in root.modules():
-            if isinstance(c, (CayleyConv, CayleyLinear)) and c.pipeline_on():
+            if isinstance(c, CayleyConv) and c.pipeline_on():
                 self.piped.append(c)
         if self.early and not all(_kernel_ok_params(self.opt, [c.weight, c.alpha]) for c in self.piped):
             self.early = False          # a group the kernel does not cover: update in step()

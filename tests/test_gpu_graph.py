@@ -106,42 +106,8 @@ def test_maps_ahead_equal_step_start_maps(train_ode, reuse):
         mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         opt = mod.configure_optimizers(capturable=True)[0][0]
         gs = GraphTrainStep(mod, opt, x, y, warmup=2, maps_ahead=ahead)
-        from fiode_amd.cayley import CayleyConv, CayleyLinear
-        assert sum(isinstance(c, CayleyConv) for c in gs.piped) == (4 if ahead else 0)
-        assert sum(isinstance(c, CayleyLinear) for c in gs.piped) == 0      # (cayley.LINEAR_AHEAD off)
+        assert len(gs.piped) == (4 if ahead else 0)
         assert gs.early == (ahead and (reuse or not train_ode))
-        losses = [float(gs.step()) for _ in range(3)]
-        torch.cuda.synchronize()
-        out[ahead] = (losses, [p.detach().clone() for p in mod.parameters()])
-        gs.close()
-    assert out[True][0] == out[False][0]
-    for a, b in zip(out[True][1], out[False][1]):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("train_ode", [False, True])
-def test_linear_maps_ahead_equal_step_start_maps(train_ode):
-    """The same with the backbone CayleyLinears' maps computed ahead too (cayley.LINEAR_AHEAD, off by
-    default: measured slower): bit-identical losses and parameters."""
-    import bench
-    from fiode_amd import cayley as CY
-    from fiode_amd.cayley import CayleyLinear
-    from fiode_amd.graph_step import GraphTrainStep
-    dev = _dev()
-    g = torch.Generator(device="cpu").manual_seed(7)
-    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
-    y = torch.randint(0, 10, (32,), generator=g).to(dev)
-    out = {}
-    for ahead in (True, False):
-        CY.LINEAR_AHEAD = ahead
-        try:
-            mod = bench.build_module(dev, seed=0, train_ode=train_ode)
-            mod.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
-            opt = mod.configure_optimizers(capturable=True)[0][0]
-            gs = GraphTrainStep(mod, opt, x, y, warmup=2, maps_ahead=True)
-        finally:
-            CY.LINEAR_AHEAD = False
-        assert sum(isinstance(c, CayleyLinear) for c in gs.piped) == (3 if ahead else 0)
         losses = [float(gs.step()) for _ in range(3)]
         torch.cuda.synchronize()
         out[ahead] = (losses, [p.detach().clone() for p in mod.parameters()])

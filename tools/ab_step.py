@@ -207,22 +207,7 @@ def conv_wgrad_main(m):
     RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_SIDE", True))
 
 
-def linear_ahead(m):
-    from fiode_amd import cayley as CY
-    CY.LINEAR_AHEAD = True        # the CayleyLinear maps computed ahead inside the backward (as the convs')
-    RESTORE.append(lambda: setattr(CY, "LINEAR_AHEAD", False))
-
-
-def maps_bwd_side(m):
-    from fiode_amd import cayley as CY
-    CY.DENSE_BWD_ON_MAIN = False  # the linear maps' backward on their forward's (prefetch) stream
-    CY.SMALL_BWD_ON_MAIN = False
-    RESTORE.append(lambda: setattr(CY, "DENSE_BWD_ON_MAIN", True))
-    RESTORE.append(lambda: setattr(CY, "SMALL_BWD_ON_MAIN", True))
-
-
-ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
-       "linear_ahead": linear_ahead, "maps_bwd_side": maps_bwd_side, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
+ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
