@@ -13,6 +13,7 @@ validation_step, configure_optimizers, log, current_epoch, global_step).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -143,6 +144,42 @@ class ODELossMixFn(torch.autograd.Function):
 # attribute GraphTrainStep sets on the gradient seed it passes to backward(): a float32 scalar 1.0
 UNIT_GRAD = "_fiode_unit_grad"
 
+# The dynamics weights' gradient of the training loss as its own autograd node on a side stream
+# (_DynWeightTapFn): LyapODELossFn's backward then ends with dL/dx_feat, which alone the backbone's
+# backward waits for
+DYN_WGRAD_SIDE = os.environ.get("FIODE_DYN_WGRAD_SIDE", "1") != "0"
+
+
+_ONES: dict = {}
+
+
+def _one(dev) -> torch.Tensor:
+    t = _ONES.get(str(dev))
+    if t is None:
+        t = _ONES[str(dev)] = torch.ones(1, dtype=torch.float32, device=dev)
+    return t
+
+
+class _DynWeightTapFn(torch.autograd.Function):
+    """Carries the dynamics weights' gradients of LyapODELossFn to the weights.  Its forward (applied
+    on a side stream) returns a token that LyapODELossFn takes as an input; LyapODELossFn's backward
+    returns the token's gradient after the solve's adjoint sweep and dL/dx_feat, and leaves the
+    weight-gradient work (the solve's weight-gradient chain, the fan-out's saved weight gradients
+    added) in ``box``.  Autograd runs this node's backward after it, on the side stream its forward
+    ran on, and synchronises the streams itself -- so the backbone's backward (on the step's stream)
+    starts right after dL/dx_feat instead of after the weight-gradient chain."""
+
+    @staticmethod
+    def forward(ctx, box: dict, *weights):
+        ctx.box = box
+        return torch.empty((), dtype=torch.float32, device=weights[0].device)
+
+    @staticmethod
+    def backward(ctx, _gtok):
+        fn = ctx.box.pop("weights")
+        ctx.box = None
+        return (None,) + tuple(fn())
+
 
 class LyapODELossFn(torch.autograd.Function):
     """The configs[1] training loss as ONE autograd node (pl_modules.py:444-500): the fused
@@ -156,7 +193,7 @@ class LyapODELossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_feat, x_ode, Q1, b1, Qx, bx, Q2, b2, Q3, b3, h0, y, plan: dict, oplan: dict, p: float,
-                ode_stream):
+                ode_stream, box=None, tok=None):
         from .cayley import _prefetch, _take
         w = {"Q1": Q1, "b1": b1, "Qx": Qx, "bx": bx, "Q2": Q2, "b2": b2, "Q3": Q3, "b3": b3}
         w = {k: v.detach().contiguous() for k, v in w.items()}
@@ -201,6 +238,7 @@ class LyapODELossFn(torch.autograd.Function):
         ctx.ode = (gunit, xo, w, oplan, ws)
         ctx.p = float(p)
         ctx.split = x_ode is not None
+        ctx.box = box
         return total
 
     @staticmethod
@@ -214,6 +252,30 @@ class LyapODELossFn(torch.autograd.Function):
         ctx.ode = None
         unit = getattr(go, UNIT_GRAD, False)
         g_y = gunit if unit else gunit * go
+        box, ctx.box = ctx.box, None
+        if box is not None:
+            # dL/dx_feat here (the adjoint sweep); the weights' gradients in _DynWeightTapFn's backward
+            lyap = ctx.lyap_unit if unit else torch._foreach_mul(ctx.lyap, go * (1.0 - ctx.p))
+            ctx.lyap = ctx.lyap_unit = None
+            if ctx.split:
+                gxo = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
+                gx = lyap[0]
+            else:      # ode + lyap inside the dL/dx_feat kernel (times an exact 1.0: the same sum)
+                gx = ops.odetrain_backward_x(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws, gx_add=lyap[0],
+                                             gx_add_scale=_one(g_y.device))
+                gxo = None
+
+            def weights():       # (on the tap's side stream: what it reads was allocated elsewhere)
+                side = torch.cuda.current_stream(xo.device)
+                for t in [xo, ws] + list(w.values()) + list(lyap[1:]):
+                    t.record_stream(side)
+                gr = ops.odetrain_backward_weights(xo, w, oplan["dyn"], oplan["cfg"], ws)
+                ode = [gr[k] for k in ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")]
+                torch._foreach_add_(ode, lyap[1:])
+                return ode
+            box["weights"] = weights
+            tg = go if go.dim() == 0 else go.reshape(())
+            return (gx, gxo) + (None,) * 8 + (None, None, None, None, None, None, None, tg)
         gr, _ = ops.odetrain_backward(g_y, xo, w, oplan["dyn"], oplan["cfg"], ws)
         keys = ("x_feat", "Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         ode = [gr[k] for k in keys]
@@ -225,7 +287,7 @@ class LyapODELossFn(torch.autograd.Function):
         else:
             torch._foreach_add_(ode, lyap)
             gx, gxo = ode[0], None
-        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None)
+        return (gx, gxo) + tuple(ode[1:]) + (None, None, None, None, None, None, None, None)
 
 
 class DecisionBoundary(nn.Module):
@@ -661,8 +723,20 @@ class LyapunovLearning(nn.Module):
                 self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
             stream = self._ode_stream
         p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
-        total = LyapODELossFn.apply(static_state, x_ode, w["Q1"], w["b1"], w["Qx"], w["bx"], w["Q2"], w["b2"], w["Q3"],
-                                    w["b3"], h0, y, plan, oplan, p, stream)
+        keys = ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
+        if DYN_WGRAD_SIDE and static_state.is_cuda and torch.is_grad_enabled():
+            box = {}
+            if getattr(self, "_wtap_stream", None) is None:
+                self._wtap_stream = torch.cuda.Stream(static_state.device)
+            side, main = self._wtap_stream, torch.cuda.current_stream(static_state.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                tok = _DynWeightTapFn.apply(box, *[w[k] for k in keys])
+            main.wait_stream(side)
+            wd = [w[k].detach() for k in keys]
+            total = LyapODELossFn.apply(static_state, x_ode, *wd, h0, y, plan, oplan, p, stream, box, tok)
+        else:
+            total = LyapODELossFn.apply(static_state, x_ode, *[w[k] for k in keys], h0, y, plan, oplan, p, stream)
         sc = plan["scalars"]
         self.log("kappa", plan["kappa_dev"] if plan.get("kappa_dev") is not None else plan["kappa"])
         self.log("effective_batch_size", sc[1])

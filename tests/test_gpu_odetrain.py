@@ -133,26 +133,65 @@ def test_fused_loss_node_equals_three_nodes(reuse):
     the node sums ode + lyap * ((1 - p) go) exactly as autograd's accumulation does, with the same
     Philox draws (same seed / offset) and the solve on its side stream in both."""
     import bench
+    from fiode_amd import lyapunov as LY
     dev = _dev()
     x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
     yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
     out = {}
-    for variant in ("fused", "three"):
-        mod = bench.build_module(dev, seed=0, train_ode=True)
-        mod.parallel_cayley = False
-        mod.ode_reuse_features = reuse
-        mod.fused_ode_loss = variant != "three"
-        mod._rng_offset = 0
-        loss = mod.compute_loss(x, yb, 32, "relu")
-        loss.backward()
-        torch.cuda.synchronize()
-        out[variant] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
-                        {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
+    LY.DYN_WGRAD_SIDE = False          # the one-call backward (the split one: the test below)
+    try:
+        for variant in ("fused", "three"):
+            mod = bench.build_module(dev, seed=0, train_ode=True)
+            mod.parallel_cayley = False
+            mod.ode_reuse_features = reuse
+            mod.fused_ode_loss = variant != "three"
+            mod._rng_offset = 0
+            loss = mod.compute_loss(x, yb, 32, "relu")
+            loss.backward()
+            torch.cuda.synchronize()
+            out[variant] = (loss.detach().clone(), float(mod.logged["loss_ode"]),
+                            {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
+    finally:
+        LY.DYN_WGRAD_SIDE = True
     lb, ob, gb = out["three"]
     la, oa, ga = out["fused"]
     assert torch.equal(la, lb) and oa == ob
     for n in ga:
         assert torch.equal(ga[n], gb[n]), n
+
+
+@pytest.mark.parametrize("reuse", [True, False])
+def test_dynamics_weight_grad_node_matches_one_call(reuse):
+    """The dynamics weights' gradients as their own side-stream node (_DynWeightTapFn: the solve's
+    backward split into fiode_odetrain_backward_x + _weights) against the one-call backward: the same
+    loss, the dynamics parameters' gradients bit for bit, the backbone's within float32 rounding
+    (dL/dx_feat is the same sum in another order, test_split_backward_entry_points_equal_one_call)."""
+    import bench
+    from fiode_amd import lyapunov as LY
+    dev = _dev()
+    x = torch.rand(32, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    yb = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
+    out = {}
+    try:
+        for side in (True, False):
+            LY.DYN_WGRAD_SIDE = side
+            mod = bench.build_module(dev, seed=0, train_ode=True)
+            mod.ode_reuse_features = reuse
+            mod._rng_offset = 0
+            loss = mod.compute_loss(x, yb, 32, "relu")
+            loss.backward()
+            torch.cuda.synchronize()
+            out[side] = (loss.detach().clone(),
+                         {n: p.grad.detach().clone() for n, p in mod.named_parameters() if p.requires_grad})
+    finally:
+        LY.DYN_WGRAD_SIDE = True
+    assert torch.equal(out[True][0], out[False][0])
+    for n, a in out[True][1].items():
+        b = out[False][1][n]
+        if "dyn_fun" in n:
+            assert torch.equal(a, b), n
+        else:
+            torch.testing.assert_close(a, b, rtol=2e-4, atol=1e-7, msg=n)
 
 
 def test_split_backward_entry_points_equal_one_call():

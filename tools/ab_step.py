@@ -207,7 +207,14 @@ def conv_wgrad_main(m):
     RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_SIDE", True))
 
 
-ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
+def dyn_wgrad_main(m):
+    from fiode_amd import lyapunov as LY
+    LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
+    RESTORE.append(lambda: setattr(LY, "DYN_WGRAD_SIDE", True))
+
+
+ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+       "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
