@@ -684,8 +684,9 @@ class _SpectralConvFn(torch.autograd.Function):
         G = rfft2(d/dpre),  dQ = (w_kb / n^2) G X^H,  dx = irfft2(Q^H G),  dbias = sum_b Re G[0]."""
 
     @staticmethod
-    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool):
+    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None):
         from . import ops
+        ctx.wstream = wstream
         B = x.shape[-1]
         nf, cout, cin = Q.shape
         X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
@@ -720,6 +721,31 @@ class _SpectralConvFn(torch.autograd.Function):
             gq = torch.matmul(G, X.mH) * wq if need_q else None
             gbias = G[0].real.sum(-1) if need_b else None
             return gq, gbias
+        ws = ctx.wstream
+        ctx.wstream = None
+        if ws is not None and CONV_WGRAD_MAPSTREAM and G.is_cuda and (need_q or need_b):
+            # the weight gradient on the layer's map stream, where its consumer (the stored map's
+            # backward, then the layer's early update) runs: no join -- the step's stream goes on
+            # with dL/dx while it runs.  The bias gradient (read by the optimizer's final step) on
+            # the step's stream, or with CONV_WGRAD_MAPSTREAM_BIAS on the map stream too, joined
+            # through conv_wgrad_join (GraphTrainStep, after the backward).
+            cur = torch.cuda.current_stream(G.device)
+            ws.wait_stream(cur)
+            with torch.cuda.stream(ws):
+                gQ = torch.matmul(G, X.mH) * wq if need_q else None
+                if need_b and CONV_WGRAD_MAPSTREAM_BIAS:
+                    gb = G[0].real.sum(-1)
+                    ev = torch.cuda.Event()
+                    ev.record(ws)
+                    _CONV_WGRAD_EVENTS.append(ev)
+                    gb.record_stream(cur)
+            G.record_stream(ws)
+            X.record_stream(ws)
+            if need_b and not CONV_WGRAD_MAPSTREAM_BIAS:
+                gb = G[0].real.sum(-1)
+            if need_x:
+                gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
+            return gx, gQ, gb, None, None, None, None
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
         # critical chain), on the side stream of the linear head's, joined before returning
         side = _head_stream(G.device) if (CONV_WGRAD_SIDE and G.is_cuda and need_x and (need_q or need_b)) else None
@@ -739,11 +765,23 @@ class _SpectralConvFn(torch.autograd.Function):
                     t.record_stream(cur)
         else:
             gQ, gb = wgrad()
-        return gx, gQ, gb, None, None, None
+        return gx, gQ, gb, None, None, None, None
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
 CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
+# a layer whose map is computed ahead with an early update (GraphTrainStep on one rank): its weight /
+# bias gradients on the layer's map stream instead of the head's side stream joined before returning
+CONV_WGRAD_MAPSTREAM = os.environ.get("FIODE_CONV_WGRAD_MAPSTREAM", "0") != "0"
+CONV_WGRAD_MAPSTREAM_BIAS = False
+_CONV_WGRAD_EVENTS: list = []
+
+
+def conv_wgrad_join(stream) -> None:
+    """Make ``stream`` wait for the conv bias gradients computed on the layers' map streams in the
+    backward that just ran (CONV_WGRAD_MAPSTREAM): call before the optimizer step reads them."""
+    while _CONV_WGRAD_EVENTS:
+        stream.wait_event(_CONV_WGRAD_EVENTS.pop())
 
 # The conv layers' map-ahead work (map backward, early update, refresh) runs on one stream per layer
 # (False) or on one stream shared by all layers (True; tools/ab_step.py conv_one_stream).
@@ -778,6 +816,7 @@ class CayleyConv(nn.Conv2d):
         self._n = None
         self._pre = None
         self._store = None              # map computed ahead (pipeline_on), else None
+        self._wstream = None            # the stream of the stored map's backward, for the next apply
 
     def _load_from_state_dict(self, *args, **kw):
         super()._load_from_state_dict(*args, **kw)
@@ -864,7 +903,11 @@ class CayleyConv(nn.Conv2d):
                 Q = _SpectralCayleyStoredFn.apply(self.weight, self.alpha, n, st)
             main.wait_stream(side)
             self._pre = None
+            # the weight gradients go to this stream only with the early update (one rank): there
+            # the stored map's backward and the update consume them on it
+            self._wstream = side if st.get("on_grads") is not None else None
             return Q
+        self._wstream = None
         if self._pre is not None and self.training and self._n == n:
             Q = _take(self._pre)
         else:
@@ -893,7 +936,8 @@ class CayleyConv(nn.Conv2d):
         (_SpectralConvFn): [n][n][cin][B] (stride 2: [2n][2n][cin/4][B]) -> [n][n][cout][B]."""
         n = x.shape[0] // 2 if self.downsample else x.shape[0]
         Q = self._take_spectral(n, x.device)
-        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort)
+        ws, self._wstream = self._wstream, None
+        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, ws)
 
     def forward_hwcb(self, x: torch.Tensor) -> torch.Tensor:
         """The same map on spatial-major activations [n, n, C, B] (the conv stack's HBM layout):

@@ -207,6 +207,25 @@ def conv_wgrad_main(m):
     RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_SIDE", True))
 
 
+def conv_wgrad_head(m):
+    from fiode_amd import cayley as CY
+    CY.CONV_WGRAD_MAPSTREAM = False   # the conv weight gradients on the head's side stream, joined (r05af)
+
+
+def conv_wgrad_map(m):
+    from fiode_amd import cayley as CY
+    CY.CONV_WGRAD_MAPSTREAM = True    # the conv weight gradients on the layers' map streams, bias on the step's
+    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM", False))
+
+
+def conv_wgrad_bias_side(m):
+    from fiode_amd import cayley as CY
+    CY.CONV_WGRAD_MAPSTREAM = True    # ... and the bias gradients on the map streams too, joined at the end
+    CY.CONV_WGRAD_MAPSTREAM_BIAS = True
+    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM_BIAS", False))
+    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM", False))
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -214,6 +233,7 @@ def dyn_wgrad_main(m):
 
 
 ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+       "conv_wgrad_head": conv_wgrad_head, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
        "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,

@@ -1,0 +1,10 @@
+#!/bin/bash
+# r05al: conv weight gradients on the layers' map streams (no join): graph tests, interleaved A/B
+set -u
+O=gpurun_out/${TAG:-r05al}; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_graph.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+for t in 1 2; do
+  FIODE_PLACEMENT_TRIALS=4 timeout -k 10 500 python -u tools/ab_step.py 10 default,conv_wgrad_map,conv_wgrad_bias_side > $O/ab_$t.json 2> $O/ab_$t.err || { tail $O/ab_$t.err; exit 1; }
+  tail -1 $O/ab_$t.json
+done
