@@ -39,6 +39,9 @@ from typing import Optional
 
 import torch
 
+# priority of the stream the step is captured on (its nodes' hardware queue; tools/ab_step.py cap_hi)
+CAPTURE_PRIORITY = 0
+
 
 
 # The HIP runtime of this image (ROCm 7.x, torch's libamdhip64) dereferences a null internal stream in
@@ -130,6 +133,8 @@ class GraphTrainStep:
 
         if maps_ahead:
             self._maps_ahead_on()
+        if CAPTURE_PRIORITY:
+            self.capture_stream = torch.cuda.Stream(dev, priority=CAPTURE_PRIORITY)
         self.comm_fallback = None
         try:
             self._capture()
@@ -212,7 +217,7 @@ class GraphTrainStep:
         for _ in range(trials - 1):
             # fresh pool streams for the maps' prefetch, the ODE solve, the conv maps computed ahead
             # and the capture itself
-            use((None, None, [torch.cuda.Stream(dev) for _ in stores], torch.cuda.Stream(dev)))
+            use((None, None, [torch.cuda.Stream(dev) for _ in stores], torch.cuda.Stream(dev, priority=CAPTURE_PRIORITY)))
             self._capture()
             trials_t.append((clock(), streams()))
         times = [t for t, _ in trials_t]

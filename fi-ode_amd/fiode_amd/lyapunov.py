@@ -703,7 +703,7 @@ class LyapunovLearning(nn.Module):
         if static_state.is_cuda and self.parallel_cayley and getattr(self, "ode_side_stream", True):
             from .cayley import _prefetch
             if getattr(self, "_ode_stream", None) is None:
-                self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
+                self._ode_stream = torch.cuda.Stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
             return _prefetch(self._ode_stream, lambda: ODETrainFn.apply(*args))
         return ODETrainFn.apply(*args)
 
@@ -720,7 +720,7 @@ class LyapunovLearning(nn.Module):
         stream = None
         if self.parallel_cayley and getattr(self, "ode_side_stream", True):
             if getattr(self, "_ode_stream", None) is None:
-                self._ode_stream = torch.cuda.Stream(static_state.device, priority=-1)
+                self._ode_stream = torch.cuda.Stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
             stream = self._ode_stream
         p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
         keys = ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")

@@ -226,6 +226,16 @@ def conv_wgrad_bias_side(m):
     RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM", False))
 
 
+def cap_hi(m):
+    from fiode_amd import graph_step as GS
+    GS.CAPTURE_PRIORITY = -1          # the step captured on a high-priority stream
+    RESTORE.append(lambda: setattr(GS, "CAPTURE_PRIORITY", 0))
+
+
+def ode_lo(m):
+    m._ode_prio = 0                   # the train_ode solve's stream at normal priority
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -233,7 +243,7 @@ def dyn_wgrad_main(m):
 
 
 ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
-       "conv_wgrad_head": conv_wgrad_head, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
+       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
        "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
