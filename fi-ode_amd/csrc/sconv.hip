@@ -27,12 +27,49 @@
 namespace {
 
 typedef float2 c32;
-// threads per workgroup: 1024, or 512 for n = 32 (a length-32 FFT keeps 64 values + temporaries
-// live: 256 registers at 2 waves per SIMD instead of 128 at 4)
-template <int N>
-constexpr int nthreads() { return N == 32 ? 512 : 1024; }
 constexpr int BT_F = 16;     // images per forward-transform workgroup
 constexpr int BT_I = 8;      // images per inverse-transform workgroup
+// threads per workgroup (compile-time; tools/gpu_r05ar.sh sweeps 64-1024): 512 for the n = 8 / 16
+// forward and inverse transforms (with 1024 half the waves idled through the FFT phases), 256 for
+// the n = 8 inverse, 512 at n = 32 (the 4-image input-layer forward: 128 threads measured 11.4 us at
+// best against 8.3, though steadier beside other kernels)
+#ifndef SCONV_NTF8
+#define SCONV_NTF8 512
+#endif
+#ifndef SCONV_NTF16
+#define SCONV_NTF16 512
+#endif
+#ifndef SCONV_NTF32
+#define SCONV_NTF32 512
+#endif
+#ifndef SCONV_NTF32S
+#define SCONV_NTF32S 512
+#endif
+#ifndef SCONV_NTI8
+#define SCONV_NTI8 256
+#endif
+#ifndef SCONV_NTI16
+#define SCONV_NTI16 512
+#endif
+#ifndef SCONV_NTI32
+#define SCONV_NTI32 512
+#endif
+// n = 32 forward transforms: 8 images per workgroup (69 KB of LDS, two workgroups per CU; 16 images
+// left one per CU: k_sconv_rfft2<32> 33.1 -> 29.4 us in the step); the inverse keeps 8 (4: no gain)
+#ifndef SCONV_BTF32
+#define SCONV_BTF32 8
+#endif
+#ifndef SCONV_BTI32
+#define SCONV_BTI32 8
+#endif
+template <int N, int BT, bool INV>
+constexpr int nthreads() {
+  return INV ? (N == 8 ? SCONV_NTI8 : N == 16 ? SCONV_NTI16 : SCONV_NTI32)
+             : (N == 8 ? SCONV_NTF8 : N == 16 ? SCONV_NTF16 : BT == 4 ? SCONV_NTF32S : SCONV_NTF32);
+}
+// images per inverse-transform workgroup
+template <int N>
+constexpr int bt_inv() { return N == 32 ? SCONV_BTI32 : BT_I; }
 
 enum : uint8_t { GS_GT = 0, GS_LT = 1, GS_EQ = 2 };
 
@@ -65,21 +102,35 @@ __device__ __forceinline__ int64_t raw_index(const SArgs& a, int h, int w, int c
   return (((int64_t)(2 * h + dh) * n2 + (2 * w + dw)) * C4 + cr) * a.B + b;
 }
 
-// LDS image strides (in elements): odd per-image strides so the BT images a wave touches at one
-// (h, w) / (h, kb) land in distinct banks (a power-of-two stride put all 16 images in 1-2 banks).
-template <int N>
+// LDS image strides (in elements) per kernel: the per-image padding that puts the lanes of every
+// LDS instruction of that kernel in distinct banks as far as the gfx950 lane groups allow
+// (tools/probes/sconv_lds_banks.py models each instruction's lane -> address map: e.g. k_sconv_irfft2<16>
+// 824 -> 432 LDS cycles per workgroup against 428 conflict-free; the plain odd strides N (N+1) + 1 /
+// N (N/2+1) + 1 left 30-70 % of the LDS cycles to conflicts in PMC).  INV: k_sconv_irfft2.
+constexpr int pad_is(int n, int bt, bool inv) {
+  return inv ? (n == 8 ? 76 : n == 16 ? 276 : (bt == 4 ? 1064 : 1060))
+             : n == 8 ? (bt == 4 ? 72 : 74) : n == 16 ? (bt == 4 ? 280 : 274)
+                                                      : (bt == 4 ? 1064 : bt == 8 ? 1060 : 1058);
+}
+constexpr int pad_zs(int n, int bt, bool inv) {
+  return inv ? (n == 8 ? 42 : n == 16 ? 146 : (bt == 4 ? 548 : 546))
+             : n == 8 ? (bt == 4 ? 44 : 41) : n == 16 ? (bt == 4 ? 148 : 145)
+                                                      : (bt == 4 ? 548 : bt == 8 ? 546 : 545);
+}
+template <int N, int BT, bool INV>
 struct Geo {
   static constexpr int H = N / 2 + 1;
-  static constexpr int RS = N + 1;              // real row stride
-  static constexpr int IS = N * RS + 1;         // real image stride (odd)
-  static constexpr int ZS = N * H + 1;          // complex image stride (odd, in float2)
+  static constexpr int RS = N + 1;                  // real row stride
+  static constexpr int IS = pad_is(N, BT, INV);     // real image stride
+  static constexpr int ZS = pad_zs(N, BT, INV);     // complex image stride (in float2)
+  static_assert(IS >= N * RS && ZS >= N * H, "image strides");
 };
 
 // ---- X[f][c][b0..b0+BT) = rfft2 of channel c ------------------------------------------------------
 template <int N, int BT>
-__global__ void __launch_bounds__(nthreads<N>()) k_sconv_rfft2(SArgs a) {
-  constexpr int NT = nthreads<N>();
-  typedef Geo<N> g;
+__global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArgs a) {
+  constexpr int NT = nthreads<N, BT, false>();
+  typedef Geo<N, BT, false> g;
   __shared__ float img[BT * g::IS];
   __shared__ c32 Z[BT * g::ZS];
   constexpr int H = g::H;
@@ -146,24 +197,25 @@ __global__ void __launch_bounds__(nthreads<N>()) k_sconv_rfft2(SArgs a) {
   }
 }
 
-// irfft2 of one channel of BT_I images into out (LDS, real image stride Geo<N>::IS)
+// irfft2 of one channel of BTI images into out (LDS, real image stride Geo<N, BTI, true>::IS)
 template <int N>
 __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c32* Ys, c32* Zs, float* out) {
-  constexpr int NT = nthreads<N>();
-  typedef Geo<N> g;
+  constexpr int BTI = bt_inv<N>();
+  constexpr int NT = nthreads<N, BTI, true>();
+  typedef Geo<N, BTI, true> g;
   constexpr int H = g::H;
   const int tid = threadIdx.x;
 #pragma unroll 16
-  for (int idx = tid; idx < BT_I * N * H; idx += NT) {
-    const int bt = idx % BT_I, f = idx / BT_I;
+  for (int idx = tid; idx < BTI * N * H; idx += NT) {
+    const int bt = idx % BTI, f = idx / BTI;
     const int b = min(b0 + bt, a.B - 1);
     const c32 v = a.Y[((int64_t)f * a.C + c) * a.B + b];
     Ys[bt * g::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
   }
   __syncthreads();
   // inverse c2c along ka: one (image, kb) column per thread (in-register FFT, fft.h)
-  for (int col = tid; col < BT_I * H; col += NT) {
-    const int bt = col % BT_I, kb = col / BT_I;
+  for (int col = tid; col < BTI * H; col += NT) {
+    const int bt = col % BTI, kb = col / BTI;
     c32 x[N];
 #pragma unroll
     for (int ka = 0; ka < N; ++ka) x[ka] = Ys[bt * g::ZS + ka * H + kb];
@@ -176,8 +228,8 @@ __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c3
   // (imaginary parts of X[0], X[N/2] ignored, as torch's irfft does), inverse FFT, real part, 1/n^2
   constexpr float inv = 1.0f / (float)(N * N);
   constexpr int nh = N / 2;
-  for (int row = tid; row < BT_I * N; row += NT) {
-    const int bt = row % BT_I, h = row / BT_I;
+  for (int row = tid; row < BTI * N; row += NT) {
+    const int bt = row % BTI, h = row / BTI;
     const c32* src = Zs + bt * g::ZS + h * H;
     c32 x[N];
     x[0] = make_float2(src[0].x, 0.f);
@@ -198,21 +250,22 @@ __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c3
 // ---- y = irfft2(Y) (+ bias, GroupSort) or the space-to-channel scatter ---------------------------
 // gs: grid.x = C/2 channel pairs; else grid.x = C channels.
 template <int N>
-__global__ void __launch_bounds__(nthreads<N>()) k_sconv_irfft2(SArgs a) {
-  constexpr int NT = nthreads<N>();
-  typedef Geo<N> g;
-  __shared__ c32 Ys[BT_I * g::ZS];
-  __shared__ c32 Zs[BT_I * g::ZS];
-  __shared__ float o0[BT_I * g::IS];
-  __shared__ float o1[BT_I * g::IS];
-  const int b0 = blockIdx.y * BT_I, tid = threadIdx.x;
+__global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_irfft2(SArgs a) {
+  constexpr int BTI = bt_inv<N>();
+  constexpr int NT = nthreads<N, BTI, true>();
+  typedef Geo<N, BTI, true> g;
+  __shared__ c32 Ys[BTI * g::ZS];
+  __shared__ c32 Zs[BTI * g::ZS];
+  __shared__ float o0[BTI * g::IS];
+  __shared__ float o1[BTI * g::IS];
+  const int b0 = blockIdx.y * BTI, tid = threadIdx.x;
   if (a.gs) {
     const int half = a.C >> 1, c0 = blockIdx.x, c1 = c0 + half;
     irfft2_channel<N>(a, c0, b0, Ys, Zs, o0);
     irfft2_channel<N>(a, c1, b0, Ys, Zs, o1);
     const float bb0 = a.bias ? a.bias[c0] : 0.f, bb1 = a.bias ? a.bias[c1] : 0.f;
-    for (int idx = tid; idx < BT_I * N * N; idx += NT) {
-      const int bt = idx % BT_I, hw = idx / BT_I, h = hw / N, w = hw % N;
+    for (int idx = tid; idx < BTI * N * N; idx += NT) {
+      const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
       const int li = bt * g::IS + h * g::RS + w;
@@ -225,8 +278,8 @@ __global__ void __launch_bounds__(nthreads<N>()) k_sconv_irfft2(SArgs a) {
     const int c = blockIdx.x;
     irfft2_channel<N>(a, c, b0, Ys, Zs, o0);
     const float bb = a.bias ? a.bias[c] : 0.f;
-    for (int idx = tid; idx < BT_I * N * N; idx += NT) {
-      const int bt = idx % BT_I, hw = idx / BT_I, h = hw / N, w = hw % N;
+    for (int idx = tid; idx < BTI * N * N; idx += NT) {
+      const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
       const float v = o0[bt * g::IS + h * g::RS + w] + bb;
@@ -264,17 +317,17 @@ extern "C" int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, co
   hipStream_t st = (hipStream_t)stream;
   // few channels (the 3-channel input of conv 1): 4 images per workgroup to spread over the CUs
   const bool small = (int64_t)a.C * ((a.B + BT_F - 1) / BT_F) < 256;
-  const int bt = small ? 4 : BT_F;
+  const int bt = small ? 4 : a.n == 32 ? SCONV_BTF32 : BT_F;
   const dim3 grid(a.C, (a.B + bt - 1) / bt);
   if (a.n == 8) {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8>()), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8>()), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8, BT_F, false>()), 0, st, a);
   } else if (a.n == 16) {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(nthreads<16>()), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(nthreads<16>()), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(nthreads<16, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(nthreads<16, BT_F, false>()), 0, st, a);
   } else {
-    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(nthreads<32>()), 0, st, a);
-    else hipLaunchKernelGGL((k_sconv_rfft2<32, BT_F>), grid, dim3(nthreads<32>()), 0, st, a);
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(nthreads<32, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<32, SCONV_BTF32>), grid, dim3(nthreads<32, SCONV_BTF32, false>()), 0, st, a);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
@@ -292,11 +345,12 @@ extern "C" int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, c
   a.y = y;
   a.code_out = code_out;
   const int gx = a.gs ? a.C / 2 : a.C;
-  const dim3 grid(gx, (a.B + BT_I - 1) / BT_I);
+  const int bt = a.n == 32 ? bt_inv<32>() : BT_I;
+  const dim3 grid(gx, (a.B + bt - 1) / bt);
   hipStream_t st = (hipStream_t)stream;
-  if (a.n == 8) hipLaunchKernelGGL(k_sconv_irfft2<8>, grid, dim3(nthreads<8>()), 0, st, a);
-  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_irfft2<16>, grid, dim3(nthreads<16>()), 0, st, a);
-  else hipLaunchKernelGGL(k_sconv_irfft2<32>, grid, dim3(nthreads<32>()), 0, st, a);
+  if (a.n == 8) hipLaunchKernelGGL(k_sconv_irfft2<8>, grid, dim3(nthreads<8, BT_I, true>()), 0, st, a);
+  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_irfft2<16>, grid, dim3(nthreads<16, BT_I, true>()), 0, st, a);
+  else hipLaunchKernelGGL(k_sconv_irfft2<32>, grid, dim3(nthreads<32, bt_inv<32>(), true>()), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
