@@ -197,40 +197,65 @@ __global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArg
   }
 }
 
-// irfft2 of one channel of BTI images into out (LDS, real image stride Geo<N, BTI, true>::IS)
+// irfft2 of the workgroup's NCH channels x BTI images in place in Ys (one complex image per
+// (channel, image), row stride H, channel stride BTI ZS): every channel's spectra are loaded at once,
+// then the column transforms (inverse c2c along ka) of all channels, then the rows (c2r along kb; the
+// row's N real outputs written over its own 2H floats).  Pixel (h, w) of image bt of channel ch ends
+// at float offset pix(ch, bt, h) + w.  (Round 4 ran the two channels of a GroupSort pair one after
+// the other through separate column / row / output buffers: 137 KB of LDS at n = 32, one workgroup
+// per CU, two load latencies per workgroup.)
 template <int N>
-__device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c32* Ys, c32* Zs, float* out) {
-  constexpr int BTI = bt_inv<N>();
-  constexpr int NT = nthreads<N, BTI, true>();
-  typedef Geo<N, BTI, true> g;
-  constexpr int H = g::H;
+struct IGeo {
+  typedef Geo<N, bt_inv<N>(), true> g;
+  static constexpr int BTI = bt_inv<N>();
+  static constexpr int H = g::H;
+  static constexpr int ZS = g::ZS;
+  static constexpr int CS = BTI * ZS;      // channel stride (float2)
+  static constexpr int NT = nthreads<N, BTI, true>();
+  __device__ static int pix(int ch, int bt, int h) { return 2 * (ch * CS + bt * ZS + h * H); }
+};
+
+template <int N, int NCH>
+__device__ __forceinline__ void irfft2_inplace(const SArgs& a, int c0, int c1, int b0, c32* Ys) {
+  typedef IGeo<N> G;
+  constexpr int BTI = G::BTI, H = G::H, NT = G::NT;
+  constexpr int NL = NCH * BTI * N * H;
+  constexpr int TR = (NL + NT - 1) / NT;
   const int tid = threadIdx.x;
-#pragma unroll 16
-  for (int idx = tid; idx < BTI * N * H; idx += NT) {
-    const int bt = idx % BTI, f = idx / BTI;
-    const int b = min(b0 + bt, a.B - 1);
-    const c32 v = a.Y[((int64_t)f * a.C + c) * a.B + b];
-    Ys[bt * g::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
+  // all loads in flight together: a fixed trip count, unrolled
+#pragma unroll
+  for (int t = 0; t < TR; ++t) {
+    const int idx = tid + t * NT;
+    if (idx < NL) {
+      const int ch = idx / (BTI * N * H), r = idx - ch * (BTI * N * H);
+      const int bt = r % BTI, f = r / BTI;
+      const int b = min(b0 + bt, a.B - 1);
+      const c32 v = a.Y[((int64_t)f * a.C + (ch ? c1 : c0)) * a.B + b];
+      Ys[ch * G::CS + bt * G::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
+    }
   }
   __syncthreads();
-  // inverse c2c along ka: one (image, kb) column per thread (in-register FFT, fft.h)
-  for (int col = tid; col < BTI * H; col += NT) {
-    const int bt = col % BTI, kb = col / BTI;
+  // inverse c2c along ka: one (channel, image, kb) column per thread, in place
+  for (int col = tid; col < NCH * BTI * H; col += NT) {
+    const int ch = col / (BTI * H), r = col - ch * (BTI * H);
+    const int bt = r % BTI, kb = r / BTI;
+    c32* cp = Ys + ch * G::CS + bt * G::ZS + kb;
     c32 x[N];
 #pragma unroll
-    for (int ka = 0; ka < N; ++ka) x[ka] = Ys[bt * g::ZS + ka * H + kb];
+    for (int ka = 0; ka < N; ++ka) x[ka] = cp[ka * H];
     fiode_fft::fft_reg<N, true>(x);
 #pragma unroll
-    for (int h = 0; h < N; ++h) Zs[bt * g::ZS + h * H + kb] = x[h];
+    for (int h = 0; h < N; ++h) cp[h * H] = x[h];
   }
   __syncthreads();
-  // c2r along kb: one (image, h) row per thread: the Hermitian completion X[N - k] = conj X[k]
+  // c2r along kb: one (channel, image, h) row per thread: the Hermitian completion X[N - k] = conj X[k]
   // (imaginary parts of X[0], X[N/2] ignored, as torch's irfft does), inverse FFT, real part, 1/n^2
   constexpr float inv = 1.0f / (float)(N * N);
   constexpr int nh = N / 2;
-  for (int row = tid; row < BTI * N; row += NT) {
-    const int bt = row % BTI, h = row / BTI;
-    const c32* src = Zs + bt * g::ZS + h * H;
+  for (int row = tid; row < NCH * BTI * N; row += NT) {
+    const int ch = row / (BTI * N), r = row - ch * (BTI * N);
+    const int bt = r % BTI, h = r / BTI;
+    const c32* src = Ys + ch * G::CS + bt * G::ZS + h * H;
     c32 x[N];
     x[0] = make_float2(src[0].x, 0.f);
     x[nh] = make_float2(src[nh].x, 0.f);
@@ -241,48 +266,44 @@ __device__ __forceinline__ void irfft2_channel(const SArgs& a, int c, int b0, c3
       x[N - kb] = make_float2(v.x, -v.y);
     }
     fiode_fft::fft_reg<N, true>(x);
+    float* dst = reinterpret_cast<float*>(Ys) + G::pix(ch, bt, h);
 #pragma unroll
-    for (int w = 0; w < N; ++w) out[bt * g::IS + h * g::RS + w] = x[w].x * inv;
+    for (int w = 0; w < N; ++w) dst[w] = x[w].x * inv;
   }
   __syncthreads();
 }
 
 // ---- y = irfft2(Y) (+ bias, GroupSort) or the space-to-channel scatter ---------------------------
-// gs: grid.x = C/2 channel pairs; else grid.x = C channels.
+// gs: grid.x = C/2 channel pairs (both channels of a pair in one workgroup); else grid.x = C channels.
 template <int N>
 __global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_irfft2(SArgs a) {
-  constexpr int BTI = bt_inv<N>();
-  constexpr int NT = nthreads<N, BTI, true>();
-  typedef Geo<N, BTI, true> g;
-  __shared__ c32 Ys[BTI * g::ZS];
-  __shared__ c32 Zs[BTI * g::ZS];
-  __shared__ float o0[BTI * g::IS];
-  __shared__ float o1[BTI * g::IS];
+  typedef IGeo<N> G;
+  constexpr int BTI = G::BTI, NT = G::NT;
+  __shared__ c32 Ys[2 * G::CS];
+  const float* o = reinterpret_cast<const float*>(Ys);
   const int b0 = blockIdx.y * BTI, tid = threadIdx.x;
   if (a.gs) {
     const int half = a.C >> 1, c0 = blockIdx.x, c1 = c0 + half;
-    irfft2_channel<N>(a, c0, b0, Ys, Zs, o0);
-    irfft2_channel<N>(a, c1, b0, Ys, Zs, o1);
+    irfft2_inplace<N, 2>(a, c0, c1, b0, Ys);
     const float bb0 = a.bias ? a.bias[c0] : 0.f, bb1 = a.bias ? a.bias[c1] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
       const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
-      const int li = bt * g::IS + h * g::RS + w;
-      const float p = o0[li] + bb0, q = o1[li] + bb1;
+      const float p = o[G::pix(0, bt, h) + w] + bb0, q = o[G::pix(1, bt, h) + w] + bb1;
       a.y[act_index(a, h, w, c0, b)] = fmaxf(p, q);
       a.y[act_index(a, h, w, c1, b)] = fminf(p, q);
       a.code_out[(((int64_t)h * N + w) * half + c0) * a.B + b] = p > q ? GS_GT : (p < q ? GS_LT : GS_EQ);
     }
   } else {
     const int c = blockIdx.x;
-    irfft2_channel<N>(a, c, b0, Ys, Zs, o0);
+    irfft2_inplace<N, 1>(a, c, c, b0, Ys);
     const float bb = a.bias ? a.bias[c] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
       const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
-      const float v = o0[bt * g::IS + h * g::RS + w] + bb;
+      const float v = o[G::pix(0, bt, h) + w] + bb;
       if (a.ds) a.y[raw_index(a, h, w, c, b)] = v;
       else a.y[act_index(a, h, w, c, b)] = v;
     }

@@ -114,3 +114,49 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def irfft_inplace_cost(N, ZS, NCH=2, BT=8, NT=512):
+    """k_sconv_irfft2 since r05: both channels in place in one complex buffer (channel stride BT ZS)."""
+    H = N // 2 + 1
+    CS = BT * ZS
+    c = i = 0
+    NL = NCH * BT * N * H
+
+    def ys(x):      # load: ch, bt, f
+        ch, r = divmod(x, BT * N * H)
+        return 2 * (ch * CS + (r % BT) * ZS + r // BT)
+    for ad in wave_instrs(NT, NL, ys):
+        c += cycles("w64", ad); i += 4
+
+    def col(x, k):
+        ch, r = divmod(x, BT * H)
+        return 2 * (ch * CS + (r % BT) * ZS + k * H + r // BT)
+    for k in range(N):
+        for kind in ("r64", "w64"):
+            for ad in wave_instrs(NT, NCH * BT * H, lambda x, k=k: col(x, k)):
+                c += cycles(kind, ad); i += 2 if kind == "r64" else 4
+
+    def row(x):
+        ch, r = divmod(x, BT * N)
+        return 2 * (ch * CS + (r % BT) * ZS + (r // BT) * H)
+    for kb in range(N // 2 + 1):
+        for ad in wave_instrs(NT, NCH * BT * N, lambda x, kb=kb: row(x) + 2 * kb):
+            c += cycles("r64", ad); i += 2
+    for w in range(N):
+        for ad in wave_instrs(NT, NCH * BT * N, lambda x, w=w: row(x) + w):
+            c += cycles("w32", ad); i += 2
+    # epilogue: each channel's pixel (bt, h, w), idx -> bt fastest
+    for ch in range(NCH):
+        for ad in wave_instrs(NT, BT * N * N, lambda x, ch=ch: 2 * (ch * CS + (x % BT) * ZS + (x // BT // N) * H) + (x // BT) % N):
+            c += cycles("r32", ad); i += 2
+    return c, i
+
+
+def search_inplace():
+    for N, NT in ((8, 256), (16, 512), (32, 512)):
+        H = N // 2 + 1
+        for nch in (2, 1):
+            res = sorted((irfft_inplace_cost(N, zs, nch, 8, NT)[0], zs) for zs in range(N * H, N * H + 33))
+            print(f"irfft2 in place N={N} NCH={nch}: ideal {irfft_inplace_cost(N, N * H + 1, nch, 8, NT)[1]}, "
+                  f"best {res[:4]}, ZS={N * H + 1}: {irfft_inplace_cost(N, N * H + 1, nch, 8, NT)[0]}", flush=True)
