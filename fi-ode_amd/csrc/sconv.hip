@@ -127,74 +127,119 @@ struct Geo {
 };
 
 // ---- X[f][c][b0..b0+BT) = rfft2 of channel c ------------------------------------------------------
+// One complex buffer per channel, [bt][h][kb] (row stride H, image stride ZS, channel stride BT ZS):
+// the real input is stored in place (pixel (h, w) of image bt at float offset pix(ch, bt, h) + w,
+// the row's first N of its 2H floats), the row transforms (r2c) overwrite their own rows, the column
+// transforms (c2c) go to X.  The GroupSort backward prologue takes both channels of a pair in one
+// workgroup: d/dmax, d/dmin and the codes are read once for both (round 4: a workgroup per channel
+// read the pair's d/dout twice, through a separate real image buffer).
 template <int N, int BT>
-__global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArgs a) {
-  constexpr int NT = nthreads<N, BT, false>();
+struct FGeo {
   typedef Geo<N, BT, false> g;
-  __shared__ float img[BT * g::IS];
-  __shared__ c32 Z[BT * g::ZS];
-  constexpr int H = g::H;
-  constexpr int NL = BT * N * N;
-  const int c = blockIdx.x, b0 = blockIdx.y * BT, tid = threadIdx.x;
-  const int half = a.C >> 1;
-  // the loads of many loop trips must be in flight together (a trip-by-trip loop waits ~1 us per
-  // trip on the memory latency): fixed trip counts, unrolled, one loop per source mode
-  if (a.gy) {                                      // GroupSort backward: d/dpre of channel c
-    const bool first = c < half;
-    const int cp = first ? c + half : c - half, cmx = first ? c : cp, cmn = first ? cp : c;
-#pragma unroll 16
-    for (int idx = tid; idx < NL; idx += NT) {
-      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
-      const int b = min(b0 + bt, a.B - 1);
-      const uint8_t code = a.code[(((int64_t)h * N + w) * half + cmx) * a.B + b];
-      const float gmx = a.gy[act_index(a, h, w, cmx, b)], gmn = a.gy[act_index(a, h, w, cmn, b)];
-      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? gs_grad(gmx, gmn, code, first) : 0.f;
-    }
-  } else if (a.ds) {
-#pragma unroll 16
-    for (int idx = tid; idx < NL; idx += NT) {
-      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
-      const int b = min(b0 + bt, a.B - 1);
-      const float v = a.x[raw_index(a, h, w, c, b)];
-      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? v : 0.f;
-    }
-  } else {
-#pragma unroll 16
-    for (int idx = tid; idx < NL; idx += NT) {
-      const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
-      const int b = min(b0 + bt, a.B - 1);
-      const float v = a.x[act_index(a, h, w, c, b)];
-      img[bt * g::IS + h * g::RS + w] = b0 + bt < a.B ? v : 0.f;
-    }
-  }
-  __syncthreads();
+  static constexpr int H = g::H;
+  static constexpr int ZS = g::ZS;
+  static constexpr int CS = BT * ZS;       // channel stride (float2)
+  static constexpr int NT = nthreads<N, BT, false>();
+  __device__ static int pix(int ch, int bt, int h) { return 2 * (ch * CS + bt * ZS + h * H); }
+};
+
+template <int N, int BT, int NCH>
+__device__ __forceinline__ void rfft2_inplace(const SArgs& a, int c0, int c1, int b0, c32* Z) {
+  typedef FGeo<N, BT> G;
+  constexpr int H = G::H, NT = G::NT;
+  const float* img = reinterpret_cast<const float*>(Z);
+  const int tid = threadIdx.x;
   // The two 1-D transforms as one length-N FFT per thread in registers (rows, then columns;
   // fft.h): a direct DFT here (N^2 complex MACs per transform) left the workgroups VALU-bound.
-  // r2c along w: one (image, h) row per thread (imaginary part 0, the N/2 + 1 kept outputs)
-  for (int row = tid; row < BT * N; row += NT) {
-    const int bt = row % BT, h = row / BT;
-    const float* src = img + bt * g::IS + h * g::RS;
+  // r2c along w: one (channel, image, h) row per thread (imaginary part 0, the N/2 + 1 kept
+  // outputs written over the row's own floats)
+  for (int row = tid; row < NCH * BT * N; row += NT) {
+    const int ch = row / (BT * N), r = row - ch * (BT * N);
+    const int bt = r % BT, h = r / BT;
+    const float* src = img + G::pix(ch, bt, h);
     c32 x[N];
 #pragma unroll
     for (int w = 0; w < N; ++w) x[w] = make_float2(src[w], 0.f);
     fiode_fft::fft_reg<N, false>(x);
+    c32* dst = Z + ch * G::CS + bt * G::ZS + h * H;
 #pragma unroll
-    for (int kb = 0; kb < H; ++kb) Z[bt * g::ZS + h * H + kb] = x[kb];
+    for (int kb = 0; kb < H; ++kb) dst[kb] = x[kb];
   }
   __syncthreads();
-  // c2c along h: one (image, kb) column per thread, written as X[f][c][b]
-  for (int col = tid; col < BT * H; col += NT) {
-    const int bt = col % BT, kb = col / BT;
+  // c2c along h: one (channel, image, kb) column per thread, written as X[f][c][b]
+  for (int col = tid; col < NCH * BT * H; col += NT) {
+    const int ch = col / (BT * H), r = col - ch * (BT * H);
+    const int bt = r % BT, kb = r / BT;
+    const c32* cp = Z + ch * G::CS + bt * G::ZS + kb;
     c32 x[N];
 #pragma unroll
-    for (int h = 0; h < N; ++h) x[h] = Z[bt * g::ZS + h * H + kb];
+    for (int h = 0; h < N; ++h) x[h] = cp[h * H];
     fiode_fft::fft_reg<N, false>(x);
-    const int b = b0 + bt;
+    const int b = b0 + bt, c = ch ? c1 : c0;
     if (b < a.B) {
 #pragma unroll
       for (int ka = 0; ka < N; ++ka) a.X[((int64_t)(ka * H + kb) * a.C + c) * a.B + b] = x[ka];
     }
   }
+}
+
+// gy (GroupSort backward): grid.x = C/2 channel pairs; else grid.x = C channels
+template <int N, int BT>
+__global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArgs a) {
+  typedef FGeo<N, BT> G;
+  constexpr int NT = G::NT;
+  constexpr int NL = BT * N * N;
+  constexpr int TR = (NL + NT - 1) / NT;
+  __shared__ c32 Z[2 * G::CS];
+  float* img = reinterpret_cast<float*>(Z);
+  const int b0 = blockIdx.y * BT, tid = threadIdx.x;
+  // the loads of all trips in flight together (a trip-by-trip loop waits ~1 us per trip on the
+  // memory latency): a fixed trip count, unrolled, one loop per source mode
+  if (a.gy) {                                      // GroupSort backward: d/dpre of both channels
+    const int half = a.C >> 1, c0 = blockIdx.x, c1 = c0 + half;
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL) {
+        const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+        const int b = min(b0 + bt, a.B - 1);
+        const uint8_t code = a.code[(((int64_t)h * N + w) * half + c0) * a.B + b];
+        const float gmx = a.gy[act_index(a, h, w, c0, b)], gmn = a.gy[act_index(a, h, w, c1, b)];
+        const bool in = b0 + bt < a.B;
+        img[G::pix(0, bt, h) + w] = in ? gs_grad(gmx, gmn, code, true) : 0.f;
+        img[G::pix(1, bt, h) + w] = in ? gs_grad(gmx, gmn, code, false) : 0.f;
+      }
+    }
+    __syncthreads();
+    rfft2_inplace<N, BT, 2>(a, c0, c1, b0, Z);
+    return;
+  }
+  const int c = blockIdx.x;
+  if (a.ds) {
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL) {
+        const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+        const int b = min(b0 + bt, a.B - 1);
+        const float v = a.x[raw_index(a, h, w, c, b)];
+        img[G::pix(0, bt, h) + w] = b0 + bt < a.B ? v : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL) {
+        const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+        const int b = min(b0 + bt, a.B - 1);
+        const float v = a.x[act_index(a, h, w, c, b)];
+        img[G::pix(0, bt, h) + w] = b0 + bt < a.B ? v : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  rfft2_inplace<N, BT, 1>(a, c, c, b0, Z);
 }
 
 // irfft2 of the workgroup's NCH channels x BTI images in place in Ys (one complex image per
@@ -339,7 +384,7 @@ extern "C" int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, co
   // few channels (the 3-channel input of conv 1): 4 images per workgroup to spread over the CUs
   const bool small = (int64_t)a.C * ((a.B + BT_F - 1) / BT_F) < 256;
   const int bt = small ? 4 : a.n == 32 ? SCONV_BTF32 : BT_F;
-  const dim3 grid(a.C, (a.B + bt - 1) / bt);
+  const dim3 grid(gy ? a.C / 2 : a.C, (a.B + bt - 1) / bt);
   if (a.n == 8) {
     if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8, 4, false>()), 0, st, a);
     else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8, BT_F, false>()), 0, st, a);

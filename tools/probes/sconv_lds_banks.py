@@ -160,3 +160,43 @@ def search_inplace():
             res = sorted((irfft_inplace_cost(N, zs, nch, 8, NT)[0], zs) for zs in range(N * H, N * H + 33))
             print(f"irfft2 in place N={N} NCH={nch}: ideal {irfft_inplace_cost(N, N * H + 1, nch, 8, NT)[1]}, "
                   f"best {res[:4]}, ZS={N * H + 1}: {irfft_inplace_cost(N, N * H + 1, nch, 8, NT)[0]}", flush=True)
+
+
+def rfft_inplace_cost(N, BT, ZS, NCH, NT):
+    """k_sconv_rfft2 since r05: real input in place in the complex buffer (row stride 2H floats)."""
+    H = N // 2 + 1
+    CS = BT * ZS
+    c = i = 0
+
+    def pix(ch, bt, h):
+        return 2 * (ch * CS + bt * ZS + h * H)
+    for ch in range(NCH):
+        for ad in wave_instrs(NT, BT * N * N, lambda x, ch=ch: pix(ch, x % BT, x // BT // N) + (x // BT) % N):
+            c += cycles("w32", ad); i += 2
+
+    def row(x):
+        ch, r = divmod(x, BT * N)
+        return pix(ch, r % BT, r // BT)
+    for w in range(N):
+        for ad in wave_instrs(NT, NCH * BT * N, lambda x, w=w: row(x) + w):
+            c += cycles("r32", ad); i += 2
+    for kb in range(H):
+        for ad in wave_instrs(NT, NCH * BT * N, lambda x, kb=kb: row(x) + 2 * kb):
+            c += cycles("w64", ad); i += 4
+
+    def col(x, h):
+        ch, r = divmod(x, BT * H)
+        return 2 * (ch * CS + (r % BT) * ZS + h * H + r // BT)
+    for h in range(N):
+        for ad in wave_instrs(NT, NCH * BT * H, lambda x, h=h: col(x, h)):
+            c += cycles("r64", ad); i += 2
+    return c, i
+
+
+def search_rfft_inplace():
+    for N, BT, NCH, NT in ((8, 16, 1, 512), (8, 16, 2, 512), (16, 16, 1, 512), (16, 16, 2, 512),
+                           (32, 8, 2, 512), (32, 4, 1, 512), (8, 4, 1, 512), (16, 4, 1, 512)):
+        H = N // 2 + 1
+        res = sorted((rfft_inplace_cost(N, BT, zs, NCH, NT)[0], zs) for zs in range(N * H, N * H + 33))
+        print(f"rfft2 in place N={N} BT={BT} NCH={NCH}: ideal {rfft_inplace_cost(N, BT, N * H + 1, NCH, NT)[1]}, "
+              f"best {res[:4]}", flush=True)
