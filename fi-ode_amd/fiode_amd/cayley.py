@@ -690,7 +690,9 @@ class _SpectralConvFn(torch.autograd.Function):
         B = x.shape[-1]
         nf, cout, cin = Q.shape
         X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
-        Y = torch.matmul(Q.detach(), X)
+        # (the library's solution stays faster for a 32-row product over K >= 128: conv 2, 11.6 vs 15 us)
+        own = SCONV_CGEMM and not (cout <= 32 and cin >= 128)
+        Y = ops.cgemm(Q.detach(), X) if own else torch.matmul(Q.detach(), X)
         y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort)
         ctx.save_for_backward(X, Q, code)
         ctx.cfg = (n, downsample, groupsort, bias is not None, cin, cout, B)
@@ -744,7 +746,7 @@ class _SpectralConvFn(torch.autograd.Function):
             if need_b and not CONV_WGRAD_MAPSTREAM_BIAS:
                 gb = G[0].real.sum(-1)
             if need_x:
-                gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
+                gx, _ = ops.sconv_irfft2(_q_h_g(Q, G), n, cin, B, downsample=downsample)
             return gx, gQ, gb, None, None, None, None
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
         # critical chain), on the side stream of the linear head's, joined before returning
@@ -757,7 +759,7 @@ class _SpectralConvFn(torch.autograd.Function):
             G.record_stream(side)
             X.record_stream(side)
         if need_x:
-            gx, _ = ops.sconv_irfft2(torch.matmul(Q.detach().mH, G), n, cin, B, downsample=downsample)
+            gx, _ = ops.sconv_irfft2(_q_h_g(Q, G), n, cin, B, downsample=downsample)
         if side is not None:
             cur.wait_stream(side)
             for t in (gQ, gb):
@@ -769,6 +771,17 @@ class _SpectralConvFn(torch.autograd.Function):
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
+# the per-frequency channel products Q X and Q^H G by fiode_cgemm (cgemm.hip) instead of torch.matmul
+# (the library's batched complex GEMM: one 128 x 64 tile per frequency; the n = 8 layer's forward
+# 41 -> 16 us, its input gradient 17 -> 16, conv 3's 16 -> 10, conv 1's forward 13 -> 10 us; step
+# -25 to -40 us in the alternating A/B, profiles/r05bd)
+SCONV_CGEMM = os.environ.get("FIODE_SCONV_CGEMM", "1") != "0"
+
+
+def _q_h_g(Q, G):
+    from . import ops
+    return ops.cgemm(Q.detach(), G, conj_trans_a=True) if SCONV_CGEMM else torch.matmul(Q.detach().mH, G)
+
 CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
 # a layer whose map is computed ahead with an early update (GraphTrainStep on one rank): its weight /
 # bias gradients on the layer's map stream instead of the head's side stream joined before returning

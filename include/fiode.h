@@ -415,6 +415,13 @@ FIODE_API int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, con
 FIODE_API int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,
                                  int32_t groupsort, float* y, uint8_t* code_out);
 
+/* Batched complex64 GEMM of the spectral convolutions' per-frequency channel products (CayleyConv
+ * forward_hwcb; replaces torch.matmul on complex64 in fiode_amd/cayley.py _SpectralConvFn):
+ * C[f] = opA(A[f]) B[f] for f < F, B [F][K][N], C [F][M][N] (row-major, contiguous);
+ * conj_trans_a == 0: A [F][M][K], opA = A; else A [F][K][M], opA = conj(A)^T (dL/dX = Q^H G). */
+FIODE_API int fiode_cgemm(void* stream, int32_t F, int32_t M, int32_t N, int32_t K, int32_t conj_trans_a,
+                          const void* A, const void* B, void* C);
+
 /* ---- spectral Cayley map of an orthogonal convolution (CayleyConv; libs/ortho_conv, absent:
  * restated in fiode_amd/cayley.py).  Replaces CayleyConv.spectral_weight + cayley_scaled
  * (rfft2 of the taps, shift, conj, ||.||, the per-frequency Cayley map) and its autograd. */

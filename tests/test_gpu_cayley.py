@@ -353,6 +353,31 @@ def test_spectral_conv_fused_matches_torch_fft(case):
         assert float((d - r).abs().max()) <= 2e-4 * (float(r.abs().max()) + 1e-6), name
 
 
+# (F, M, N, K, conj_trans_a): the four KWLarge layers' forward products, the three input-gradient
+# products, and ragged / tiny shapes (partial tiles, K not a multiple of 4, K = 0)
+CGEMM_CASES = [(544, 32, 128, 3, False), (144, 32, 128, 128, False), (144, 64, 128, 32, False),
+               (40, 64, 128, 256, False), (144, 128, 128, 32, True), (144, 32, 128, 64, True),
+               (40, 256, 128, 64, True), (3, 33, 7, 70, False), (5, 17, 40, 5, True), (1, 1, 1, 1, False),
+               (2, 8, 4, 0, False)]
+
+
+@pytest.mark.parametrize("case", CGEMM_CASES)
+def test_cgemm_matches_complex128(case):
+    """fiode_cgemm (cgemm.hip, the spectral convs' per-frequency products) vs torch.matmul in
+    complex128: C[f] = A[f] B[f] or A[f]^H B[f]."""
+    from fiode_amd import ops
+    F, M, N, K, ca = case
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(F * 131 + M * 7 + K)
+    A = torch.randn((F, K, M) if ca else (F, M, K), dtype=torch.complex64, generator=g)
+    B = torch.randn((F, K, N), dtype=torch.complex64, generator=g)
+    C = ops.cgemm(A.to(dev), B.to(dev), conj_trans_a=ca).cpu()
+    ref = (A.cdouble().mH if ca else A.cdouble()) @ B.cdouble()
+    assert C.shape == (F, M, N)
+    err = float((C.cdouble() - ref).abs().max()) if C.numel() else 0.0
+    assert err <= 2e-6 * (K + 1) ** 0.5 * 4, err
+
+
 def test_sconv_rejects_bad_shapes():
     from fiode_amd import ops
     from fiode_amd._lib import FiodeError
