@@ -11,7 +11,9 @@
 // K in chunks of 32 staged through LDS, with the global loads two chunks ahead in registers.  LDS row strides: A 34 complex (lanes i = 0..15 at k, k+1 of one
 // ds_read_b64 group land on 64 distinct banks), B 48 (rows k and k+1 of a group half a bank row
 // apart).  Out-of-range rows / columns / k are zeros in LDS and skipped at the store, so any shape
-// works (K = 3 for the 3-channel input layer).  ca: A is conj(Q)^T, read from Q [F][K][M].
+// works (K = 3 for the 3-channel input layer).  ca: A is conj(Q)^T, read from Q [F][K][M]; cb: B is
+// conj(X)^T, read from X [F][N][K] (the weight gradient G X^H, B row stride 49 then: the stores of a
+// k-run spread over the banks); scale: C[f] *= scale[f] (the rfft gradient weights).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,7 +27,9 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 constexpr int TM = 32, TN = 32, KC = 32;
 constexpr int SA = KC + 2;       // A chunk [TM][SA] (complex)
-constexpr int SB = TN + 16;      // B chunk [KC][SB] (complex)
+template <bool CB>
+constexpr int sbs() { return CB ? TN + 17 : TN + 16; }   // B chunk [KC][SB] (complex)
+constexpr int SBMAX = TN + 17;
 constexpr int NTH = 256;
 constexpr int PER = TM * KC / NTH;   // complex elements per thread per operand chunk (4)
 constexpr int KS = KC / 4;           // MFMA k-steps per full chunk
@@ -33,6 +37,7 @@ static_assert(TM == TN, "one load shape for both operands");
 
 struct CgArgs {
   int M, N, K;
+  const float* scale;        // [F] or null
   const c32* A;
   const c32* B;
   c32* C;
@@ -45,7 +50,7 @@ __device__ __forceinline__ f4v mfma(float a, float b, f4v c) {
 
 // every load is issued (out-of-range elements read element 0 of the operand and are replaced by 0):
 // no per-element branch between the loads, so all of a thread's loads are in flight together
-template <bool CA>
+template <bool CA, bool CB>
 __device__ __forceinline__ void load_chunk(const CgArgs& a, const c32* A, const c32* B, int m0, int n0, int k0,
                                            c32 (&ra)[PER], c32 (&rb)[PER]) {
   const int tid = threadIdx.x;
@@ -63,14 +68,21 @@ __device__ __forceinline__ void load_chunk(const CgArgs& a, const c32* A, const 
       const c32 v = A[in ? (int64_t)(m0 + m) * a.K + k0 + k : 0];
       ra[q] = in ? v : make_float2(0.f, 0.f);
     }
-    const int k = idx / TN, n = idx % TN;
-    const bool in = k0 + k < a.K && n0 + n < a.N;
-    const c32 v = B[in ? (int64_t)(k0 + k) * a.N + n0 + n : 0];
-    rb[q] = in ? v : make_float2(0.f, 0.f);
+    if (CB) {              // opB[k][n] = conj(X[n][k]): rows n of X, contiguous along k
+      const int n = idx / KC, k = idx % KC;
+      const bool in = k0 + k < a.K && n0 + n < a.N;
+      const c32 v = B[in ? (int64_t)(n0 + n) * a.K + k0 + k : 0];
+      rb[q] = in ? make_float2(v.x, -v.y) : make_float2(0.f, 0.f);
+    } else {
+      const int k = idx / TN, n = idx % TN;
+      const bool in = k0 + k < a.K && n0 + n < a.N;
+      const c32 v = B[in ? (int64_t)(k0 + k) * a.N + n0 + n : 0];
+      rb[q] = in ? v : make_float2(0.f, 0.f);
+    }
   }
 }
 
-template <bool CA>
+template <bool CA, bool CB>
 __device__ __forceinline__ void store_chunk(c32* As, c32* Bs, const c32 (&ra)[PER], const c32 (&rb)[PER]) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -83,13 +95,19 @@ __device__ __forceinline__ void store_chunk(c32* As, c32* Bs, const c32 (&ra)[PE
       const int m = idx / KC, k = idx % KC;
       As[m * SA + k] = ra[q];
     }
-    const int k = idx / TN, n = idx % TN;
-    Bs[k * SB + n] = rb[q];
+    if (CB) {
+      const int n = idx / KC, k = idx % KC;
+      Bs[k * sbs<CB>() + n] = rb[q];
+    } else {
+      const int k = idx / TN, n = idx % TN;
+      Bs[k * sbs<CB>() + n] = rb[q];
+    }
   }
 }
 
 // one chunk's MFMAs from LDS (As / Bs at the chunk's buffer): a full chunk reads all its operands
 // first and alternates two accumulator pairs; the K tail runs the plain loop
+template <int SB>
 __device__ __forceinline__ void chunk_mfma(const c32* As, const c32* Bs, int ks, int lane, int wm, int wn, f4v& cr0,
                                            f4v& ci0, f4v& cr1, f4v& ci1) {
   const c32* as = As + (wm + (lane & 15)) * SA + (lane >> 4);
@@ -125,10 +143,11 @@ __device__ __forceinline__ void chunk_mfma(const c32* As, const c32* Bs, int ks,
 
 // One LDS buffer (21 KB: seven workgroups per CU -- the many-tile products run in one round) and two
 // register sets: chunk c + 2's global loads are issued when chunk c's MFMAs start.
-template <bool CA>
+template <bool CA, bool CB>
 __global__ __launch_bounds__(NTH) void k_cgemm(CgArgs a) {
+  constexpr int SB = sbs<CB>();
   __shared__ c32 As[TM * SA];
-  __shared__ c32 Bs[KC * SB];
+  __shared__ c32 Bs[KC * SBMAX];
   const int f = blockIdx.z;
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -138,27 +157,32 @@ __global__ __launch_bounds__(NTH) void k_cgemm(CgArgs a) {
   const int nch = (a.K + KC - 1) / KC;       // >= 1 (K = 0 never launches)
   auto steps = [&](int c) { return (min(KC, a.K - c * KC) + 3) >> 2; };   // 4 complex k per step
   c32 ra0[PER], rb0[PER], ra1[PER], rb1[PER];
-  load_chunk<CA>(a, A, B, m0, n0, 0, ra0, rb0);
-  if (nch > 1) load_chunk<CA>(a, A, B, m0, n0, KC, ra1, rb1);
-  store_chunk<CA>(As, Bs, ra0, rb0);
+  load_chunk<CA, CB>(a, A, B, m0, n0, 0, ra0, rb0);
+  if (nch > 1) load_chunk<CA, CB>(a, A, B, m0, n0, KC, ra1, rb1);
+  store_chunk<CA, CB>(As, Bs, ra0, rb0);
   __syncthreads();
   const f4v z4 = {0.f, 0.f, 0.f, 0.f};
   f4v cr0 = z4, ci0 = z4, cr1 = z4, ci1 = z4;     // even / odd k-steps of a chunk
   for (int c = 0; c < nch; c += 2) {
-    if (c + 2 < nch) load_chunk<CA>(a, A, B, m0, n0, (c + 2) * KC, ra0, rb0);
-    chunk_mfma(As, Bs, steps(c), lane, wm, wn, cr0, ci0, cr1, ci1);
+    if (c + 2 < nch) load_chunk<CA, CB>(a, A, B, m0, n0, (c + 2) * KC, ra0, rb0);
+    chunk_mfma<SB>(As, Bs, steps(c), lane, wm, wn, cr0, ci0, cr1, ci1);
     if (c + 1 >= nch) break;
     __syncthreads();
-    store_chunk<CA>(As, Bs, ra1, rb1);
+    store_chunk<CA, CB>(As, Bs, ra1, rb1);
     __syncthreads();
-    if (c + 3 < nch) load_chunk<CA>(a, A, B, m0, n0, (c + 3) * KC, ra1, rb1);
-    chunk_mfma(As, Bs, steps(c + 1), lane, wm, wn, cr0, ci0, cr1, ci1);
+    if (c + 3 < nch) load_chunk<CA, CB>(a, A, B, m0, n0, (c + 3) * KC, ra1, rb1);
+    chunk_mfma<SB>(As, Bs, steps(c + 1), lane, wm, wn, cr0, ci0, cr1, ci1);
     if (c + 2 >= nch) break;
     __syncthreads();
-    store_chunk<CA>(As, Bs, ra0, rb0);
+    store_chunk<CA, CB>(As, Bs, ra0, rb0);
     __syncthreads();
   }
-  const f4v cr = cr0 + cr1, ci = ci0 + ci1;
+  f4v cr = cr0 + cr1, ci = ci0 + ci1;
+  if (a.scale) {
+    const float sc = a.scale[f];
+    cr *= sc;
+    ci *= sc;
+  }
   // C/D layout of 16x16x4: lane l holds rows 4 (l >> 4) + r, column l & 15
   c32* C = a.C + (int64_t)f * a.sc;
   const int n = n0 + wn + (lane & 15);
@@ -174,15 +198,17 @@ __global__ __launch_bounds__(NTH) void k_cgemm(CgArgs a) {
 }  // namespace
 
 extern "C" int fiode_cgemm(void* stream, int32_t F, int32_t M, int32_t N, int32_t K, int32_t conj_trans_a,
-                           const void* A, const void* B, void* C) {
+                           int32_t conj_trans_b, const float* scale, const void* A, const void* B, void* C) {
   if (F < 0 || M < 0 || N < 0 || K < 0) return FIODE_EINVAL;
   if (F == 0 || M == 0 || N == 0) return FIODE_OK;
   if (!C || (K > 0 && (!A || !B))) return FIODE_EINVAL;     // K = 0: C = 0 (empty operands may be null)
   if ((int64_t)F > 65535) return FIODE_ESHAPE;
+  if (conj_trans_a && conj_trans_b) return FIODE_ESHAPE;    // not needed by the convs: not instantiated
   CgArgs a;
   a.M = M;
   a.N = N;
   a.K = K;
+  a.scale = scale;
   a.A = (const c32*)A;
   a.B = (const c32*)B;
   a.C = (c32*)C;
@@ -192,8 +218,9 @@ extern "C" int fiode_cgemm(void* stream, int32_t F, int32_t M, int32_t N, int32_
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, F);
   if (K == 0) return hipMemsetAsync(C, 0, (size_t)F * M * N * sizeof(c32), st) == hipSuccess ? FIODE_OK : FIODE_EHIP;
-  if (conj_trans_a) hipLaunchKernelGGL(k_cgemm<true>, grid, dim3(NTH), 0, st, a);
-  else hipLaunchKernelGGL(k_cgemm<false>, grid, dim3(NTH), 0, st, a);
+  if (conj_trans_a) hipLaunchKernelGGL((k_cgemm<true, false>), grid, dim3(NTH), 0, st, a);
+  else if (conj_trans_b) hipLaunchKernelGGL((k_cgemm<false, true>), grid, dim3(NTH), 0, st, a);
+  else hipLaunchKernelGGL((k_cgemm<false, false>), grid, dim3(NTH), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

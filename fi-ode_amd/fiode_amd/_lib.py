@@ -187,7 +187,8 @@ def _load():
         "fiode_dense_gemm": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp]),
         "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
         "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
-        "fiode_cgemm": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp]),
+        "fiode_cgemm": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp,
+                                   _vp, _vp, _vp]),
         "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),
         "fiode_spectral_cayley_forward": (ct.c_int, [_vp, ct.POINTER(SpectralConfig), _vp, _vp, _vp, _vp, _vp,
                                                      ct.c_size_t]),

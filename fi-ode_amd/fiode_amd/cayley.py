@@ -719,8 +719,13 @@ class _SpectralConvFn(torch.autograd.Function):
                 w = torch.where((kb == 0) | (kb == n // 2), 1.0, 2.0) / float(n * n)
                 wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
 
+        def qgrad():        # dL/dQ = w G X^H (fiode_cgemm with the rfft weights folded in)
+            if SCONV_CGEMM and SCONV_CGEMM_WGRAD:
+                return ops.cgemm(G, X, conj_trans_b=True, scale=wq)
+            return torch.matmul(G, X.mH) * wq
+
         def wgrad():
-            gq = torch.matmul(G, X.mH) * wq if need_q else None
+            gq = qgrad() if need_q else None
             gbias = G[0].real.sum(-1) if need_b else None
             return gq, gbias
         ws = ctx.wstream
@@ -734,7 +739,7 @@ class _SpectralConvFn(torch.autograd.Function):
             cur = torch.cuda.current_stream(G.device)
             ws.wait_stream(cur)
             with torch.cuda.stream(ws):
-                gQ = torch.matmul(G, X.mH) * wq if need_q else None
+                gQ = qgrad() if need_q else None
                 if need_b and CONV_WGRAD_MAPSTREAM_BIAS:
                     gb = G[0].real.sum(-1)
                     ev = torch.cuda.Event()
@@ -776,6 +781,9 @@ _SPECTRAL_GRAD_WEIGHTS = {}
 # 41 -> 16 us, its input gradient 17 -> 16, conv 3's 16 -> 10, conv 1's forward 13 -> 10 us; step
 # -25 to -40 us in the alternating A/B, profiles/r05bd)
 SCONV_CGEMM = os.environ.get("FIODE_SCONV_CGEMM", "1") != "0"
+# w G X^H in one fiode_cgemm launch too: measured 10-20 us SLOWER in the step than the library GEMM +
+# the scale kernel (profiles/r05bj), so off
+SCONV_CGEMM_WGRAD = os.environ.get("FIODE_SCONV_CGEMM_WGRAD", "0") != "0"
 
 
 def _q_h_g(Q, G):

@@ -552,23 +552,28 @@ def sconv_irfft2(Y: torch.Tensor, n: int, C: int, B: int, bias: Optional[torch.T
     return y, code
 
 
-def cgemm(A: torch.Tensor, B: torch.Tensor, conj_trans_a: bool = False) -> torch.Tensor:
-    """fiode_cgemm: batched complex64 C[f] = A[f] @ B[f] (or A[f]^H @ B[f]) for contiguous
-    A [F, M, K] ([F, K, M] with conj_trans_a), B [F, K, N] -> C [F, M, N]."""
+def cgemm(A: torch.Tensor, B: torch.Tensor, conj_trans_a: bool = False, conj_trans_b: bool = False,
+          scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fiode_cgemm: batched complex64 C[f] = scale[f] opA(A[f]) @ opB(B[f]); A [F, M, K] ([F, K, M]
+    with conj_trans_a: A^H), B [F, K, N] ([F, N, K] with conj_trans_b: B^H), scale [F] float32."""
     dev = B.device
     if A.dim() != 3 or B.dim() != 3 or A.dtype != torch.complex64 or B.dtype != torch.complex64:
         raise ValueError(f"cgemm: complex64 [F, ., .] operands, got {tuple(A.shape)} {A.dtype}, "
                          f"{tuple(B.shape)} {B.dtype}")
-    F, K, N = B.shape
-    M = A.shape[2] if conj_trans_a else A.shape[1]
-    ka = A.shape[1] if conj_trans_a else A.shape[2]
+    if conj_trans_a and conj_trans_b:
+        raise ValueError("cgemm: conj_trans_a and conj_trans_b together are not supported")
+    F = B.shape[0]
+    K, N = (B.shape[2], B.shape[1]) if conj_trans_b else (B.shape[1], B.shape[2])
+    M, ka = (A.shape[2], A.shape[1]) if conj_trans_a else (A.shape[1], A.shape[2])
     if A.shape[0] != F or ka != K or A.device != dev:
         raise ValueError(f"cgemm: A {tuple(A.shape)} does not match B {tuple(B.shape)}")
+    if scale is not None:
+        scale = _need(scale.detach().reshape(-1), "scale", (F,), torch.float32, dev)
     A = A.contiguous()
     B = B.contiguous()
     C = torch.empty((F, M, N), dtype=torch.complex64, device=dev)
-    L.check(L.lib().fiode_cgemm(_stream(dev), F, M, N, K, int(bool(conj_trans_a)), A.data_ptr(), B.data_ptr(),
-                                C.data_ptr()), "fiode_cgemm")
+    L.check(L.lib().fiode_cgemm(_stream(dev), F, M, N, K, int(bool(conj_trans_a)), int(bool(conj_trans_b)),
+                                _ptr(scale), A.data_ptr(), B.data_ptr(), C.data_ptr()), "fiode_cgemm")
     return C
 
 

@@ -417,10 +417,12 @@ FIODE_API int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, co
 
 /* Batched complex64 GEMM of the spectral convolutions' per-frequency channel products (CayleyConv
  * forward_hwcb; replaces torch.matmul on complex64 in fiode_amd/cayley.py _SpectralConvFn):
- * C[f] = opA(A[f]) B[f] for f < F, B [F][K][N], C [F][M][N] (row-major, contiguous);
- * conj_trans_a == 0: A [F][M][K], opA = A; else A [F][K][M], opA = conj(A)^T (dL/dX = Q^H G). */
+ * C[f] = scale[f] opA(A[f]) opB(B[f]) for f < F, C [F][M][N] (row-major, contiguous);
+ * conj_trans_a == 0: A [F][M][K], opA = A; else A [F][K][M], opA = conj(A)^T (dL/dX = Q^H G);
+ * conj_trans_b == 0: B [F][K][N], opB = B; else B [F][N][K], opB = conj(B)^T (dL/dQ = w G X^H);
+ * not both; scale [F] float32 or NULL (1). */
 FIODE_API int fiode_cgemm(void* stream, int32_t F, int32_t M, int32_t N, int32_t K, int32_t conj_trans_a,
-                          const void* A, const void* B, void* C);
+                          int32_t conj_trans_b, const float* scale, const void* A, const void* B, void* C);
 
 /* ---- spectral Cayley map of an orthogonal convolution (CayleyConv; libs/ortho_conv, absent:
  * restated in fiode_amd/cayley.py).  Replaces CayleyConv.spectral_weight + cayley_scaled

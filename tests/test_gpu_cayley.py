@@ -355,24 +355,31 @@ def test_spectral_conv_fused_matches_torch_fft(case):
 
 # (F, M, N, K, conj_trans_a): the four KWLarge layers' forward products, the three input-gradient
 # products, and ragged / tiny shapes (partial tiles, K not a multiple of 4, K = 0)
-CGEMM_CASES = [(544, 32, 128, 3, False), (144, 32, 128, 128, False), (144, 64, 128, 32, False),
-               (40, 64, 128, 256, False), (144, 128, 128, 32, True), (144, 32, 128, 64, True),
-               (40, 256, 128, 64, True), (3, 33, 7, 70, False), (5, 17, 40, 5, True), (1, 1, 1, 1, False),
-               (2, 8, 4, 0, False)]
+# (F, M, N, K, op): "n" C = A B, "ca" C = A^H B, "cb" C = w A B^H (the weight gradient, scaled)
+CGEMM_CASES = [(544, 32, 128, 3, "n"), (144, 32, 128, 128, "n"), (144, 64, 128, 32, "n"),
+               (40, 64, 128, 256, "n"), (144, 128, 128, 32, "ca"), (144, 32, 128, 64, "ca"),
+               (40, 256, 128, 64, "ca"), (40, 64, 256, 128, "cb"), (544, 32, 3, 128, "cb"), (144, 32, 128, 128, "cb"),
+               (3, 33, 7, 70, "n"), (5, 17, 40, 5, "ca"), (4, 19, 45, 37, "cb"), (1, 1, 1, 1, "n"),
+               (2, 8, 4, 0, "n")]
 
 
 @pytest.mark.parametrize("case", CGEMM_CASES)
 def test_cgemm_matches_complex128(case):
     """fiode_cgemm (cgemm.hip, the spectral convs' per-frequency products) vs torch.matmul in
-    complex128: C[f] = A[f] B[f] or A[f]^H B[f]."""
+    complex128: C[f] = A[f] B[f], A[f]^H B[f] or w[f] A[f] B[f]^H."""
     from fiode_amd import ops
-    F, M, N, K, ca = case
+    F, M, N, K, op = case
+    ca, cb = op == "ca", op == "cb"
     dev = _dev()
     g = torch.Generator(device="cpu").manual_seed(F * 131 + M * 7 + K)
     A = torch.randn((F, K, M) if ca else (F, M, K), dtype=torch.complex64, generator=g)
-    B = torch.randn((F, K, N), dtype=torch.complex64, generator=g)
-    C = ops.cgemm(A.to(dev), B.to(dev), conj_trans_a=ca).cpu()
-    ref = (A.cdouble().mH if ca else A.cdouble()) @ B.cdouble()
+    B = torch.randn((F, N, K) if cb else (F, K, N), dtype=torch.complex64, generator=g)
+    w = torch.rand(F, generator=g) + 0.5 if cb else None
+    C = ops.cgemm(A.to(dev), B.to(dev), conj_trans_a=ca, conj_trans_b=cb,
+                  scale=None if w is None else w.to(dev)).cpu()
+    ref = (A.cdouble().mH if ca else A.cdouble()) @ (B.cdouble().mH if cb else B.cdouble())
+    if w is not None:
+        ref = ref * w.double()[:, None, None]
     assert C.shape == (F, M, N)
     err = float((C.cdouble() - ref).abs().max()) if C.numel() else 0.0
     assert err <= 2e-6 * (K + 1) ** 0.5 * 4, err

@@ -236,6 +236,12 @@ def ode_lo(m):
     m._ode_prio = 0                   # the train_ode solve's stream at normal priority
 
 
+def cgemm_wgrad_on(m):
+    from fiode_amd import cayley as CY
+    CY.SCONV_CGEMM_WGRAD = True       # the conv weight gradient w G X^H by fiode_cgemm (r05bj: slower)
+    RESTORE.append(lambda: setattr(CY, "SCONV_CGEMM_WGRAD", False))
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -243,7 +249,7 @@ def dyn_wgrad_main(m):
 
 
 ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
-       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
+       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "cgemm_wgrad_on": cgemm_wgrad_on, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
        "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
