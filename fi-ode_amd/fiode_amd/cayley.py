@@ -690,8 +690,7 @@ class _SpectralConvFn(torch.autograd.Function):
         B = x.shape[-1]
         nf, cout, cin = Q.shape
         X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
-        # (the library's solution stays faster for a 32-row product over K >= 128: conv 2, 11.6 vs 15 us)
-        own = SCONV_CGEMM and not (cout <= 32 and cin >= 128)
+        own = SCONV_CGEMM and not (SCONV_CGEMM_LIB_THIN and cout <= 32 and cin >= 128)
         Y = ops.cgemm(Q.detach(), X) if own else torch.matmul(Q.detach(), X)
         y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort)
         ctx.save_for_backward(X, Q, code)
@@ -786,9 +785,17 @@ SCONV_CGEMM = os.environ.get("FIODE_SCONV_CGEMM", "1") != "0"
 SCONV_CGEMM_WGRAD = os.environ.get("FIODE_SCONV_CGEMM_WGRAD", "0") != "0"
 
 
+# the library for the 32-row forward products over K >= 128 (conv 2): 11.6 vs 15 us per call under
+# the profiler, but 13 us SLOWER in the step's interleaved A/B (profiles/r05bk): off
+SCONV_CGEMM_LIB_THIN = False
+SCONV_CGEMM_DX = True            # Q^H G by fiode_cgemm (the library: equal within 7 us, r05bk)
+
+
 def _q_h_g(Q, G):
     from . import ops
-    return ops.cgemm(Q.detach(), G, conj_trans_a=True) if SCONV_CGEMM else torch.matmul(Q.detach().mH, G)
+    if SCONV_CGEMM and SCONV_CGEMM_DX:
+        return ops.cgemm(Q.detach(), G, conj_trans_a=True)
+    return torch.matmul(Q.detach().mH, G)
 
 CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
 # a layer whose map is computed ahead with an early update (GraphTrainStep on one rank): its weight /
