@@ -91,6 +91,9 @@ struct SArgs {
   const float* bias;             // [C] or null
   float* y;                      // irfft2 output [n][n][C][B] (ds: [2n][2n][C/4][B])
   uint8_t* code_out;             // [n][n][C/2][B]
+  const float* xn;               // rfft2 input in NCHW [B][C][n][n], normalised on load (the backbone's
+  const float* mu;               //   first layer: Normalize fused, models.py:17-26), mu / sd [C]
+  const float* sd;               //   (sd nullable)
 };
 
 __device__ __forceinline__ int64_t act_index(const SArgs& a, int h, int w, int c, int b) {
@@ -215,7 +218,20 @@ __global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArg
     return;
   }
   const int c = blockIdx.x;
-  if (a.ds) {
+  if (a.xn) {      // NCHW input, (x - mu) / sd as fiode_normalize_hwcb computes it; lanes along w
+    const float m = a.mu[c], sdv = a.sd ? a.sd[c] : 1.0f;
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL) {
+        const int w = idx % N, h = (idx / N) % N, bt = idx / (N * N);
+        const int b = min(b0 + bt, a.B - 1);
+        float v = a.xn[(((int64_t)b * a.C + c) * N + h) * N + w] - m;
+        if (a.sd) v = v / sdv;
+        img[G::pix(0, bt, h) + w] = b0 + bt < a.B ? v : 0.f;
+      }
+    }
+  } else if (a.ds) {
 #pragma unroll
     for (int t = 0; t < TR; ++t) {
       const int idx = tid + t * NT;
@@ -385,6 +401,34 @@ extern "C" int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, co
   const bool small = (int64_t)a.C * ((a.B + BT_F - 1) / BT_F) < 256;
   const int bt = small ? 4 : a.n == 32 ? SCONV_BTF32 : BT_F;
   const dim3 grid(gy ? a.C / 2 : a.C, (a.B + bt - 1) / bt);
+  if (a.n == 8) {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8, BT_F, false>()), 0, st, a);
+  } else if (a.n == 16) {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<16, 4>), grid, dim3(nthreads<16, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<16, BT_F>), grid, dim3(nthreads<16, BT_F, false>()), 0, st, a);
+  } else {
+    if (small) hipLaunchKernelGGL((k_sconv_rfft2<32, 4>), grid, dim3(nthreads<32, 4, false>()), 0, st, a);
+    else hipLaunchKernelGGL((k_sconv_rfft2<32, SCONV_BTF32>), grid, dim3(nthreads<32, SCONV_BTF32, false>()), 0, st, a);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_sconv_rfft2_nchw(void* stream, const fiode_sconv_config* cfg, const float* x, const float* mu,
+                                      const float* sd, void* X) {
+  SArgs a;
+  int rc = check(cfg, a);
+  if (rc) return rc;
+  if (!X || !x || !mu || a.ds) return FIODE_EINVAL;
+  a.xn = x;
+  a.mu = mu;
+  a.sd = sd;
+  a.X = (c32*)X;
+  hipStream_t st = (hipStream_t)stream;
+  const bool small = (int64_t)a.C * ((a.B + BT_F - 1) / BT_F) < 256;
+  const int bt = small ? 4 : a.n == 32 ? SCONV_BTF32 : BT_F;
+  const dim3 grid(a.C, (a.B + bt - 1) / bt);
   if (a.n == 8) {
     if (small) hipLaunchKernelGGL((k_sconv_rfft2<8, 4>), grid, dim3(nthreads<8, 4, false>()), 0, st, a);
     else hipLaunchKernelGGL((k_sconv_rfft2<8, BT_F>), grid, dim3(nthreads<8, BT_F, false>()), 0, st, a);

@@ -684,12 +684,16 @@ class _SpectralConvFn(torch.autograd.Function):
         G = rfft2(d/dpre),  dQ = (w_kb / n^2) G X^H,  dx = irfft2(Q^H G),  dbias = sum_b Re G[0]."""
 
     @staticmethod
-    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None):
+    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None, norm=None):
         from . import ops
         ctx.wstream = wstream
-        B = x.shape[-1]
         nf, cout, cin = Q.shape
-        X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
+        if norm is not None:     # x: the NCHW network input, normalised on load (no input gradient)
+            B = x.shape[0]
+            X = ops.sconv_rfft2_nchw(x.detach(), norm[0], norm[1], n)
+        else:
+            B = x.shape[-1]
+            X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
         own = SCONV_CGEMM and not (SCONV_CGEMM_LIB_THIN and cout <= 32 and cin >= 128)
         Y = ops.cgemm(Q.detach(), X) if own else torch.matmul(Q.detach(), X)
         y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort)
@@ -751,7 +755,7 @@ class _SpectralConvFn(torch.autograd.Function):
                 gb = G[0].real.sum(-1)
             if need_x:
                 gx, _ = ops.sconv_irfft2(_q_h_g(Q, G), n, cin, B, downsample=downsample)
-            return gx, gQ, gb, None, None, None, None
+            return gx, gQ, gb, None, None, None, None, None
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
         # critical chain), on the side stream of the linear head's, joined before returning
         side = _head_stream(G.device) if (CONV_WGRAD_SIDE and G.is_cuda and need_x and (need_q or need_b)) else None
@@ -771,7 +775,7 @@ class _SpectralConvFn(torch.autograd.Function):
                     t.record_stream(cur)
         else:
             gQ, gb = wgrad()
-        return gx, gQ, gb, None, None, None, None
+        return gx, gQ, gb, None, None, None, None, None
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
@@ -966,6 +970,16 @@ class CayleyConv(nn.Conv2d):
         Q = self._take_spectral(n, x.device)
         ws, self._wstream = self._wstream, None
         return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, ws)
+
+    def forward_nchw_fused(self, x: torch.Tensor, mu: torch.Tensor, sd, groupsort: bool) -> torch.Tensor:
+        """forward_hwcb_fused of the network's first layer straight from the NCHW input x [B][C][n][n]
+        with the preceding Normalize's (x - mu) / sd applied in the transform's loads (one launch and
+        one HBM round trip fewer than Normalize's spatial-major kernel + the transform; x needs no
+        gradient)."""
+        n = x.shape[-1]
+        Q = self._take_spectral(n, x.device)
+        ws, self._wstream = self._wstream, None
+        return _SpectralConvFn.apply(x, Q, self.bias, n, False, groupsort, ws, (mu, sd))
 
     def forward_hwcb(self, x: torch.Tensor) -> torch.Tensor:
         """The same map on spatial-major activations [n, n, C, B] (the conv stack's HBM layout):

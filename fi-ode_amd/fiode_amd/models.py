@@ -69,20 +69,38 @@ class KWLargeConcat(nn.Module):
         self.spatial_major = True
         self.fused_transforms = True      # sconv.hip rfft2 / irfft2 (+ GroupSort) around the GEMMs
 
-    def forward(self, x):
+    def can_take_nchw(self, x) -> bool:
+        """Whether forward(x, norm=...) can run the first conv straight from the NCHW input."""
+        m = self.model[0]
+        return (self.spatial_major and self.fused_transforms and x.is_cuda and x.dtype == torch.float32
+                and x.dim() == 4 and not x.requires_grad and isinstance(m, CayleyConv) and not m.downsample
+                and x.shape[-1] == x.shape[-2] and x.shape[-1] in (8, 16, 32))
+
+    def forward(self, x, norm=None):
         """On ROCm the conv stack runs spatial-major ([h, w, C, B]: FFT and GEMM operands without
         permute copies, CayleyConv.forward_hwcb); the flatten restores the reference's (C, h, w)
-        feature order.  Host tensors take the module-by-module NCHW path."""
+        feature order.  Host tensors take the module-by-module NCHW path.  norm = (mu, sd): x is the
+        raw NCHW input and the first conv applies the Normalize in its transform (NormalizedBackbone)."""
         if not (self.spatial_major and x.is_cuda):
             return self.model(x)
         mods = list(self.model)
-        h = x.permute(2, 3, 1, 0).contiguous()
         i = 0
         nconv = 0
         # after_conv_hook(conv index) -> None (e.g. a prefetch launch), re-read at every call site so a
         # hook may install the next one; index -1: input laid out, before the first conv
-        if getattr(self, "after_conv_hook", None) is not None:
-            self.after_conv_hook(-1)
+        if norm is not None:
+            if getattr(self, "after_conv_hook", None) is not None:
+                self.after_conv_hook(-1)
+            gs = isinstance(mods[1], GroupSort)
+            h = mods[0].forward_nchw_fused(x, norm[0], norm[1], gs)
+            i = 2 if gs else 1
+            if getattr(self, "after_conv_hook", None) is not None:
+                self.after_conv_hook(0)
+            nconv = 1
+        else:
+            h = x.permute(2, 3, 1, 0).contiguous()
+            if getattr(self, "after_conv_hook", None) is not None:
+                self.after_conv_hook(-1)
         while not isinstance(mods[i], nn.Flatten):
             m = mods[i]
             if isinstance(m, CayleyConv):
@@ -107,10 +125,26 @@ class KWLargeConcat(nn.Module):
         return linear_head(mods[i + 1:], h)
 
 
+class NormalizedBackbone(nn.Sequential):
+    """nn.Sequential(Normalize, KWLargeConcat) (the same modules and state-dict keys) whose forward on
+    ROCm hands the raw NCHW input and the normalisation to the backbone's first conv transform
+    (fiode_sconv_rfft2_nchw): the spatial-major normalised copy and its launch drop out.  Anything
+    else runs the two modules in turn."""
+
+    fused_input = True
+
+    def forward(self, x):
+        norm, net = self[0], self[1]
+        if (self.fused_input and len(self) == 2 and isinstance(norm, Normalize) and isinstance(net, KWLargeConcat)
+                and norm.fused_hwcb and net.can_take_nchw(x)):
+            return net(x.contiguous(), norm=(norm.mu, norm.std))
+        return super().forward(x)
+
+
 def make_ortho_KWLarge_Concat(n_in_channels=3, n_outputs=10, mu=(0.485, 0.456, 0.406), std=(0.225, 0.225, 0.225),
                               out_dim=10, act="GroupSort"):
     """models.py:29-35 (CIFAR10 MU/STD from ExpConfig.py:57-58)."""
-    return nn.Sequential(Normalize(mu, std), KWLargeConcat(out_dim=out_dim, act=act))
+    return NormalizedBackbone(Normalize(mu, std), KWLargeConcat(out_dim=out_dim, act=act))
 
 
 class DefaultOutputFun(nn.Module):

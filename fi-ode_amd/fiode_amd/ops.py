@@ -535,6 +535,22 @@ def sconv_rfft2(x: Optional[torch.Tensor], n: int, C: int, B: int, downsample: b
     return X
 
 
+def sconv_rfft2_nchw(x: torch.Tensor, mu: torch.Tensor, sd: Optional[torch.Tensor], n: int) -> torch.Tensor:
+    """fiode_sconv_rfft2_nchw: X = rfft2((x - mu) / sd) of an NCHW input x [B][C][n][n] -> complex64
+    [n (n/2+1), C, B] (the first conv with the backbone's Normalize fused)."""
+    dev = x.device
+    B, C = x.shape[0], x.shape[1]
+    x = _need(x, "x", (B, C, n, n), torch.float32, dev)
+    mu = _need(mu.detach().reshape(-1), "mu", (C,), torch.float32, dev)
+    if sd is not None:
+        sd = _need(sd.detach().reshape(-1), "sd", (C,), torch.float32, dev)
+    X = torch.empty((n * (n // 2 + 1), C, B), dtype=torch.complex64, device=dev)
+    cfg = L.SconvConfig(n, C, B, 0)
+    L.check(L.lib().fiode_sconv_rfft2_nchw(_stream(dev), ct.byref(cfg), x.data_ptr(), mu.data_ptr(), _ptr(sd),
+                                           X.data_ptr()), "fiode_sconv_rfft2_nchw")
+    return X
+
+
 def sconv_irfft2(Y: torch.Tensor, n: int, C: int, B: int, bias: Optional[torch.Tensor] = None,
                  groupsort: bool = False, downsample: bool = False):
     """fiode_sconv_irfft2: complex64 [n (n/2+1), C, B] -> y [n][n][C][B] (+ bias; GroupSort with its

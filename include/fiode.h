@@ -410,6 +410,10 @@ typedef struct fiode_sconv_config {
  * [n][n][C][B]) with the comparison codes [n][n][C/2][B] of the forward (x unused). */
 FIODE_API int fiode_sconv_rfft2(void* stream, const fiode_sconv_config* cfg, const float* x, const float* gy,
                                 const uint8_t* code, void* X);
+/* X = rfft2((x - mu) / std) for an NCHW input x [B][C][n][n] (the backbone's first conv with its
+ * Normalize fused, models.py:17-26; std nullable: x - mu; downsample must be 0). */
+FIODE_API int fiode_sconv_rfft2_nchw(void* stream, const fiode_sconv_config* cfg, const float* x, const float* mu,
+                                     const float* std, void* X);
 /* y = irfft2(Y) (c2c over h, c2r over w, 1/n^2), + bias[C] if given; groupsort != 0: y = GroupSort
  * of it over the channel halves and code_out [n][n][C/2][B] records max/min/tie. */
 FIODE_API int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,

@@ -211,6 +211,28 @@ def test_spatial_major_backbone_matches_nchw():
         assert float((a.grad - b).abs().max()) <= 1e-3 * (float(b.abs().max()) + 1e-6)
 
 
+def test_normalized_backbone_fused_input_bit_identical():
+    """NormalizedBackbone: the first conv's transform reading the raw NCHW input and normalising on
+    load (fiode_sconv_rfft2_nchw) = Normalize's spatial-major kernel + the transform, bit for bit
+    (forward and every parameter gradient)."""
+    from fiode_amd.models import make_ortho_KWLarge_Concat
+    dev = _dev()
+    torch.manual_seed(1)
+    bb = make_ortho_KWLarge_Concat(out_dim=10, act="GroupSort").to(dev).train()
+    x = torch.rand(12, 3, 32, 32, device=dev)
+    bb(x)                           # alpha init
+    outs = []
+    for fused in (False, True):
+        bb.fused_input = fused
+        bb.zero_grad()
+        y = bb(x)
+        y.square().sum().backward()
+        outs.append((y.detach().clone(), [p.grad.clone() for p in bb.parameters()]))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a, b)
+
+
 # ---- fused spectral Cayley map of CayleyConv (spectral.hip) ---------------------------------------
 # (cout, cin, n): the four KWLarge convs (cin after the stride-2 space-to-channel) + square / tall /
 # small-K cases.  Reference: CayleyConv.spectral_weight_reference (rfft2 + shift + conj +
