@@ -83,6 +83,7 @@ __device__ __forceinline__ float gs_grad(float gmx, float gmn, uint8_t code, boo
 
 struct SArgs {
   int n, H, C, B, ds, gs;        // H = n/2 + 1; ds: stride-2 space-to-channel; gs: GroupSort
+  int nchw;                      // irfft2 output y / rfft2 gy input as [B][C][n][n], codes [B][C/2][n][n]
   const float* x;                // rfft2 input [n][n][C][B] (ds: [2n][2n][C/4][B])
   const float* gy;               // rfft2 GroupSort-backward prologue: d/dout [n][n][C][B]
   const uint8_t* code;           // [n][n][C/2][B]
@@ -98,6 +99,14 @@ struct SArgs {
 
 __device__ __forceinline__ int64_t act_index(const SArgs& a, int h, int w, int c, int b) {
   return (((int64_t)h * a.n + w) * a.C + c) * a.B + b;
+}
+// NCHW element / GroupSort code (the last conv's output, read by the flatten as (C, h, w) features)
+__device__ __forceinline__ int64_t nchw_index(const SArgs& a, int h, int w, int c, int b) {
+  return (((int64_t)b * a.C + c) * a.n + h) * a.n + w;
+}
+__device__ __forceinline__ int64_t code_index(const SArgs& a, int h, int w, int c0, int b) {
+  const int half = a.C >> 1;
+  return a.nchw ? (((int64_t)b * half + c0) * a.n + h) * a.n + w : (((int64_t)h * a.n + w) * half + c0) * a.B + b;
 }
 // element (h, w, c) of the (space-to-channel) input in the raw [2n][2n][C/4][B] tensor
 __device__ __forceinline__ int64_t raw_index(const SArgs& a, int h, int w, int c, int b) {
@@ -204,10 +213,13 @@ __global__ void __launch_bounds__((nthreads<N, BT, false>())) k_sconv_rfft2(SArg
     for (int t = 0; t < TR; ++t) {
       const int idx = tid + t * NT;
       if (idx < NL) {
-        const int bt = idx % BT, hw = idx / BT, h = hw / N, w = hw % N;
+        // lanes along b for the spatial-major layout, along w for NCHW (coalesced either way)
+        const int bt = a.nchw ? idx / (N * N) : idx % BT;
+        const int hw = a.nchw ? idx % (N * N) : idx / BT, h = hw / N, w = hw % N;
         const int b = min(b0 + bt, a.B - 1);
-        const uint8_t code = a.code[(((int64_t)h * N + w) * half + c0) * a.B + b];
-        const float gmx = a.gy[act_index(a, h, w, c0, b)], gmn = a.gy[act_index(a, h, w, c1, b)];
+        const uint8_t code = a.code[code_index(a, h, w, c0, b)];
+        const float gmx = a.gy[a.nchw ? nchw_index(a, h, w, c0, b) : act_index(a, h, w, c0, b)];
+        const float gmn = a.gy[a.nchw ? nchw_index(a, h, w, c1, b) : act_index(a, h, w, c1, b)];
         const bool in = b0 + bt < a.B;
         img[G::pix(0, bt, h) + w] = in ? gs_grad(gmx, gmn, code, true) : 0.f;
         img[G::pix(1, bt, h) + w] = in ? gs_grad(gmx, gmn, code, false) : 0.f;
@@ -348,24 +360,28 @@ __global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_ir
     irfft2_inplace<N, 2>(a, c0, c1, b0, Ys);
     const float bb0 = a.bias ? a.bias[c0] : 0.f, bb1 = a.bias ? a.bias[c1] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
-      const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
+      const int bt = a.nchw ? idx / (N * N) : idx % BTI;
+      const int hw = a.nchw ? idx % (N * N) : idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
       const float p = o[G::pix(0, bt, h) + w] + bb0, q = o[G::pix(1, bt, h) + w] + bb1;
-      a.y[act_index(a, h, w, c0, b)] = fmaxf(p, q);
-      a.y[act_index(a, h, w, c1, b)] = fminf(p, q);
-      a.code_out[(((int64_t)h * N + w) * half + c0) * a.B + b] = p > q ? GS_GT : (p < q ? GS_LT : GS_EQ);
+      a.y[a.nchw ? nchw_index(a, h, w, c0, b) : act_index(a, h, w, c0, b)] = fmaxf(p, q);
+      a.y[a.nchw ? nchw_index(a, h, w, c1, b) : act_index(a, h, w, c1, b)] = fminf(p, q);
+      a.code_out[code_index(a, h, w, c0, b)] = p > q ? GS_GT : (p < q ? GS_LT : GS_EQ);
     }
+    (void)half;
   } else {
     const int c = blockIdx.x;
     irfft2_inplace<N, 1>(a, c, c, b0, Ys);
     const float bb = a.bias ? a.bias[c] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
-      const int bt = idx % BTI, hw = idx / BTI, h = hw / N, w = hw % N;
+      const int bt = a.nchw ? idx / (N * N) : idx % BTI;
+      const int hw = a.nchw ? idx % (N * N) : idx / BTI, h = hw / N, w = hw % N;
       const int b = b0 + bt;
       if (b >= a.B) continue;
       const float v = o[G::pix(0, bt, h) + w] + bb;
       if (a.ds) a.y[raw_index(a, h, w, c, b)] = v;
+      else if (a.nchw) a.y[nchw_index(a, h, w, c, b)] = v;
       else a.y[act_index(a, h, w, c, b)] = v;
     }
   }
@@ -378,7 +394,9 @@ int check(const fiode_sconv_config* cfg, SArgs& a) {
   a.C = cfg->C;
   a.B = cfg->B;
   a.ds = cfg->downsample ? 1 : 0;
+  a.nchw = cfg->nchw ? 1 : 0;
   if ((a.n != 8 && a.n != 16 && a.n != 32) || a.C < 1 || a.B < 1) return FIODE_ESHAPE;
+  if (a.nchw && a.ds) return FIODE_ESHAPE;
   if (a.ds && (a.C & 3)) return FIODE_ESHAPE;
   a.H = a.n / 2 + 1;
   return FIODE_OK;

@@ -102,7 +102,8 @@ class AdamConfig(ct.Structure):
 
 
 class SconvConfig(ct.Structure):
-    _fields_ = [("n", ct.c_int32), ("C", ct.c_int32), ("B", ct.c_int32), ("downsample", ct.c_int32)]
+    _fields_ = [("n", ct.c_int32), ("C", ct.c_int32), ("B", ct.c_int32), ("downsample", ct.c_int32),
+                ("nchw", ct.c_int32)]
 
 
 class DenseConfig(ct.Structure):

@@ -684,7 +684,8 @@ class _SpectralConvFn(torch.autograd.Function):
         G = rfft2(d/dpre),  dQ = (w_kb / n^2) G X^H,  dx = irfft2(Q^H G),  dbias = sum_b Re G[0]."""
 
     @staticmethod
-    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None, norm=None):
+    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None, norm=None,
+                nchw_out: bool = False):
         from . import ops
         ctx.wstream = wstream
         nf, cout, cin = Q.shape
@@ -696,9 +697,11 @@ class _SpectralConvFn(torch.autograd.Function):
             X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
         own = SCONV_CGEMM and not (SCONV_CGEMM_LIB_THIN and cout <= 32 and cin >= 128)
         Y = ops.cgemm(Q.detach(), X) if own else torch.matmul(Q.detach(), X)
-        y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort)
+        y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort,
+                                   nchw=nchw_out)
         ctx.save_for_backward(X, Q, code)
         ctx.cfg = (n, downsample, groupsort, bias is not None, cin, cout, B)
+        ctx.nchw_out = nchw_out
         return y
 
     @staticmethod
@@ -708,7 +711,7 @@ class _SpectralConvFn(torch.autograd.Function):
         n, downsample, groupsort, has_bias, cin, cout, B = ctx.cfg
         gy = gy.contiguous()
         if groupsort:
-            G = ops.sconv_rfft2(None, n, cout, B, gy=gy, code=code)
+            G = ops.sconv_rfft2(None, n, cout, B, gy=gy, code=code, nchw=ctx.nchw_out)
         else:
             G = ops.sconv_rfft2(gy, n, cout, B)
         gx = gQ = gb = None
@@ -755,7 +758,7 @@ class _SpectralConvFn(torch.autograd.Function):
                 gb = G[0].real.sum(-1)
             if need_x:
                 gx, _ = ops.sconv_irfft2(_q_h_g(Q, G), n, cin, B, downsample=downsample)
-            return gx, gQ, gb, None, None, None, None, None
+            return gx, gQ, gb, None, None, None, None, None, None
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
         # critical chain), on the side stream of the linear head's, joined before returning
         side = _head_stream(G.device) if (CONV_WGRAD_SIDE and G.is_cuda and need_x and (need_q or need_b)) else None
@@ -775,7 +778,7 @@ class _SpectralConvFn(torch.autograd.Function):
                     t.record_stream(cur)
         else:
             gQ, gb = wgrad()
-        return gx, gQ, gb, None, None, None, None, None
+        return gx, gQ, gb, None, None, None, None, None, None
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
@@ -963,13 +966,15 @@ class CayleyConv(nn.Conv2d):
             y = y + self.bias[:, None, None]
         return y
 
-    def forward_hwcb_fused(self, x: torch.Tensor, groupsort: bool) -> torch.Tensor:
+    def forward_hwcb_fused(self, x: torch.Tensor, groupsort: bool, nchw_out: bool = False) -> torch.Tensor:
         """forward_hwcb (+ the following GroupSort) with the transforms as HIP kernels
-        (_SpectralConvFn): [n][n][cin][B] (stride 2: [2n][2n][cin/4][B]) -> [n][n][cout][B]."""
+        (_SpectralConvFn): [n][n][cin][B] (stride 2: [2n][2n][cin/4][B]) -> [n][n][cout][B], or with
+        nchw_out (GroupSort only) [B][cout][n][n] -- the last conv, whose output the flatten reads."""
         n = x.shape[0] // 2 if self.downsample else x.shape[0]
         Q = self._take_spectral(n, x.device)
         ws, self._wstream = self._wstream, None
-        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, ws)
+        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, ws, None,
+                                     bool(nchw_out and groupsort))
 
     def forward_nchw_fused(self, x: torch.Tensor, mu: torch.Tensor, sd, groupsort: bool) -> torch.Tensor:
         """forward_hwcb_fused of the network's first layer straight from the NCHW input x [B][C][n][n]

@@ -68,6 +68,7 @@ class KWLargeConcat(nn.Module):
 
         self.spatial_major = True
         self.fused_transforms = True      # sconv.hip rfft2 / irfft2 (+ GroupSort) around the GEMMs
+        self.nchw_last = True             # the last conv's transform writes the flatten's NCHW order
 
     def can_take_nchw(self, x) -> bool:
         """Whether forward(x, norm=...) can run the first conv straight from the NCHW input."""
@@ -101,12 +102,15 @@ class KWLargeConcat(nn.Module):
             h = x.permute(2, 3, 1, 0).contiguous()
             if getattr(self, "after_conv_hook", None) is not None:
                 self.after_conv_hook(-1)
+        nchw = False
         while not isinstance(mods[i], nn.Flatten):
             m = mods[i]
             if isinstance(m, CayleyConv):
                 gs = i + 1 < len(mods) and isinstance(mods[i + 1], GroupSort)
                 if self.fused_transforms and h.shape[0] // (2 if m.downsample else 1) <= 32:
-                    h = m.forward_hwcb_fused(h, gs)     # transforms (+ GroupSort) in HIP kernels
+                    # the last conv (+ GroupSort) writes NCHW: the flatten below is then a view
+                    nchw = bool(self.nchw_last and gs and i + 2 < len(mods) and isinstance(mods[i + 2], nn.Flatten))
+                    h = m.forward_hwcb_fused(h, gs, nchw_out=nchw)     # transforms (+ GroupSort) in HIP kernels
                     i += 2 if gs else 1
                     if getattr(self, "after_conv_hook", None) is not None:
                         self.after_conv_hook(nconv)
@@ -121,7 +125,7 @@ class KWLargeConcat(nn.Module):
             else:
                 h = m(h)
             i += 1
-        h = h.permute(3, 2, 0, 1).reshape(h.shape[3], -1)
+        h = h.reshape(h.shape[0], -1) if nchw else h.permute(3, 2, 0, 1).reshape(h.shape[3], -1)
         return linear_head(mods[i + 1:], h)
 
 

@@ -517,19 +517,23 @@ def block_inverse(M: torch.Tensor, out: Optional[torch.Tensor] = None,
 
 
 def sconv_rfft2(x: Optional[torch.Tensor], n: int, C: int, B: int, downsample: bool = False,
-                gy: Optional[torch.Tensor] = None, code: Optional[torch.Tensor] = None) -> torch.Tensor:
+                gy: Optional[torch.Tensor] = None, code: Optional[torch.Tensor] = None,
+                nchw: bool = False) -> torch.Tensor:
     """fiode_sconv_rfft2: spatial-major x [n][n][C][B] (downsample: [2n][2n][C/4][B]) -> complex64
-    [n (n/2+1), C, B].  With gy/code: the transform of GroupSort's backward of gy [n][n][C][B]."""
+    [n (n/2+1), C, B].  With gy/code: the transform of GroupSort's backward of gy [n][n][C][B]
+    (nchw: gy [B][C][n][n] and codes [B][C/2][n][n], as sconv_irfft2(nchw=True) wrote them)."""
     src = gy if gy is not None else x
     dev = src.device
+    if nchw and gy is None:
+        raise ValueError("sconv_rfft2: nchw only for the GroupSort-backward input (gy)")
     if gy is not None:
-        gy = _need(gy, "gy", (n, n, C, B), torch.float32, dev)
-        code = _need(code, "code", (n, n, C // 2, B), torch.uint8, dev)
+        gy = _need(gy, "gy", (B, C, n, n) if nchw else (n, n, C, B), torch.float32, dev)
+        code = _need(code, "code", (B, C // 2, n, n) if nchw else (n, n, C // 2, B), torch.uint8, dev)
     else:
         shape = (2 * n, 2 * n, C // 4, B) if downsample else (n, n, C, B)
         x = _need(x, "x", shape, torch.float32, dev)
     X = torch.empty((n * (n // 2 + 1), C, B), dtype=torch.complex64, device=dev)
-    cfg = L.SconvConfig(n, C, B, int(bool(downsample)))
+    cfg = L.SconvConfig(n, C, B, int(bool(downsample)), int(bool(nchw)))
     L.check(L.lib().fiode_sconv_rfft2(_stream(dev), ct.byref(cfg), _ptr(x), _ptr(gy), _ptr(code), X.data_ptr()),
             "fiode_sconv_rfft2")
     return X
@@ -545,24 +549,28 @@ def sconv_rfft2_nchw(x: torch.Tensor, mu: torch.Tensor, sd: Optional[torch.Tenso
     if sd is not None:
         sd = _need(sd.detach().reshape(-1), "sd", (C,), torch.float32, dev)
     X = torch.empty((n * (n // 2 + 1), C, B), dtype=torch.complex64, device=dev)
-    cfg = L.SconvConfig(n, C, B, 0)
+    cfg = L.SconvConfig(n, C, B, 0, 0)
     L.check(L.lib().fiode_sconv_rfft2_nchw(_stream(dev), ct.byref(cfg), x.data_ptr(), mu.data_ptr(), _ptr(sd),
                                            X.data_ptr()), "fiode_sconv_rfft2_nchw")
     return X
 
 
 def sconv_irfft2(Y: torch.Tensor, n: int, C: int, B: int, bias: Optional[torch.Tensor] = None,
-                 groupsort: bool = False, downsample: bool = False):
+                 groupsort: bool = False, downsample: bool = False, nchw: bool = False):
     """fiode_sconv_irfft2: complex64 [n (n/2+1), C, B] -> y [n][n][C][B] (+ bias; GroupSort with its
-    comparison codes [n][n][C/2][B]; or downsample: scattered to [2n][2n][C/4][B])."""
+    comparison codes [n][n][C/2][B]; or downsample: scattered to [2n][2n][C/4][B]; nchw: y
+    [B][C][n][n], codes [B][C/2][n][n])."""
     dev = Y.device
     Y = _need(Y, "Y", (n * (n // 2 + 1), C, B), torch.complex64, dev)
     if bias is not None:
         bias = _need(bias.detach(), "bias", (C,), torch.float32, dev)
-    shape = (2 * n, 2 * n, C // 4, B) if downsample else (n, n, C, B)
+    if nchw and downsample:
+        raise ValueError("sconv_irfft2: nchw and downsample together")
+    shape = (2 * n, 2 * n, C // 4, B) if downsample else ((B, C, n, n) if nchw else (n, n, C, B))
     y = torch.empty(shape, dtype=torch.float32, device=dev)
-    code = torch.empty((n, n, C // 2, B), dtype=torch.uint8, device=dev) if groupsort else None
-    cfg = L.SconvConfig(n, C, B, int(bool(downsample)))
+    code = (torch.empty((B, C // 2, n, n) if nchw else (n, n, C // 2, B), dtype=torch.uint8, device=dev)
+            if groupsort else None)
+    cfg = L.SconvConfig(n, C, B, int(bool(downsample)), int(bool(nchw)))
     L.check(L.lib().fiode_sconv_irfft2(_stream(dev), ct.byref(cfg), Y.data_ptr(), _ptr(bias), int(bool(groupsort)),
                                        y.data_ptr(), _ptr(code)), "fiode_sconv_irfft2")
     return y, code

@@ -405,6 +405,9 @@ typedef struct fiode_sconv_config {
   int32_t C;             /* channels of the transformed tensor (after space-to-channel)         */
   int32_t B;             /* batch                                                               */
   int32_t downsample;    /* rfft2: gather x from [2n][2n][C/4][B]; irfft2: scatter y to it       */
+  int32_t nchw;          /* irfft2's y and rfft2's gy in NCHW [B][C][n][n], the GroupSort codes in
+                          * [B][C/2][n][n] (the last conv, whose output the flatten reads as (C, h, w)
+                          * features); not with downsample                                          */
 } fiode_sconv_config;
 /* X = rfft2(x) over (h, w).  With gy != NULL the input is the GroupSort backward of gy (d/dout
  * [n][n][C][B]) with the comparison codes [n][n][C/2][B] of the forward (x unused). */

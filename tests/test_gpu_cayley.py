@@ -213,8 +213,9 @@ def test_spatial_major_backbone_matches_nchw():
 
 def test_normalized_backbone_fused_input_bit_identical():
     """NormalizedBackbone: the first conv's transform reading the raw NCHW input and normalising on
-    load (fiode_sconv_rfft2_nchw) = Normalize's spatial-major kernel + the transform, bit for bit
-    (forward and every parameter gradient)."""
+    load (fiode_sconv_rfft2_nchw) = Normalize's spatial-major kernel + the transform, and the last
+    conv writing NCHW (its GroupSort-backward transform reading NCHW) = the permute copies, bit for
+    bit (forward and every parameter gradient)."""
     from fiode_amd.models import make_ortho_KWLarge_Concat
     dev = _dev()
     torch.manual_seed(1)
@@ -224,6 +225,7 @@ def test_normalized_backbone_fused_input_bit_identical():
     outs = []
     for fused in (False, True):
         bb.fused_input = fused
+        bb[1].nchw_last = fused     # and the last conv writing the flatten's NCHW order directly
         bb.zero_grad()
         y = bb(x)
         y.square().sum().backward()
