@@ -312,6 +312,9 @@ def odetrain_evals(cfg: L.OdeTrainConfig) -> int:
     return E
 
 
+ODETRAIN_STATS_ZERO = False     # tools/ab_step.py stats_zero: the torch zero fill before the solve
+
+
 def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
                      cfg: L.OdeTrainConfig, masks: Optional[torch.Tensor] = None,
                      offset_dev: Optional[torch.Tensor] = None):
@@ -334,7 +337,8 @@ def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, 
     ws = torch.empty(lib.fiode_odetrain_workspace_bytes(ct.byref(cfg)), dtype=torch.uint8, device=dev)
     ws_w, cw = _weights_c(weights, dev)
     y = torch.empty((B, C), dtype=torch.float32, device=dev)
-    stats = torch.zeros(8, dtype=torch.int32, device=dev)
+    # k_ot_masks zeroes the stats words itself (a zero fill here ran on the chain ahead of the solve)
+    stats = (torch.zeros if ODETRAIN_STATS_ZERO else torch.empty)(8, dtype=torch.int32, device=dev)
     dc = dyn.to_c()
     rc = lib.fiode_odetrain_forward(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(),
                                     h0.data_ptr(), _ptr(masks), _ptr(offset_dev), y.data_ptr(), stats.data_ptr(),

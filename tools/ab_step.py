@@ -266,6 +266,13 @@ def nchw_last_off(m):
     m.init_coordinates.param_map[1].nchw_last = False    # the flatten's permute copies (before r05bo)
 
 
+def pre_solve_old(m):
+    from fiode_amd import ops as OPS
+    OPS.ODETRAIN_STATS_ZERO = True          # the stats zero fill and the Q3 copy on the chain (before r05bw)
+    m.dyn_fun.q3_contiguous = False
+    RESTORE.append(lambda: setattr(OPS, "ODETRAIN_STATS_ZERO", False))
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -273,7 +280,7 @@ def dyn_wgrad_main(m):
 
 
 ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
-       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "cgemm_wgrad_on": cgemm_wgrad_on, "cgemm_thin_lib": cgemm_thin_lib, "h0_repeat": h0_repeat, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "cgemm_dx_lib": cgemm_dx_lib, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
+       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "cgemm_wgrad_on": cgemm_wgrad_on, "cgemm_thin_lib": cgemm_thin_lib, "h0_repeat": h0_repeat, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "pre_solve_old": pre_solve_old, "cgemm_dx_lib": cgemm_dx_lib, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
        "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
