@@ -684,10 +684,8 @@ class _SpectralConvFn(torch.autograd.Function):
         G = rfft2(d/dpre),  dQ = (w_kb / n^2) G X^H,  dx = irfft2(Q^H G),  dbias = sum_b Re G[0]."""
 
     @staticmethod
-    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, wstream=None, norm=None,
-                nchw_out: bool = False):
+    def forward(ctx, x, Q, bias, n: int, downsample: bool, groupsort: bool, norm=None, nchw_out: bool = False):
         from . import ops
-        ctx.wstream = wstream
         nf, cout, cin = Q.shape
         if norm is not None:     # x: the NCHW network input, normalised on load (no input gradient)
             B = x.shape[0]
@@ -695,8 +693,7 @@ class _SpectralConvFn(torch.autograd.Function):
         else:
             B = x.shape[-1]
             X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
-        own = SCONV_CGEMM and not (SCONV_CGEMM_LIB_THIN and cout <= 32 and cin >= 128)
-        Y = ops.cgemm(Q.detach(), X) if own else torch.matmul(Q.detach(), X)
+        Y = ops.cgemm(Q.detach(), X)
         y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort,
                                    nchw=nchw_out)
         ctx.save_for_backward(X, Q, code)
@@ -725,40 +722,10 @@ class _SpectralConvFn(torch.autograd.Function):
                 w = torch.where((kb == 0) | (kb == n // 2), 1.0, 2.0) / float(n * n)
                 wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
 
-        def qgrad():        # dL/dQ = w G X^H (fiode_cgemm with the rfft weights folded in)
-            if SCONV_CGEMM and SCONV_CGEMM_WGRAD:
-                return ops.cgemm(G, X, conj_trans_b=True, scale=wq)
-            return torch.matmul(G, X.mH) * wq
-
-        def wgrad():
-            gq = qgrad() if need_q else None
+        def wgrad():        # dL/dQ = w G X^H (the library GEMM: see the note on fiode_cgemm below)
+            gq = torch.matmul(G, X.mH) * wq if need_q else None
             gbias = G[0].real.sum(-1) if need_b else None
             return gq, gbias
-        ws = ctx.wstream
-        ctx.wstream = None
-        if ws is not None and CONV_WGRAD_MAPSTREAM and G.is_cuda and (need_q or need_b):
-            # the weight gradient on the layer's map stream, where its consumer (the stored map's
-            # backward, then the layer's early update) runs: no join -- the step's stream goes on
-            # with dL/dx while it runs.  The bias gradient (read by the optimizer's final step) on
-            # the step's stream, or with CONV_WGRAD_MAPSTREAM_BIAS on the map stream too, joined
-            # through conv_wgrad_join (GraphTrainStep, after the backward).
-            cur = torch.cuda.current_stream(G.device)
-            ws.wait_stream(cur)
-            with torch.cuda.stream(ws):
-                gQ = qgrad() if need_q else None
-                if need_b and CONV_WGRAD_MAPSTREAM_BIAS:
-                    gb = G[0].real.sum(-1)
-                    ev = torch.cuda.Event()
-                    ev.record(ws)
-                    _CONV_WGRAD_EVENTS.append(ev)
-                    gb.record_stream(cur)
-            G.record_stream(ws)
-            X.record_stream(ws)
-            if need_b and not CONV_WGRAD_MAPSTREAM_BIAS:
-                gb = G[0].real.sum(-1)
-            if need_x:
-                gx, _ = ops.sconv_irfft2(_q_h_g(Q, G), n, cin, B, downsample=downsample)
-            return gx, gQ, gb, None, None, None, None, None, None
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
         # critical chain), on the side stream of the linear head's, joined before returning
         side = _head_stream(G.device) if (CONV_WGRAD_SIDE and G.is_cuda and need_x and (need_q or need_b)) else None
@@ -778,59 +745,29 @@ class _SpectralConvFn(torch.autograd.Function):
                     t.record_stream(cur)
         else:
             gQ, gb = wgrad()
-        return gx, gQ, gb, None, None, None, None, None, None
+        return gx, gQ, gb, None, None, None, None, None
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
-# the per-frequency channel products Q X and Q^H G by fiode_cgemm (cgemm.hip) instead of torch.matmul
-# (the library's batched complex GEMM: one 128 x 64 tile per frequency; the n = 8 layer's forward
-# 41 -> 16 us, its input gradient 17 -> 16, conv 3's 16 -> 10, conv 1's forward 13 -> 10 us; step
-# -25 to -40 us in the alternating A/B, profiles/r05bd)
-SCONV_CGEMM = os.environ.get("FIODE_SCONV_CGEMM", "1") != "0"
-# w G X^H in one fiode_cgemm launch too: measured 10-20 us SLOWER in the step than the library GEMM +
-# the scale kernel (profiles/r05bj), so off
-SCONV_CGEMM_WGRAD = os.environ.get("FIODE_SCONV_CGEMM_WGRAD", "0") != "0"
-
-
-# the library for the 32-row forward products over K >= 128 (conv 2): 11.6 vs 15 us per call under
-# the profiler, but 13 us SLOWER in the step's interleaved A/B (profiles/r05bk): off
-SCONV_CGEMM_LIB_THIN = False
-SCONV_CGEMM_DX = True            # Q^H G by fiode_cgemm (the library: equal within 7 us, r05bk)
-
-
+# The per-frequency channel products Q X and Q^H G are fiode_cgemm (cgemm.hip), not torch.matmul (the
+# library's batched complex GEMM: one 128 x 64 tile per frequency; the n = 8 layer's forward 41 ->
+# 16 us, conv 3's input gradient 16 -> 10, conv 1's forward 13 -> 10 us; step -25 to -40 us in the
+# alternating A/B, profiles/r05bd).  The weight gradient w G X^H stays the library GEMM + the scale on
+# the side stream: one fiode_cgemm launch (conjugate-transposed B, w folded in) measured 10-20 us
+# slower in the step (profiles/r05bj), as did the library for conv 2's forward (r05bk).
 def _q_h_g(Q, G):
     from . import ops
-    if SCONV_CGEMM and SCONV_CGEMM_DX:
-        return ops.cgemm(Q.detach(), G, conj_trans_a=True)
-    return torch.matmul(Q.detach().mH, G)
+    return ops.cgemm(Q.detach(), G, conj_trans_a=True)
+
 
 CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
-# a layer whose map is computed ahead with an early update (GraphTrainStep on one rank): its weight /
-# bias gradients on the layer's map stream instead of the head's side stream joined before returning
-CONV_WGRAD_MAPSTREAM = os.environ.get("FIODE_CONV_WGRAD_MAPSTREAM", "0") != "0"
-CONV_WGRAD_MAPSTREAM_BIAS = False
-_CONV_WGRAD_EVENTS: list = []
 
 
-def conv_wgrad_join(stream) -> None:
-    """Make ``stream`` wait for the conv bias gradients computed on the layers' map streams in the
-    backward that just ran (CONV_WGRAD_MAPSTREAM): call before the optimizer step reads them."""
-    while _CONV_WGRAD_EVENTS:
-        stream.wait_event(_CONV_WGRAD_EVENTS.pop())
-
-# The conv layers' map-ahead work (map backward, early update, refresh) runs on one stream per layer
-# (False) or on one stream shared by all layers (True; tools/ab_step.py conv_one_stream).
-CONV_STREAM_SHARED = False
-_CONV_STREAMS = {}
-
-
+# The conv layers' map-ahead work (map backward, early update, refresh) runs on one stream per layer.
+# (Their weight gradients on those streams instead of the head's side stream -- no join: 110-140 us
+# SLOWER in the step, profiles/r05an -- and one stream shared by all layers were measured and removed.)
 def _conv_map_stream(device) -> "torch.cuda.Stream":
-    if not CONV_STREAM_SHARED:
-        return torch.cuda.Stream(device)
-    key = str(device)
-    if key not in _CONV_STREAMS:
-        _CONV_STREAMS[key] = torch.cuda.Stream(device)
-    return _CONV_STREAMS[key]
+    return torch.cuda.Stream(device)
 
 
 class CayleyConv(nn.Conv2d):
@@ -851,7 +788,6 @@ class CayleyConv(nn.Conv2d):
         self._n = None
         self._pre = None
         self._store = None              # map computed ahead (pipeline_on), else None
-        self._wstream = None            # the stream of the stored map's backward, for the next apply
 
     def _load_from_state_dict(self, *args, **kw):
         super()._load_from_state_dict(*args, **kw)
@@ -938,11 +874,7 @@ class CayleyConv(nn.Conv2d):
                 Q = _SpectralCayleyStoredFn.apply(self.weight, self.alpha, n, st)
             main.wait_stream(side)
             self._pre = None
-            # the weight gradients go to this stream only with the early update (one rank): there
-            # the stored map's backward and the update consume them on it
-            self._wstream = side if st.get("on_grads") is not None else None
             return Q
-        self._wstream = None
         if self._pre is not None and self.training and self._n == n:
             Q = _take(self._pre)
         else:
@@ -972,8 +904,7 @@ class CayleyConv(nn.Conv2d):
         nchw_out (GroupSort only) [B][cout][n][n] -- the last conv, whose output the flatten reads."""
         n = x.shape[0] // 2 if self.downsample else x.shape[0]
         Q = self._take_spectral(n, x.device)
-        ws, self._wstream = self._wstream, None
-        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, ws, None,
+        return _SpectralConvFn.apply(x, Q, self.bias, n, self.downsample, groupsort, None,
                                      bool(nchw_out and groupsort))
 
     def forward_nchw_fused(self, x: torch.Tensor, mu: torch.Tensor, sd, groupsort: bool) -> torch.Tensor:
@@ -983,8 +914,7 @@ class CayleyConv(nn.Conv2d):
         gradient)."""
         n = x.shape[-1]
         Q = self._take_spectral(n, x.device)
-        ws, self._wstream = self._wstream, None
-        return _SpectralConvFn.apply(x, Q, self.bias, n, False, groupsort, ws, (mu, sd))
+        return _SpectralConvFn.apply(x, Q, self.bias, n, False, groupsort, (mu, sd))
 
     def forward_hwcb(self, x: torch.Tensor) -> torch.Tensor:
         """The same map on spatial-major activations [n, n, C, B] (the conv stack's HBM layout):

@@ -31,8 +31,6 @@ class LipsLinear(nn.Linear):
 
 
 class OrthoClassDynProjectSimplexLips(nn.Module):
-    q3_contiguous = True        # effective_weights' Q3 contiguous (tools/ab_step.py q3_view: the view)
-
     def __init__(self, n_hidden=10, activation="ReLU", dropout=0.5, mlp_size=128, kappa=5.0, kappa_length=3e4,
                  alpha_1=100.0, alpha_2=5.0, sigma_1=0.02, scale_nominal=False, x_dim=10, cayley=True):
         super().__init__()
@@ -87,7 +85,7 @@ class OrthoClassDynProjectSimplexLips(nn.Module):
             Qb = cayley_scaled(Wb, ab, per_matrix=True)
             # Q3 made contiguous here (on the maps' prefetch stream): the solve and the fan-out read
             # it contiguous, and the copy otherwise ran on the step's chain right before the solve
-            Q3 = Qb[2].t().contiguous() if self.q3_contiguous else Qb[2].t()
+            Q3 = Qb[2].t().contiguous()
             return {"Q1": Qb[0], "b1": l1.bias, "Qx": Qb[1], "bx": lx.bias,
                     "Q2": self.mlp_to_mlp.effective_weight(), "b2": self.mlp_to_mlp.bias,
                     "Q3": Q3, "b3": l3.bias}

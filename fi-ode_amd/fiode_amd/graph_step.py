@@ -365,8 +365,6 @@ class GraphTrainStep:
         loss = m.compute_loss(self.static_x, self.static_y, self.static_x.shape[0], self.act)
         self._arm_guard(loss)
         loss.backward(self._unit_grad(loss))
-        from .cayley import conv_wgrad_join
-        conv_wgrad_join(torch.cuda.current_stream(self.static_x.device))
         if overlap:
             self.reducer.finish()                 # the last buckets, join the comm stream, 1/world
         elif self.comm != "none":

@@ -309,8 +309,6 @@ class DecisionBoundary(nn.Module):
 class UniformInitFun(nn.Module):
     """dynamics/init_coordinates.py:38-44: h0 = 1/C, static = param_map(x)."""
 
-    h0_view = True          # False: the reference's repeat (tools/ab_step.py h0_repeat)
-
     def __init__(self, h_dims=(10,), param_map: Optional[nn.Module] = None):
         super().__init__()
         self.h_dims = tuple(h_dims)
@@ -322,10 +320,7 @@ class UniformInitFun(nn.Module):
         # h0 as a broadcast view of the buffer (the reference's repeat is a copy kernel at the head of
         # the captured step's chain, and the fused training loss does not read it); an in-place write
         # into the view raises instead of touching the buffer
-        if self.h0_view:
-            h0 = tuple(getattr(self, f"h0_{i}")[None].expand(x.shape[0], -1).to(x.device) for i in range(len(self.h_dims)))
-        else:
-            h0 = tuple(getattr(self, f"h0_{i}")[None].repeat(x.shape[0], 1).to(x.device) for i in range(len(self.h_dims)))
+        h0 = tuple(getattr(self, f"h0_{i}")[None].expand(x.shape[0], -1).to(x.device) for i in range(len(self.h_dims)))
         return self.param_map(x), h0
 
 

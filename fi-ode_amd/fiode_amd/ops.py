@@ -312,7 +312,6 @@ def odetrain_evals(cfg: L.OdeTrainConfig) -> int:
     return E
 
 
-ODETRAIN_STATS_ZERO = False     # tools/ab_step.py stats_zero: the torch zero fill before the solve
 
 
 def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, torch.Tensor], dyn: DynCfg,
@@ -338,7 +337,7 @@ def odetrain_forward(x_feat: torch.Tensor, h0: torch.Tensor, weights: Dict[str, 
     ws_w, cw = _weights_c(weights, dev)
     y = torch.empty((B, C), dtype=torch.float32, device=dev)
     # k_ot_masks zeroes the stats words itself (a zero fill here ran on the chain ahead of the solve)
-    stats = (torch.zeros if ODETRAIN_STATS_ZERO else torch.empty)(8, dtype=torch.int32, device=dev)
+    stats = torch.empty(8, dtype=torch.int32, device=dev)
     dc = dyn.to_c()
     rc = lib.fiode_odetrain_forward(_stream(dev), ct.byref(cfg), ct.byref(dc), ct.byref(cw), x_feat.data_ptr(),
                                     h0.data_ptr(), _ptr(masks), _ptr(offset_dev), y.data_ptr(), stats.data_ptr(),

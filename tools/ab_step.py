@@ -93,10 +93,6 @@ def seed1000(m):
     m.seed = 1000
 
 
-def conv_one_stream(m):
-    from fiode_amd import cayley as CY
-    CY.CONV_STREAM_SHARED = True          # read when GraphTrainStep turns the maps-ahead pipeline on
-    RESTORE.append(lambda: setattr(CY, "CONV_STREAM_SHARED", False))
 
 
 def old_seed(m):
@@ -207,23 +203,10 @@ def conv_wgrad_main(m):
     RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_SIDE", True))
 
 
-def conv_wgrad_head(m):
-    from fiode_amd import cayley as CY
-    CY.CONV_WGRAD_MAPSTREAM = False   # the conv weight gradients on the head's side stream, joined (r05af)
 
 
-def conv_wgrad_map(m):
-    from fiode_amd import cayley as CY
-    CY.CONV_WGRAD_MAPSTREAM = True    # the conv weight gradients on the layers' map streams, bias on the step's
-    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM", False))
 
 
-def conv_wgrad_bias_side(m):
-    from fiode_amd import cayley as CY
-    CY.CONV_WGRAD_MAPSTREAM = True    # ... and the bias gradients on the map streams too, joined at the end
-    CY.CONV_WGRAD_MAPSTREAM_BIAS = True
-    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM_BIAS", False))
-    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_MAPSTREAM", False))
 
 
 def cap_hi(m):
@@ -236,26 +219,12 @@ def ode_lo(m):
     m._ode_prio = 0                   # the train_ode solve's stream at normal priority
 
 
-def cgemm_wgrad_on(m):
-    from fiode_amd import cayley as CY
-    CY.SCONV_CGEMM_WGRAD = True       # the conv weight gradient w G X^H by fiode_cgemm (r05bj: slower)
-    RESTORE.append(lambda: setattr(CY, "SCONV_CGEMM_WGRAD", False))
 
 
-def cgemm_thin_lib(m):
-    from fiode_amd import cayley as CY
-    CY.SCONV_CGEMM_LIB_THIN = True    # conv 2's forward product by the library (r05bk: slower)
-    RESTORE.append(lambda: setattr(CY, "SCONV_CGEMM_LIB_THIN", False))
 
 
-def cgemm_dx_lib(m):
-    from fiode_amd import cayley as CY
-    CY.SCONV_CGEMM_DX = False         # Q^H G by the library
-    RESTORE.append(lambda: setattr(CY, "SCONV_CGEMM_DX", True))
 
 
-def h0_repeat(m):
-    m.init_coordinates.h0_view = False     # h0 as the reference's repeat copy (before r05bl)
 
 
 def norm_unfused(m):
@@ -266,11 +235,6 @@ def nchw_last_off(m):
     m.init_coordinates.param_map[1].nchw_last = False    # the flatten's permute copies (before r05bo)
 
 
-def pre_solve_old(m):
-    from fiode_amd import ops as OPS
-    OPS.ODETRAIN_STATS_ZERO = True          # the stats zero fill and the Q3 copy on the chain (before r05bw)
-    m.dyn_fun.q3_contiguous = False
-    RESTORE.append(lambda: setattr(OPS, "ODETRAIN_STATS_ZERO", False))
 
 
 def dyn_wgrad_main(m):
@@ -279,14 +243,15 @@ def dyn_wgrad_main(m):
     RESTORE.append(lambda: setattr(LY, "DYN_WGRAD_SIDE", True))
 
 
+# variants of paths removed from the product after their A/B (the conv weight gradients on the map
+# streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
+# zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
 ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
-       "conv_wgrad_head": conv_wgrad_head, "cap_hi": cap_hi, "ode_lo": ode_lo, "cgemm_wgrad_on": cgemm_wgrad_on, "cgemm_thin_lib": cgemm_thin_lib, "h0_repeat": h0_repeat, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "pre_solve_old": pre_solve_old, "cgemm_dx_lib": cgemm_dx_lib, "conv_wgrad_map": conv_wgrad_map, "conv_wgrad_bias_side": conv_wgrad_bias_side,
-       "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
+       "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
        "unfused_loss": unfused_loss, "ode_on_main": ode_on_main, "seed1000": seed1000, "pf_conv0": pf_conv0,
-       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "old_seed": old_seed,
-       "conv_one_stream": conv_one_stream}
+       "pf_conv1": pf_conv1, "dense_bwd_side": dense_bwd_side, "lib_gmn": lib_gmn, "old_seed": old_seed}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["default", "no_ahead"]
 VARIANTS = {k: ALL[k] for k in names}
