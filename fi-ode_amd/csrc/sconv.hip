@@ -95,6 +95,8 @@ struct SArgs {
   const float* xn;               // rfft2 input in NCHW [B][C][n][n], normalised on load (the backbone's
   const float* mu;               //   first layer: Normalize fused, models.py:17-26), mu / sd [C]
   const float* sd;               //   (sd nullable)
+  const c32* Q;                  // irfft2 with the channel product fused (fiode_sconv_irfft2_qx): Y[f] = Q[f] Xq[f]
+  const c32* Xq;                 //   on load, Q [f][C][K], Xq [f][K][B], K <= 4 (conv 1: the 3 input channels)
 };
 
 __device__ __forceinline__ int64_t act_index(const SArgs& a, int h, int w, int c, int b) {
@@ -288,7 +290,9 @@ struct IGeo {
   __device__ static int pix(int ch, int bt, int h) { return 2 * (ch * CS + bt * ZS + h * H); }
 };
 
-template <int N, int NCH>
+// KQ > 0: Y[f][c][b] = sum_k Q[f][c][k] Xq[f][k][b] computed on load (k in order, products then
+// sums in float32), instead of read from a GEMM output
+template <int N, int NCH, int KQ>
 __device__ __forceinline__ void irfft2_inplace(const SArgs& a, int c0, int c1, int b0, c32* Ys) {
   typedef IGeo<N> G;
   constexpr int BTI = G::BTI, H = G::H, NT = G::NT;
@@ -303,7 +307,25 @@ __device__ __forceinline__ void irfft2_inplace(const SArgs& a, int c0, int c1, i
       const int ch = idx / (BTI * N * H), r = idx - ch * (BTI * N * H);
       const int bt = r % BTI, f = r / BTI;
       const int b = min(b0 + bt, a.B - 1);
-      const c32 v = a.Y[((int64_t)f * a.C + (ch ? c1 : c0)) * a.B + b];
+      c32 v;
+      if constexpr (KQ == 0) {
+        v = a.Y[((int64_t)f * a.C + (ch ? c1 : c0)) * a.B + b];
+      } else {
+        const c32* q = a.Q + ((int64_t)f * a.C + (ch ? c1 : c0)) * KQ;
+        const c32* xq = a.Xq + (int64_t)f * KQ * a.B + b;
+        c32 qk[KQ > 0 ? KQ : 1], xk[KQ > 0 ? KQ : 1];
+#pragma unroll
+        for (int k = 0; k < KQ; ++k) {
+          qk[k] = q[k];
+          xk[k] = xq[(int64_t)k * a.B];
+        }
+        v = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < KQ; ++k) {
+          v.x += qk[k].x * xk[k].x - qk[k].y * xk[k].y;
+          v.y += qk[k].x * xk[k].y + qk[k].y * xk[k].x;
+        }
+      }
       Ys[ch * G::CS + bt * G::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
     }
   }
@@ -348,7 +370,7 @@ __device__ __forceinline__ void irfft2_inplace(const SArgs& a, int c0, int c1, i
 
 // ---- y = irfft2(Y) (+ bias, GroupSort) or the space-to-channel scatter ---------------------------
 // gs: grid.x = C/2 channel pairs (both channels of a pair in one workgroup); else grid.x = C channels.
-template <int N>
+template <int N, int KQ>
 __global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_irfft2(SArgs a) {
   typedef IGeo<N> G;
   constexpr int BTI = G::BTI, NT = G::NT;
@@ -357,7 +379,7 @@ __global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_ir
   const int b0 = blockIdx.y * BTI, tid = threadIdx.x;
   if (a.gs) {
     const int half = a.C >> 1, c0 = blockIdx.x, c1 = c0 + half;
-    irfft2_inplace<N, 2>(a, c0, c1, b0, Ys);
+    irfft2_inplace<N, 2, KQ>(a, c0, c1, b0, Ys);
     const float bb0 = a.bias ? a.bias[c0] : 0.f, bb1 = a.bias ? a.bias[c1] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
       const int bt = a.nchw ? idx / (N * N) : idx % BTI;
@@ -372,7 +394,7 @@ __global__ void __launch_bounds__((nthreads<N, bt_inv<N>(), true>())) k_sconv_ir
     (void)half;
   } else {
     const int c = blockIdx.x;
-    irfft2_inplace<N, 1>(a, c, c, b0, Ys);
+    irfft2_inplace<N, 1, KQ>(a, c, c, b0, Ys);
     const float bb = a.bias ? a.bias[c] : 0.f;
     for (int idx = tid; idx < BTI * N * N; idx += NT) {
       const int bt = a.nchw ? idx / (N * N) : idx % BTI;
@@ -461,24 +483,55 @@ extern "C" int fiode_sconv_rfft2_nchw(void* stream, const fiode_sconv_config* cf
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }
 
-extern "C" int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,
-                                  int32_t groupsort, float* y, uint8_t* code_out) {
-  SArgs a;
-  int rc = check(cfg, a);
-  if (rc) return rc;
-  a.gs = groupsort ? 1 : 0;
-  if (!Y || !y || (a.gs && (!code_out || (a.C & 1) || a.ds))) return FIODE_EINVAL;
-  a.Y = (const c32*)Y;
-  a.bias = bias;
-  a.y = y;
-  a.code_out = code_out;
+namespace {
+
+template <int KQ>
+hipError_t launch_irfft2(const SArgs& a, hipStream_t st) {
   const int gx = a.gs ? a.C / 2 : a.C;
   const int bt = a.n == 32 ? bt_inv<32>() : BT_I;
   const dim3 grid(gx, (a.B + bt - 1) / bt);
+  if (a.n == 8) hipLaunchKernelGGL((k_sconv_irfft2<8, KQ>), grid, dim3(nthreads<8, BT_I, true>()), 0, st, a);
+  else if (a.n == 16) hipLaunchKernelGGL((k_sconv_irfft2<16, KQ>), grid, dim3(nthreads<16, BT_I, true>()), 0, st, a);
+  else hipLaunchKernelGGL((k_sconv_irfft2<32, KQ>), grid, dim3(nthreads<32, bt_inv<32>(), true>()), 0, st, a);
+  return hipGetLastError();
+}
+
+int irfft2_common(const fiode_sconv_config* cfg, const float* bias, int32_t groupsort, float* y, uint8_t* code_out,
+                  SArgs& a) {
+  int rc = check(cfg, a);
+  if (rc) return rc;
+  a.gs = groupsort ? 1 : 0;
+  if (!y || (a.gs && (!code_out || (a.C & 1) || a.ds))) return FIODE_EINVAL;
+  a.bias = bias;
+  a.y = y;
+  a.code_out = code_out;
+  return FIODE_OK;
+}
+
+}  // namespace
+
+extern "C" int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,
+                                  int32_t groupsort, float* y, uint8_t* code_out) {
+  SArgs a;
+  const int rc = irfft2_common(cfg, bias, groupsort, y, code_out, a);
+  if (rc) return rc;
+  if (!Y) return FIODE_EINVAL;
+  a.Y = (const c32*)Y;
+  const hipError_t e = launch_irfft2<0>(a, (hipStream_t)stream);
+  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+extern "C" int fiode_sconv_irfft2_qx(void* stream, const fiode_sconv_config* cfg, const void* Q, const void* X,
+                                     int32_t K, const float* bias, int32_t groupsort, float* y, uint8_t* code_out) {
+  SArgs a;
+  const int rc = irfft2_common(cfg, bias, groupsort, y, code_out, a);
+  if (rc) return rc;
+  if (K < 1 || K > 4) return FIODE_ESHAPE;
+  if (!Q || !X) return FIODE_EINVAL;
+  a.Q = (const c32*)Q;
+  a.Xq = (const c32*)X;
   hipStream_t st = (hipStream_t)stream;
-  if (a.n == 8) hipLaunchKernelGGL(k_sconv_irfft2<8>, grid, dim3(nthreads<8, BT_I, true>()), 0, st, a);
-  else if (a.n == 16) hipLaunchKernelGGL(k_sconv_irfft2<16>, grid, dim3(nthreads<16, BT_I, true>()), 0, st, a);
-  else hipLaunchKernelGGL(k_sconv_irfft2<32>, grid, dim3(nthreads<32, bt_inv<32>(), true>()), 0, st, a);
-  const hipError_t e = hipGetLastError();
+  const hipError_t e = K == 1 ? launch_irfft2<1>(a, st) : K == 2 ? launch_irfft2<2>(a, st)
+                     : K == 3 ? launch_irfft2<3>(a, st) : launch_irfft2<4>(a, st);
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
 }

@@ -189,6 +189,8 @@ def _load():
         "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
         "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
         "fiode_sconv_rfft2_nchw": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
+        "fiode_sconv_irfft2_qx": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, ct.c_int32,
+                                             _vp, _vp]),
         "fiode_cgemm": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp,
                                    _vp, _vp, _vp]),
         "fiode_spectral_workspace_bytes": (ct.c_size_t, [ct.POINTER(SpectralConfig)]),

@@ -693,9 +693,13 @@ class _SpectralConvFn(torch.autograd.Function):
         else:
             B = x.shape[-1]
             X = ops.sconv_rfft2(x.detach(), n, cin, B, downsample=downsample)
-        Y = ops.cgemm(Q.detach(), X)
-        y, code = ops.sconv_irfft2(Y, n, cout, B, bias=None if bias is None else bias.detach(), groupsort=groupsort,
-                                   nchw=nchw_out)
+        bd = None if bias is None else bias.detach()
+        if cin <= SCONV_QX_MAX_K and not downsample:
+            # few input channels (conv 1: 3): the product formed in the inverse transform's loads
+            y, code = ops.sconv_irfft2_qx(Q.detach(), X, n, B, bias=bd, groupsort=groupsort, nchw=nchw_out)
+        else:
+            y, code = ops.sconv_irfft2(ops.cgemm(Q.detach(), X), n, cout, B, bias=bd, groupsort=groupsort,
+                                       nchw=nchw_out)
         ctx.save_for_backward(X, Q, code)
         ctx.cfg = (n, downsample, groupsort, bias is not None, cin, cout, B)
         ctx.nchw_out = nchw_out
@@ -755,6 +759,12 @@ _SPECTRAL_GRAD_WEIGHTS = {}
 # alternating A/B, profiles/r05bd).  The weight gradient w G X^H stays the library GEMM + the scale on
 # the side stream: one fiode_cgemm launch (conjugate-transposed B, w folded in) measured 10-20 us
 # slower in the step (profiles/r05bj), as did the library for conv 2's forward (r05bk).
+# conv layers with at most this many input channels (conv 1: 3) form Q X inside the inverse
+# transform's loads (fiode_sconv_irfft2_qx; the kernel's limit is 4): no GEMM launch, no [f][C][B]
+# product in HBM
+SCONV_QX_MAX_K = 4
+
+
 def _q_h_g(Q, G):
     from . import ops
     return ops.cgemm(Q.detach(), G, conj_trans_a=True)

@@ -579,6 +579,28 @@ def sconv_irfft2(Y: torch.Tensor, n: int, C: int, B: int, bias: Optional[torch.T
     return y, code
 
 
+def sconv_irfft2_qx(Q: torch.Tensor, X: torch.Tensor, n: int, B: int, bias: Optional[torch.Tensor] = None,
+                    groupsort: bool = False, nchw: bool = False):
+    """fiode_sconv_irfft2_qx: sconv_irfft2(Q @ X) with the per-frequency product formed in the
+    transform's loads (few input channels: Q [n (n/2+1), C, K], X [n (n/2+1), K, B], K <= 4)."""
+    dev = X.device
+    nf = n * (n // 2 + 1)
+    if Q.dim() != 3 or Q.shape[0] != nf:
+        raise ValueError(f"sconv_irfft2_qx: Q {tuple(Q.shape)} is not [{nf}, C, K]")
+    C, K = Q.shape[1], Q.shape[2]
+    Q = _need(Q.detach(), "Q", (nf, C, K), torch.complex64, dev)
+    X = _need(X.detach(), "X", (nf, K, B), torch.complex64, dev)
+    if bias is not None:
+        bias = _need(bias.detach(), "bias", (C,), torch.float32, dev)
+    y = torch.empty((B, C, n, n) if nchw else (n, n, C, B), dtype=torch.float32, device=dev)
+    code = (torch.empty((B, C // 2, n, n) if nchw else (n, n, C // 2, B), dtype=torch.uint8, device=dev)
+            if groupsort else None)
+    cfg = L.SconvConfig(n, C, B, 0, int(bool(nchw)))
+    L.check(L.lib().fiode_sconv_irfft2_qx(_stream(dev), ct.byref(cfg), Q.data_ptr(), X.data_ptr(), K, _ptr(bias),
+                                          int(bool(groupsort)), y.data_ptr(), _ptr(code)), "fiode_sconv_irfft2_qx")
+    return y, code
+
+
 def cgemm(A: torch.Tensor, B: torch.Tensor, conj_trans_a: bool = False, conj_trans_b: bool = False,
           scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fiode_cgemm: batched complex64 C[f] = scale[f] opA(A[f]) @ opB(B[f]); A [F, M, K] ([F, K, M]

@@ -421,6 +421,12 @@ FIODE_API int fiode_sconv_rfft2_nchw(void* stream, const fiode_sconv_config* cfg
  * of it over the channel halves and code_out [n][n][C/2][B] records max/min/tie. */
 FIODE_API int fiode_sconv_irfft2(void* stream, const fiode_sconv_config* cfg, const void* Y, const float* bias,
                                  int32_t groupsort, float* y, uint8_t* code_out);
+/* fiode_sconv_irfft2 with the per-frequency channel product of a few-input-channel conv fused into
+ * its loads: Y[f] = Q[f] X[f] is formed on the fly (conv 1: K = 3 input channels), no [f][C][B]
+ * GEMM output.  Q [f][C][K], X [f][K][B] complex64 (f = n (n/2 + 1)), 1 <= K <= 4 (else
+ * FIODE_ESHAPE); bias / groupsort / y / code_out as fiode_sconv_irfft2 (cfg->C = output channels). */
+FIODE_API int fiode_sconv_irfft2_qx(void* stream, const fiode_sconv_config* cfg, const void* Q, const void* X,
+                                    int32_t K, const float* bias, int32_t groupsort, float* y, uint8_t* code_out);
 
 /* Batched complex64 GEMM of the spectral convolutions' per-frequency channel products (CayleyConv
  * forward_hwcb; replaces torch.matmul on complex64 in fiode_amd/cayley.py _SpectralConvFn):
