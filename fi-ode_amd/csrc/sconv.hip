@@ -299,34 +299,50 @@ __device__ __forceinline__ void irfft2_inplace(const SArgs& a, int c0, int c1, i
   constexpr int NL = NCH * BTI * N * H;
   constexpr int TR = (NL + NT - 1) / NT;
   const int tid = threadIdx.x;
-  // all loads in flight together: a fixed trip count, unrolled
+  if constexpr (KQ == 0) {
+    // all loads in flight together: a fixed trip count, unrolled
 #pragma unroll
-  for (int t = 0; t < TR; ++t) {
-    const int idx = tid + t * NT;
-    if (idx < NL) {
-      const int ch = idx / (BTI * N * H), r = idx - ch * (BTI * N * H);
-      const int bt = r % BTI, f = r / BTI;
-      const int b = min(b0 + bt, a.B - 1);
-      c32 v;
-      if constexpr (KQ == 0) {
-        v = a.Y[((int64_t)f * a.C + (ch ? c1 : c0)) * a.B + b];
-      } else {
-        const c32* q = a.Q + ((int64_t)f * a.C + (ch ? c1 : c0)) * KQ;
+    for (int t = 0; t < TR; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL) {
+        const int ch = idx / (BTI * N * H), r = idx - ch * (BTI * N * H);
+        const int bt = r % BTI, f = r / BTI;
+        const int b = min(b0 + bt, a.B - 1);
+        const c32 v = a.Y[((int64_t)f * a.C + (ch ? c1 : c0)) * a.B + b];
+        Ys[ch * G::CS + bt * G::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
+      }
+    }
+  } else {
+    // one (image, frequency) per thread for every channel of the workgroup: X[f][k][b] read once
+    constexpr int NL1 = BTI * N * H;
+    constexpr int TR1 = (NL1 + NT - 1) / NT;
+#pragma unroll
+    for (int t = 0; t < TR1; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < NL1) {
+        const int bt = idx % BTI, f = idx / BTI;
+        const int b = min(b0 + bt, a.B - 1);
         const c32* xq = a.Xq + (int64_t)f * KQ * a.B + b;
-        c32 qk[KQ > 0 ? KQ : 1], xk[KQ > 0 ? KQ : 1];
+        c32 xk[KQ], qk[NCH][KQ];
 #pragma unroll
-        for (int k = 0; k < KQ; ++k) {
-          qk[k] = q[k];
-          xk[k] = xq[(int64_t)k * a.B];
+        for (int k = 0; k < KQ; ++k) xk[k] = xq[(int64_t)k * a.B];
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const c32* q = a.Q + ((int64_t)f * a.C + (ch ? c1 : c0)) * KQ;
+#pragma unroll
+          for (int k = 0; k < KQ; ++k) qk[ch][k] = q[k];
         }
-        v = make_float2(0.f, 0.f);
 #pragma unroll
-        for (int k = 0; k < KQ; ++k) {
-          v.x += qk[k].x * xk[k].x - qk[k].y * xk[k].y;
-          v.y += qk[k].x * xk[k].y + qk[k].y * xk[k].x;
+        for (int ch = 0; ch < NCH; ++ch) {
+          c32 v = make_float2(0.f, 0.f);
+#pragma unroll
+          for (int k = 0; k < KQ; ++k) {
+            v.x += qk[ch][k].x * xk[k].x - qk[ch][k].y * xk[k].y;
+            v.y += qk[ch][k].x * xk[k].y + qk[ch][k].y * xk[k].x;
+          }
+          Ys[ch * G::CS + bt * G::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
         }
       }
-      Ys[ch * G::CS + bt * G::ZS + f] = b0 + bt < a.B ? v : make_float2(0.f, 0.f);
     }
   }
   __syncthreads();
