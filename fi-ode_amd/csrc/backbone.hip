@@ -49,6 +49,69 @@ __global__ __launch_bounds__(256) void k_groupsort_bwd(const float* __restrict__
                                                   gmax_part(vb.z, va.z, gm.z, gn.z), gmax_part(vb.w, va.w, gm.w, gn.w));
 }
 
+// ---- the linear head's output layer (KWLargeConcat's last Linear, 512 -> x_dim = 10) ------------
+// out[b][j] = bias[j] + sum_k z[b][k] Q[j][k] for J <= 16 outputs: one wave per row b, lane l holds
+// the k = l, l + 64, ... partial sums of all J outputs, then a fixed butterfly over the 64 lanes
+// (run to run reproducible).  The library ran this 128 x 10 x 512 product on ONE workgroup (its
+// 16 x 256 tile): ~15 us on the forward chain.
+constexpr int HEAD_JMAX = 16;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// JT: the unrolled output count (J <= JT at run time)
+template <int JT>
+__global__ __launch_bounds__(256) void k_head_out(int B, int K, int J, const float* __restrict__ z,
+                                                 const float* __restrict__ Q, const float* __restrict__ bias,
+                                                 float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float acc[JT];
+#pragma unroll
+  for (int j = 0; j < JT; ++j) acc[j] = 0.f;
+  const float* zr = z + (int64_t)b * K;
+  for (int k = lane; k < K; k += 64) {
+    const float zv = zr[k];
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[j] += zv * (j < J ? Q[(int64_t)j * K + k] : 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < JT; ++j) acc[j] = wave_sum(acc[j]);
+  if (lane < J) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < JT; ++j) v = lane == j ? acc[j] : v;
+    out[(int64_t)b * J + lane] = v + (bias ? bias[lane] : 0.f);
+  }
+}
+
+// its input gradient through the preceding GroupSort: d = g Q (d[b][k] = sum_j g[b][j] Q[j][k], j in
+// order), then GroupSort's backward on the pair (k, k + K/2) of its input y: one thread per pair
+template <int JT>
+__global__ __launch_bounds__(256) void k_head_out_bwd_gs(int B, int K, int J, const float* __restrict__ g,
+                                                        const float* __restrict__ Q, const float* __restrict__ y,
+                                                        float* __restrict__ gx) {
+  const int half = K >> 1;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)B * half) return;
+  const int b = (int)(q / half), r = (int)(q - (int64_t)b * half);
+  float da = 0.f, db = 0.f;
+#pragma unroll
+  for (int j = 0; j < JT; ++j) {
+    if (j < J) {
+      const float gv = g[(int64_t)b * J + j];
+      da += gv * Q[(int64_t)j * K + r];
+      db += gv * Q[(int64_t)j * K + r + half];
+    }
+  }
+  const float ya = y[(int64_t)b * K + r], yb = y[(int64_t)b * K + r + half];
+  gx[(int64_t)b * K + r] = gmax_part(ya, yb, da, db);
+  gx[(int64_t)b * K + r + half] = gmax_part(yb, ya, da, db);
+}
+
 int check_gs(int64_t B, int64_t C, int64_t S, const void* p0, const void* p1) {
   if (B <= 0 || C <= 0 || S <= 0 || (C & 1)) return FIODE_ESHAPE;
   if (((C / 2) * S) % 4 != 0) return FIODE_ESHAPE;     // float4 lanes need (C/2)*S % 4 == 0
@@ -117,6 +180,31 @@ extern "C" int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int6
   const int64_t half_cs4 = (C / 2) * S / 4, cs4 = C * S / 4, n4 = B * half_cs4;
   hipLaunchKernelGGL(k_groupsort_bwd, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, g, gx,
                      n4, half_cs4, cs4);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
+
+extern "C" int fiode_head_out(void* stream, int32_t B, int32_t K, int32_t J, const float* z, const float* Q,
+                              const float* bias, float* out) {
+  if (B <= 0 || K <= 0 || J <= 0 || J > HEAD_JMAX) return FIODE_ESHAPE;
+  if (!z || !Q || !out) return FIODE_EINVAL;
+  const dim3 grid((unsigned)((B + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  if (J <= 10) hipLaunchKernelGGL(k_head_out<10>, grid, dim3(256), 0, st, B, K, (int)J, z, Q, bias, out);
+  else hipLaunchKernelGGL(k_head_out<HEAD_JMAX>, grid, dim3(256), 0, st, B, K, (int)J, z, Q, bias, out);
+  FIODE_HIP_CHECK(hipGetLastError());
+  return FIODE_OK;
+}
+
+extern "C" int fiode_head_out_backward_gs(void* stream, int32_t B, int32_t K, int32_t J, const float* g,
+                                          const float* Q, const float* y, float* gx) {
+  if (B <= 0 || K <= 0 || (K & 1) || J <= 0 || J > HEAD_JMAX) return FIODE_ESHAPE;
+  if (!g || !Q || !y || !gx) return FIODE_EINVAL;
+  const int64_t n = (int64_t)B * (K / 2);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (J <= 10) hipLaunchKernelGGL(k_head_out_bwd_gs<10>, grid, dim3(256), 0, st, B, K, (int)J, g, Q, y, gx);
+  else hipLaunchKernelGGL(k_head_out_bwd_gs<HEAD_JMAX>, grid, dim3(256), 0, st, B, K, (int)J, g, Q, y, gx);
   FIODE_HIP_CHECK(hipGetLastError());
   return FIODE_OK;
 }

@@ -158,6 +158,8 @@ def _load():
                                                        ct.c_size_t]),
         "fiode_groupsort_forward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp]),
         "fiode_groupsort_backward": (ct.c_int, [_vp, ct.c_int64, ct.c_int64, ct.c_int64, _vp, _vp, _vp]),
+        "fiode_head_out": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp]),
+        "fiode_head_out_backward_gs": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp, _vp]),
         "fiode_batched_inverse": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, _vp, ct.c_int64, _vp,
                                              ct.c_int64]),
         "fiode_block_inverse_workspace_bytes": (ct.c_size_t, [ct.c_int32]),

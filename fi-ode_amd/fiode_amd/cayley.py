@@ -543,7 +543,8 @@ class _LinearHeadFn(torch.autograd.Function):
         z1 = ops.groupsort_forward(y1, 1)
         y2 = torch.addmm(b2, z1, Q2.t())
         z2 = ops.groupsort_forward(y2, 1)
-        out = torch.addmm(b3, z2, Q3.t())
+        # the 512 -> 10 output layer: the library ran it on one workgroup (~15 us on the chain)
+        out = ops.head_out(z2, Q3, b3) if HEAD_OUT_KERNEL else torch.addmm(b3, z2, Q3.t())
         ctx.save_for_backward(h, Q1, Q2, Q3, y1, z1, y2, z2)
         return out
 
@@ -564,7 +565,7 @@ class _LinearHeadFn(torch.autograd.Function):
             x.record_stream(side)
 
         wgrad(3, g, z2)
-        g2 = ops.groupsort_backward(y2, g.mm(Q3), 1)
+        g2 = ops.head_out_backward_gs(g, Q3, y2) if HEAD_OUT_KERNEL else ops.groupsort_backward(y2, g.mm(Q3), 1)
         wgrad(2, g2, z1)
         g1 = ops.groupsort_backward(y1, g2.mm(Q2), 1)
         wgrad(1, g1, h)
@@ -574,6 +575,10 @@ class _LinearHeadFn(torch.autograd.Function):
             dW.record_stream(cur)
             db.record_stream(cur)
         return dh, wg[1][0], wg[1][1], wg[2][0], wg[2][1], wg[3][0], wg[3][1]
+
+
+# the head's output layer and its GroupSort input gradient by fiode_head_out / _backward_gs
+HEAD_OUT_KERNEL = True
 
 
 def linear_head(mods, h: torch.Tensor):

@@ -714,6 +714,35 @@ def groupsort_forward(x: torch.Tensor, cdim: int = 1) -> torch.Tensor:
     return y
 
 
+def head_out(z: torch.Tensor, Q: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """fiode_head_out: z [B, K] Q [J, K]^T + bias [J] for J <= 16 (the head's output layer)."""
+    dev = z.device
+    B, K = z.shape
+    J = Q.shape[0]
+    z = _need(z, "z", (B, K), torch.float32, dev)
+    Q = _need(Q.detach(), "Q", (J, K), torch.float32, dev)
+    if bias is not None:
+        bias = _need(bias.detach(), "bias", (J,), torch.float32, dev)
+    out = torch.empty((B, J), dtype=torch.float32, device=dev)
+    L.check(L.lib().fiode_head_out(_stream(dev), B, K, J, z.data_ptr(), Q.data_ptr(), _ptr(bias), out.data_ptr()),
+            "fiode_head_out")
+    return out
+
+
+def head_out_backward_gs(g: torch.Tensor, Q: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """fiode_head_out_backward_gs: GroupSort backward (pre-activation y [B, K]) of g [B, J] Q [J, K]."""
+    dev = g.device
+    B, J = g.shape
+    K = Q.shape[1]
+    g = _need(g, "g", (B, J), torch.float32, dev)
+    Q = _need(Q.detach(), "Q", (J, K), torch.float32, dev)
+    y = _need(y, "y", (B, K), torch.float32, dev)
+    gx = torch.empty((B, K), dtype=torch.float32, device=dev)
+    L.check(L.lib().fiode_head_out_backward_gs(_stream(dev), B, K, J, g.data_ptr(), Q.data_ptr(), y.data_ptr(),
+                                               gx.data_ptr()), "fiode_head_out_backward_gs")
+    return gx
+
+
 def groupsort_backward(x: torch.Tensor, g: torch.Tensor, cdim: int = 1) -> torch.Tensor:
     x, g = x.contiguous(), g.contiguous()
     B, Cc, S = _gs_shape(x, cdim)

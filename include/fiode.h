@@ -312,6 +312,16 @@ FIODE_API int fiode_groupsort_forward(void* stream, int64_t B, int64_t C, int64_
 FIODE_API int fiode_groupsort_backward(void* stream, int64_t B, int64_t C, int64_t S, const float* x, const float* g,
                                        float* gx);
 
+/* The linear head's output layer (KWLargeConcat's last Linear, 512 -> 10; F.linear's addmm in
+ * models.py's head): out [B][J] = z [B][K] Q^T + bias (Q [J][K], bias [J] or NULL), J <= 16, one
+ * wave per row with a fixed-order lane reduction.  fiode_head_out_backward_gs: its input gradient
+ * through the preceding GroupSort, gx = GroupSort backward of y [B][K] (pairs k, k + K/2) applied to
+ * g [B][J] Q (K even). */
+FIODE_API int fiode_head_out(void* stream, int32_t B, int32_t K, int32_t J, const float* z, const float* Q,
+                             const float* bias, float* out);
+FIODE_API int fiode_head_out_backward_gs(void* stream, int32_t B, int32_t K, int32_t J, const float* g,
+                                         const float* Q, const float* y, float* gx);
+
 /* Error text for a return code. */
 /* Inverse of one real n x n matrix with positive-definite symmetric part (the Cayley systems of the
  * 512 x 512 backbone CayleyLinears and the 128 x 128 dynamics map): block Gauss-Jordan over

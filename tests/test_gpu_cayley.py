@@ -443,6 +443,34 @@ def test_sconv_irfft2_qx_matches_gemm_then_irfft2(K, n, C, B, gs, nchw):
         assert torch.equal(c1[sure], c0[sure])
 
 
+@pytest.mark.parametrize("B,K,J,bias", [(128, 512, 10, True), (5, 64, 16, False), (7, 130, 3, True)])
+def test_head_out_kernels_match_torch(B, K, J, bias):
+    """fiode_head_out = addmm and fiode_head_out_backward_gs = GroupSort backward of g Q (float64
+    references), including exact ties in the GroupSort input (gradient split in half)."""
+    from fiode_amd import ops
+    dev = _dev()
+    g0 = torch.Generator(device="cpu").manual_seed(B + K + J)
+    z = torch.randn(B, K, generator=g0).to(dev)
+    Q = torch.randn(J, K, generator=g0).to(dev)
+    b = torch.randn(J, generator=g0).to(dev) if bias else None
+    out = ops.head_out(z, Q, b)
+    ref = z.double() @ Q.double().t() + (b.double() if bias else 0)
+    assert float((out.double() - ref).abs().max()) <= 1e-5 * (float(ref.abs().max()) + 1)
+    y = torch.randn(B, K, generator=g0).to(dev)
+    y[:, 0] = y[:, K // 2]                                   # exact ties
+    g = torch.randn(B, J, generator=g0).to(dev)
+    gx = ops.head_out_backward_gs(g, Q, y)
+    d = g.double() @ Q.double()
+    h = K // 2
+    a, c = y[:, :h], y[:, h:]
+    da, dc = d[:, :h], d[:, h:]
+    ga = torch.where(a > c, da, torch.where(a < c, dc, da / 2 + dc / 2))
+    gc = torch.where(c > a, da, torch.where(c < a, dc, da / 2 + dc / 2))
+    rg = torch.cat([ga, gc], 1)
+    assert float((gx.double() - rg).abs().max()) <= 1e-5 * (float(rg.abs().max()) + 1)
+    assert torch.equal(ops.head_out(z, Q, b), out)                      # fixed-order reduction
+
+
 def test_sconv_rejects_bad_shapes():
     from fiode_amd import ops
     from fiode_amd._lib import FiodeError
@@ -606,11 +634,13 @@ def test_dense_fused_inverse_equals_staged(shape):
     assert float((Qt.mT @ Qt - eye).abs().max()) < 5e-5
 
 
-def test_linear_head_side_stream_wgrad_matches_autograd():
+@pytest.mark.parametrize("out_kernel", [True, False])
+def test_linear_head_side_stream_wgrad_matches_autograd(out_kernel):
     """KWLargeConcat's head as one node (_LinearHeadFn: weight / bias gradients on a side stream)
-    against the module-by-module autograd chain (F.linear + GroupSort) on the same inputs: the
-    output and the input gradient bit for bit (same kernels, same stream order), the weight
-    gradients within float32 rounding (the same GEMMs; bias sums may reduce in another order)."""
+    against the module-by-module autograd chain (F.linear + GroupSort) on the same inputs.  With the
+    output layer on the library (out_kernel False): the output and the input gradient bit for bit
+    (same kernels, same stream order); with fiode_head_out / _backward_gs (the product path) within
+    float32 rounding.  Weight gradients within float32 rounding either way."""
     from fiode_amd import cayley as cy
     from fiode_amd.models import KWLargeConcat
     dev = _dev()
@@ -620,6 +650,7 @@ def test_linear_head_side_stream_wgrad_matches_autograd():
     h0 = torch.randn(128, 4096, device=dev)
     gout = torch.randn(128, 10, device=dev)
     res = {}
+    cy.HEAD_OUT_KERNEL = out_kernel
     for fused in (False, True):
         cy.HEAD_WGRAD_SIDE = fused
         for m in mods:
@@ -632,7 +663,12 @@ def test_linear_head_side_stream_wgrad_matches_autograd():
         res[fused] = (out.detach().clone(), h.grad.clone(),
                       [p.grad.clone() for m in mods if isinstance(m, cy.CayleyLinear) for p in (m.weight, m.alpha, m.bias)])
     cy.HEAD_WGRAD_SIDE = True
-    assert torch.equal(res[False][0], res[True][0])
-    assert torch.equal(res[False][1], res[True][1])
-    for a, b in zip(res[False][2], res[True][2]):
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), float((a - b).abs().max())
+    cy.HEAD_OUT_KERNEL = True
+    if out_kernel:
+        assert torch.allclose(res[False][0], res[True][0], rtol=1e-5, atol=1e-5)
+        assert torch.allclose(res[False][1], res[True][1], rtol=1e-5, atol=1e-6)
+    else:
+        assert torch.equal(res[False][0], res[True][0])
+        assert torch.equal(res[False][1], res[True][1])
+    for a, b in zip(res[False][2], res[True][2]):     # the input gradients above differ in rounding
+        assert float((a - b).abs().max()) <= 1e-4 * (float(b.abs().max()) + 1e-6), float((a - b).abs().max())
