@@ -3,7 +3,9 @@ inserted in front of one part of the step (on whatever stream that part runs), a
 the hipGraph step time tells whether that part is on the critical path (growth ~ 200 us) or has
 slack (growth ~ 0).
 
-python tools/probes/slack_probe.py  ->  one JSON line: ms per step per variant
+python tools/probes/slack_probe.py  ->  one JSON line: ms per step per variant (captures picked from 4
+placement trials, as bench.py does; a spin in front of a call made k times per step adds k x 200 us
+when every one of them is on the critical path)
 """
 import json
 import pathlib
@@ -42,7 +44,7 @@ def step_ms(steps=40):
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
-    gs = GraphTrainStep(mod, opt, x, y)
+    gs = GraphTrainStep(mod, opt, x, y, placement_trials=4)
     for _ in range(5):
         gs.step()
     torch.cuda.synchronize()
@@ -65,15 +67,19 @@ def spin_before(owner, name, once_per_step=True):
 
 variants = [
     ("baseline", None),
+    ("conv1_input_transform (step start)", (ops, "sconv_rfft2_nchw")),
+    ("conv1_irfft2_qx", (ops, "sconv_irfft2_qx")),
+    ("head_out (head fwd end)", (ops, "head_out")),
     ("linear_map_fwd (side streams 1-2)", (CY.CayleyLinear, "effective_weight")),
     ("dyn_map_fwd (side stream 3)", (__import__("fiode_amd.dynamics", fromlist=["x"]), "cayley_scaled")),
+    ("lyap_step (fan-out)", (ops, "lyap_step")),
     ("odetrain_fwd (ode stream)", (ops, "odetrain_forward")),
-    ("odetrain_bwd", (ops, "odetrain_backward")),
-    ("lyap_step (main)", (ops, "lyap_step")),
-    ("sconv_bwd_rfft2 (backbone bwd)", (ops, "sconv_rfft2")),
-    ("conv_map_bwd (layer streams)", (ops, "spectral_cayley_backward")),
+    ("odetrain_bwd_x", (ops, "odetrain_backward_x")),
+    ("odetrain_bwd_weights (tap, side)", (ops, "odetrain_backward_weights")),
+    ("head_out_backward_gs (head bwd start)", (ops, "head_out_backward_gs")),
+    ("conv_map_bwd (layer streams, x4)", (ops, "spectral_cayley_backward")),
     ("conv_map_refresh (layer streams, x4)", (CY.CayleyConv, "refresh_map")),
-    ("dense_map_bwd (step stream, tail)", (CY, "_dense_backward")),
+    ("dense_map_bwd (x3)", (CY, "_dense_backward")),
 ]
 if len(sys.argv) > 1 and sys.argv[1] == "lyap_curve":
     variants = [("baseline", None)]
