@@ -318,11 +318,11 @@ __device__ __forceinline__ void pi_signal(unsigned* flag) {
 // when `acq` (FIODE_PINV_ACQUIRE=1): every load of handed-off bytes is a 16-B sc1 buffer load of
 // bytes stored sc1 and drained before the flag, the form MI355X_MICROARCH.md lists as valid without
 // the acquire ("Valid forms", row 1).
-__device__ __forceinline__ void pi_poll(const unsigned* flag, int& dead) {
+__device__ __forceinline__ void pi_poll(const unsigned* flag, int& dead, unsigned limit) {
   if (threadIdx.x == 0 && !dead) {
     unsigned spins = 0;
     while (__hip_atomic_load((gu32_t*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      if (++spins > PI_SPIN_LIMIT) {
+      if (++spins > limit) {
         dead = 1;
         break;
       }
@@ -478,7 +478,7 @@ __device__ __forceinline__ void mfma_settle(f4v (&acc)[2]) {
 template <int NB, class Src>
 __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out, float* __restrict__ qout,
                                                 float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
-                                                int acq, unsigned long long* prof) {
+                                                int acq, unsigned long long* prof, unsigned spin_limit) {
   if (skip && *skip) return;                  // (uniform)
   constexpr int n = NB * PB;
   __shared__ __attribute__((aligned(16))) float lds[4][PB][LDTS];
@@ -536,9 +536,9 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
       const int k1 = k + 1;
       auto fetch = [&]() {
         if (k1 >= NB || k == 0) return;
-        pi_poll(&tflag[((k - 1) * NB + k) * NB + k1], dead);
-        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k], dead);
-        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k1], dead);
+        pi_poll(&tflag[((k - 1) * NB + k) * NB + k1], dead, spin_limit);
+        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k], dead, spin_limit);
+        pi_poll(&tflag[((k - 1) * NB + k1) * NB + k1], dead, spin_limit);
         pi_acquire(acq);
         const __amdgpu_buffer_rsrc_t r0 = pi_rsrc(V + (size_t)vtile(k - 1, k, k1) * 4, PI_TILE);
         const __amdgpu_buffer_rsrc_t r1 = pi_rsrc(V + (size_t)vtile(k - 1, k1, k) * 4, PI_TILE);
@@ -553,11 +553,14 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
       mark(8 * k + 0);
       CG::invert(sm, fetch, 1);                                      // cm: P_k (row-major)
       mark(8 * k + 1);
+      // a timed-out chain publishes P_k as NaN: every tile applies every step's P_k, so the whole
+      // output turns NaN instead of finite values built from stale workspace tiles
+      const float cpz = dead ? __builtin_nanf("") : 0.f;
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         f4v v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = CG::at(sm, 16 * rw + 4 * q + r, 16 * (2 * ch + b) + i);
+        for (int r = 0; r < 4; ++r) v[r] = CG::at(sm, 16 * rw + 4 * q + r, 16 * (2 * ch + b) + i) + cpz;
         pi_store(rP, ptile(k) + own_e(b), v);
       }
       pi_signal(&pflag[k]);
@@ -601,10 +604,10 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
     for (int k = 0; k < NB; ++k) {
       if (ti == tj && k == ti - 1) continue;       // X_kk^(k-1) is the chain's; nobody reads this one
       const bool generic = ti != k && tj != k;
-      pi_poll(&pflag[k], dead);
+      pi_poll(&pflag[k], dead, spin_limit);
       if (generic && k > 0) {                      // this step's operands of version k - 1
-        pi_poll(&tflag[((k - 1) * NB + k) * NB + tj], dead);
-        pi_poll(&tflag[((k - 1) * NB + ti) * NB + k], dead);
+        pi_poll(&tflag[((k - 1) * NB + k) * NB + tj], dead, spin_limit);
+        pi_poll(&tflag[((k - 1) * NB + ti) * NB + k], dead, spin_limit);
       }
       pi_acquire(acq);
       const __amdgpu_buffer_rsrc_t rp = pi_rsrc(Pt + (size_t)ptile(k) * 4, PI_TILE);
@@ -649,8 +652,9 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
       // publish version k where step k + 1 or the chain reads it
       const bool rowcol = (ti == k + 1) != (tj == k + 1);
       if (k + 1 < NB && (rowcol || (ti == tj && ti == k + 2))) {
+        const float tpz = dead ? __builtin_nanf("") : 0.f;     // a timed-out tile poisons what it hands on
 #pragma unroll
-        for (int b = 0; b < 2; ++b) pi_store(rV, vtile(k, ti, tj) + own_e(b), acc[b]);
+        for (int b = 0; b < 2; ++b) pi_store(rV, vtile(k, ti, tj) + own_e(b), acc[b] + tpz);
         pi_signal(&tflag[(k * NB + ti) * NB + tj]);
       }
       mark(256 + t * NB + k);
@@ -673,6 +677,9 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
   }
 }
 
+// spin bound of every k_pinv poll (fiode_debug_set_pinv_spin_limit lowers it to test the timeout path)
+unsigned g_pinv_spin_limit = PI_SPIN_LIMIT;
+
 int pinv_acquire_knob() {
   static const int acq = [] {
     const char* e = getenv("FIODE_PINV_ACQUIRE");
@@ -689,7 +696,7 @@ int launch_pinv_src(hipStream_t st, int batch, Src src, float* out, float* qout,
     FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
                                      (size_t)batch, st));
   hipLaunchKernelGGL((k_pinv<NB, Src>), dim3(1 + NB * NB, batch), dim3(PI_NT), 0, st, src, out, qout, ws, wstride, skip,
-                     pinv_acquire_knob(), prof);
+                     pinv_acquire_knob(), prof, g_pinv_spin_limit);
   return FIODE_OK;
 }
 
@@ -795,6 +802,14 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
 extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                    size_t workspace_bytes) {
   return fiode_block_inverse_batched(stream, 1, n, in, out, workspace, workspace_bytes);
+}
+
+// Diagnostic (not in fiode.h): the spin bound of k_pinv's polls (0 restores the default); returns the
+// previous bound.  A test lowers it so that polls time out and checks that no finite output is wrong.
+extern "C" FIODE_API unsigned fiode_debug_set_pinv_spin_limit(unsigned limit) {
+  const unsigned prev = g_pinv_spin_limit;
+  g_pinv_spin_limit = limit ? limit : PI_SPIN_LIMIT;
+  return prev;
 }
 
 // Diagnostic (not in fiode.h): the one-launch inverse of one n = 512 system with phase timestamps

@@ -1108,12 +1108,18 @@ __device__ void ot_batch_sum(const OTArgs& a, int& dead, unsigned& ep, const dou
     }
   }
   // a timed-out exchange summed only the granules that arrived: NaN, so everything computed from
-  // it (y_out in the forward; g_dt and every stage adjoint upstream of it in the backward) is
-  // poisoned instead of silently wrong
-  const bool poisoned = timed_out || dead;       // (a sticky earlier timeout poisons every later sum)
+  // it (y_out, the step-size controller) is poisoned instead of silently wrong.  Every wave gathers
+  // for itself, so one wave can time out after another has finished with a finite sum; the
+  // controller then runs on different values in different waves and their loop trip counts (with
+  // the __syncthreads inside the evals) would diverge.  One barrier makes the decision uniform:
+  // every timeout wrote `dead` (lane 0 of the wave) before it, every wave reads it after it.
+  const double tot0 = wave_dsum(acc[0]);
+  (void)timed_out;
+  __syncthreads();
+  const bool poisoned = dead != 0;               // (a sticky earlier timeout poisons every later sum)
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const double tot = wave_dsum(acc[v]);
+    const double tot = v == 0 ? tot0 : wave_dsum(acc[v]);
     out[v] = poisoned ? __builtin_nan("") : tot;
   }
   ++ep;

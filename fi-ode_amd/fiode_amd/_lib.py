@@ -82,7 +82,7 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
-ABI_VERSION = 3            # FIODE_ABI_VERSION (include/fiode.h)
+ABI_VERSION = 4            # FIODE_ABI_VERSION (include/fiode.h)
 FIODE_ODETRAIN_NSAVED = 14  # entries fiode_odetrain_saved_offsets writes
 FIODE_GUARD_MAX_STATUS = 4
 
@@ -108,6 +108,14 @@ class SconvConfig(ct.Structure):
 
 class DenseConfig(ct.Structure):
     _fields_ = [("batch", ct.c_int32), ("cout", ct.c_int32), ("cin", ct.c_int32)]
+
+
+class GemmDesc(ct.Structure):
+    """fiode_gemm_desc (include/fiode.h)."""
+    _fields_ = [("batch", ct.c_int32), ("M", ct.c_int32), ("N", ct.c_int32), ("K", ct.c_int32),
+                ("trans_a", ct.c_int32), ("trans_b", ct.c_int32), ("lda", ct.c_int64), ("ldb", ct.c_int64),
+                ("ldc", ct.c_int64), ("stride_a", ct.c_int64), ("stride_b", ct.c_int64), ("stride_c", ct.c_int64),
+                ("alpha", ct.c_float), ("beta", ct.c_float), ("split_k", ct.c_int32)]
 
 
 class CertifyConfig(ct.Structure):
@@ -188,6 +196,10 @@ def _load():
         "fiode_dense_cayley_grad": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                _vp, ct.c_size_t]),
         "fiode_dense_gemm": (ct.c_int, [_vp, ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32, _vp, _vp, _vp]),
+        "fiode_gemm_splits": (ct.c_int32, [ct.POINTER(GemmDesc)]),
+        "fiode_gemm_counter_bytes": (ct.c_size_t, [ct.POINTER(GemmDesc)]),
+        "fiode_gemm_workspace_bytes": (ct.c_size_t, [ct.POINTER(GemmDesc)]),
+        "fiode_gemm": (ct.c_int, [_vp, ct.POINTER(GemmDesc), _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
         "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
         "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
         "fiode_sconv_rfft2_nchw": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),

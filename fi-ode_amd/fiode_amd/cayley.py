@@ -164,7 +164,7 @@ def _dense_prep(W: torch.Tensor, alpha: torch.Tensor, M: Optional[torch.Tensor] 
         L.check(lib.fiode_dense_norm_partials(st, ct.byref(cfg), Wb.data_ptr(), part.data_ptr(), part.numel() * 4),
                 "fiode_dense_norm_partials")
     Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
-    G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
+    G = ops.mm(Vp.mT, Vp) if Vp is not None else None
     if M is None:
         M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
     if not DENSE_NORM_PARTIALS:
@@ -184,8 +184,7 @@ def _dense_finish(st: dict, inv: torch.Tensor) -> torch.Tensor:
     Wb, k = st["Wb"], st["k"]
     P = None                    # V' inv in W's layout (wide: its transpose inv^T V'^T = inv^T W[:, k:])
     if st["Vp"] is not None:
-        P = torch.matmul(inv.mT, Wb[:, :, k:]) if st["wide"] else torch.matmul(st["Vp"], inv)
-        P = P.contiguous()
+        P = ops.mm(inv.mT, Wb[:, :, k:]) if st["wide"] else ops.mm(st["Vp"], inv)
     Q = torch.empty_like(Wb)
     L.check(L.lib().fiode_dense_cayley_finish(ops._stream(Wb.device), ct.byref(st["cfg"]), st["al"].data_ptr(),
                                               st["nrm"].data_ptr(), inv.data_ptr(), ops._ptr(P), Q.data_ptr()),
@@ -207,7 +206,7 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     if R > k:
         Vp = Wb[:, :, k:].mT if wide else Wb[:, k:, :]
         Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
-        A = torch.matmul(Vp.mT, Gb).contiguous()
+        A = ops.mm(Vp.mT, Gb)
     Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
                                         ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
@@ -220,7 +219,7 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
         L.check(lib.fiode_dense_gemm(st, b, k, 0, 1, Ginv.data_ptr(), inv.data_ptr(), T.data_ptr()), "fiode_dense_gemm")
         L.check(lib.fiode_dense_gemm(st, b, k, 1, 0, inv.data_ptr(), T.data_ptr(), GMn.data_ptr()), "fiode_dense_gemm")
     else:
-        GMn = torch.matmul(ih, torch.matmul(Ginv, ih)).contiguous()
+        GMn = ops.mm(ih, ops.mm(Ginv, ih))
     gX = torch.empty_like(Wb)                    # W layout
     H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
@@ -228,11 +227,11 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     P1 = P2 = None                  # V' H and Gb inv^T in W's layout (wide: H^T W[:, k:], inv gQ[:, k:])
     if R > k:
         if wide:
-            P1 = torch.matmul(H.mT, Wb[:, :, k:]).contiguous()
-            P2 = torch.matmul(inv, gQb[:, :, k:]).contiguous()
+            P1 = ops.mm(H.mT, Wb[:, :, k:])
+            P2 = ops.mm(inv, gQb[:, :, k:])
         else:
-            P1 = torch.matmul(Vp, H).contiguous()
-            P2 = torch.matmul(Gb, ih).contiguous()
+            P1 = ops.mm(Vp, H)
+            P2 = ops.mm(Gb, ih)
     gW = torch.empty_like(Wb)
     ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
     ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,
@@ -271,7 +270,7 @@ def _dense_forward_fused(W: torch.Tensor, alpha: torch.Tensor):
                                                 ws.data_ptr(), lib.fiode_dense_inverse_flag_bytes(k) // 4, per),
             "fiode_dense_norm_partials_clear")
     Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
-    G = torch.matmul(Vp.mT, Vp).contiguous() if Vp is not None else None
+    G = ops.mm(Vp.mT, Vp) if Vp is not None else None
     nrm = torch.empty(b, dtype=torch.float32, device=W.device)
     inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
     Q = torch.empty_like(Wb) if Vp is None else None
@@ -534,18 +533,23 @@ class _LinearHeadFn(torch.autograd.Function):
     gradient it does not need (the head's backward is on the step's critical path).  Here the
     weight / bias gradients (the same GEMM g^T x and column sum) of every layer run on a side
     stream forked as soon as that layer's output gradient exists, beside the input-gradient chain,
-    and join the step's stream once at the end."""
+    and join the step's stream once at the end.  Every product is fiode_gemm (gemm.hip; the bias
+    added in its epilogue), the output layer fiode_head_out / _backward_gs when it has <= 16 outputs
+    (KWLargeConcat's 10 classes; a wider out_dim, e.g. make_ortho_KWLarge_Concat's default 128,
+    takes fiode_gemm + the GroupSort kernel)."""
 
     @staticmethod
     def forward(ctx, h, Q1, b1, Q2, b2, Q3, b3):
         from . import ops
-        y1 = torch.addmm(b1, h, Q1.t())
+        y1 = ops.mm(h, Q1.t(), bias=b1)
         z1 = ops.groupsort_forward(y1, 1)
-        y2 = torch.addmm(b2, z1, Q2.t())
+        y2 = ops.mm(z1, Q2.t(), bias=b2)
         z2 = ops.groupsort_forward(y2, 1)
+        out_k = _head_out_ok(Q3)
         # the 512 -> 10 output layer: the library ran it on one workgroup (~15 us on the chain)
-        out = ops.head_out(z2, Q3, b3) if HEAD_OUT_KERNEL else torch.addmm(b3, z2, Q3.t())
+        out = ops.head_out(z2, Q3, b3) if out_k else ops.mm(z2, Q3.t(), bias=b3)
         ctx.save_for_backward(h, Q1, Q2, Q3, y1, z1, y2, z2)
+        ctx.out_k = out_k
         return out
 
     @staticmethod
@@ -560,16 +564,16 @@ class _LinearHeadFn(torch.autograd.Function):
         def wgrad(k, gk, x):
             side.wait_stream(cur)
             with torch.cuda.stream(side):
-                wg[k] = (gk.t().mm(x), gk.sum(0))
+                wg[k] = (ops.mm(gk.t(), x), gk.sum(0))
             gk.record_stream(side)
             x.record_stream(side)
 
         wgrad(3, g, z2)
-        g2 = ops.head_out_backward_gs(g, Q3, y2) if HEAD_OUT_KERNEL else ops.groupsort_backward(y2, g.mm(Q3), 1)
+        g2 = ops.head_out_backward_gs(g, Q3, y2) if ctx.out_k else ops.groupsort_backward(y2, ops.mm(g, Q3), 1)
         wgrad(2, g2, z1)
-        g1 = ops.groupsort_backward(y1, g2.mm(Q2), 1)
+        g1 = ops.groupsort_backward(y1, ops.mm(g2, Q2), 1)
         wgrad(1, g1, h)
-        dh = g1.mm(Q1)
+        dh = ops.mm(g1, Q1)
         cur.wait_stream(side)
         for dW, db in wg.values():
             dW.record_stream(cur)
@@ -577,8 +581,14 @@ class _LinearHeadFn(torch.autograd.Function):
         return dh, wg[1][0], wg[1][1], wg[2][0], wg[2][1], wg[3][0], wg[3][1]
 
 
-# the head's output layer and its GroupSort input gradient by fiode_head_out / _backward_gs
+# the head's output layer and its GroupSort input gradient by fiode_head_out / _backward_gs (<= 16
+# outputs: HEAD_JMAX of backbone.hip)
 HEAD_OUT_KERNEL = True
+HEAD_OUT_MAX_J = 16
+
+
+def _head_out_ok(Q3: torch.Tensor) -> bool:
+    return HEAD_OUT_KERNEL and Q3.shape[0] <= HEAD_OUT_MAX_J
 
 
 def linear_head(mods, h: torch.Tensor):
@@ -731,8 +741,8 @@ class _SpectralConvFn(torch.autograd.Function):
                 w = torch.where((kb == 0) | (kb == n // 2), 1.0, 2.0) / float(n * n)
                 wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
 
-        def wgrad():        # dL/dQ = w G X^H (the library GEMM: see the note on fiode_cgemm below)
-            gq = torch.matmul(G, X.mH) * wq if need_q else None
+        def wgrad():        # dL/dQ = w G X^H: fiode_cgemm with B = X^H read from X and w folded in
+            gq = ops.cgemm(G, X, conj_trans_b=True, scale=wq.reshape(-1)) if need_q else None
             gbias = G[0].real.sum(-1) if need_b else None
             return gq, gbias
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
@@ -758,12 +768,12 @@ class _SpectralConvFn(torch.autograd.Function):
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
-# The per-frequency channel products Q X and Q^H G are fiode_cgemm (cgemm.hip), not torch.matmul (the
-# library's batched complex GEMM: one 128 x 64 tile per frequency; the n = 8 layer's forward 41 ->
-# 16 us, conv 3's input gradient 16 -> 10, conv 1's forward 13 -> 10 us; step -25 to -40 us in the
-# alternating A/B, profiles/r05bd).  The weight gradient w G X^H stays the library GEMM + the scale on
-# the side stream: one fiode_cgemm launch (conjugate-transposed B, w folded in) measured 10-20 us
-# slower in the step (profiles/r05bj), as did the library for conv 2's forward (r05bk).
+# The per-frequency channel products Q X, Q^H G and the weight gradient w G X^H are fiode_cgemm
+# (cgemm.hip), not torch.matmul (the library's batched complex GEMM: one 128 x 64 tile per frequency;
+# the n = 8 layer's forward 41 -> 16 us, conv 3's input gradient 16 -> 10, conv 1's forward 13 -> 10 us;
+# step -25 to -40 us in the alternating A/B, profiles/r05bd).  The weight gradient runs on the side
+# stream (round 5 kept the library GEMM + a scale kernel there: profiles/r05bj; round 6 takes the one
+# fiode_cgemm launch so that no library GEMM is left in the step).
 # conv layers with at most this many input channels (conv 1: 3) form Q X inside the inverse
 # transform's loads (fiode_sconv_irfft2_qx; the kernel's limit is 4): no GEMM launch, no [f][C][B]
 # product in HBM

@@ -626,6 +626,69 @@ def cgemm(A: torch.Tensor, B: torch.Tensor, conj_trans_a: bool = False, conj_tra
     return C
 
 
+def _mat_layout(X: torch.Tensor):
+    """(trans, ld) of a 2-D (or the last two dims of a batched) float32 view X [R, Cn] over row-major
+    memory: X itself row-major (unit inner stride) -> (0, row stride); X the transposed view of a
+    row-major matrix -> (1, its row stride); else None (the caller copies)."""
+    R, Cn = X.shape[-2], X.shape[-1]
+    s0, s1 = X.stride(-2), X.stride(-1)
+    if (s1 == 1 or Cn == 1) and (s0 >= Cn or R == 1):
+        return 0, max(s0 if R > 1 else Cn, Cn, 1)
+    if (s0 == 1 or R == 1) and (s1 >= R or Cn == 1):
+        return 1, max(s1 if Cn > 1 else R, R, 1)
+    return None
+
+
+def _gemm_ws(dev: torch.device, nbytes: int) -> torch.Tensor:
+    # one split-K workspace per stream (its counter words are zero on entry and left zero by every
+    # call; calls on one stream are ordered, calls on two streams never share a workspace)
+    return _Workspace.get(dev, nbytes, f"gemm{torch.cuda.current_stream(dev).cuda_stream}", zero=True)
+
+
+def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
+       bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0) -> torch.Tensor:
+    """fiode_gemm: out = alpha A @ B + beta out + bias, float32, A [(b,) M, K], B [(b,) K, N] (a 2-D
+    operand is shared by every batch entry), bias [N].  Either operand may be a transposed view of
+    row-major memory (``W.t()``, ``X.mT``, a column slice): the kernel reads it in place.  The hand-
+    written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip)."""
+    dev = B.device
+    if A.dtype != torch.float32 or B.dtype != torch.float32 or A.device != dev or dev.type != "cuda":
+        raise ValueError(f"mm: float32 ROCm operands, got {A.dtype} on {A.device}, {B.dtype} on {B.device}")
+    if A.dim() not in (2, 3) or B.dim() not in (2, 3) or A.shape[-1] != B.shape[-2]:
+        raise ValueError(f"mm: shapes {tuple(A.shape)} @ {tuple(B.shape)}")
+    batch = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
+    for X in (A, B):
+        if X.dim() == 3 and X.shape[0] != batch:
+            raise ValueError(f"mm: batch sizes {tuple(A.shape)} / {tuple(B.shape)}")
+    M, K, N = A.shape[-2], A.shape[-1], B.shape[-1]
+    la = _mat_layout(A)
+    if la is None:
+        A = A.contiguous()
+        la = _mat_layout(A)
+    lb = _mat_layout(B)
+    if lb is None:
+        B = B.contiguous()
+        lb = _mat_layout(B)
+    oshape = (batch, M, N) if (A.dim() == 3 or B.dim() == 3) else (M, N)
+    if out is None:
+        if beta != 0.0:
+            raise ValueError("mm: beta needs out")
+        out = torch.empty(oshape, dtype=torch.float32, device=dev)
+    elif tuple(out.shape) != oshape or not out.is_contiguous() or out.dtype != torch.float32 or out.device != dev:
+        raise ValueError(f"mm: out must be a contiguous float32 {oshape} tensor on {dev}")
+    if bias is not None:
+        bias = _need(bias.detach(), "bias", (N,), torch.float32, dev)
+    d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], N,
+                   A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
+                   float(alpha), float(beta), int(split_k))
+    lib = L.lib()
+    nb = lib.fiode_gemm_workspace_bytes(ct.byref(d))
+    ws = _gemm_ws(dev, nb) if nb else None
+    L.check(lib.fiode_gemm(_stream(dev), ct.byref(d), A.data_ptr(), B.data_ptr(), _ptr(bias), out.data_ptr(),
+                           _ptr(ws), ws.numel() if ws is not None else 0), "fiode_gemm")
+    return out
+
+
 def spectral_config(weight_shape, n: int) -> L.SpectralConfig:
     cout, cin, kh, kw = weight_shape
     if kh != kw:

@@ -23,7 +23,9 @@
 extern "C" {
 #endif
 
-#define FIODE_ABI_VERSION 3
+/* ABI 4 (round 6): fiode_sconv_config gained `nchw` (20 bytes, was 16), the one-launch block inverse
+   (n = 128 .. 512) needs a larger workspace (fiode_block_inverse_workspace_bytes), fiode_gemm added. */
+#define FIODE_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define FIODE_API __attribute__((visibility("default")))
@@ -407,6 +409,31 @@ FIODE_API int fiode_dense_cayley_grad(void* stream, const fiode_dense_config* cf
  * _dense_backward; the reference's autograd through torch.inverse, classification.py:282-293). */
 FIODE_API int fiode_dense_gemm(void* stream, int32_t batch, int32_t n, int32_t trans_a, int32_t trans_b,
                                const float* A, const float* B, float* C);
+
+/* ---- real f32 GEMM of the Cayley layers (gemm.hip) ---------------------------------------------
+ * C[b] = alpha opA(A[b]) opB(B[b]) + beta C[b] + bias (bias [N] added to every row, or NULL), all
+ * row-major: opA [M][K] is A [M][lda] (trans_a 0) or the transpose of A [K][lda] (trans_a 1); opB
+ * [K][N] is B [K][ldb] (trans_b 0) or the transpose of B [N][ldb] (trans_b 1).  Replaces the library
+ * GEMMs of the dense Cayley maps (cayley_scaled's V'^T V', V' inv and their backward products,
+ * classification.py:282-293) and the head's CayleyLinear products (F.linear / addmm and autograd's
+ * mm of KWLarge_Concat, models.py:29-35).  K is split over workgroups when the output has too few
+ * 64 x 64 tiles to fill the chip (split_k 0: the library's choice, fiode_gemm_splits); the partial
+ * tiles are summed in split order by the last workgroup of each tile (deterministic).  Workspace:
+ * fiode_gemm_workspace_bytes (0 when unsplit); its first fiode_gemm_counter_bytes must be zero
+ * before the first call, and every completed call leaves them zero (one workspace per stream). */
+typedef struct fiode_gemm_desc {
+  int32_t batch, M, N, K;
+  int32_t trans_a, trans_b;
+  int64_t lda, ldb, ldc;
+  int64_t stride_a, stride_b, stride_c;   /* elements between batch entries */
+  float alpha, beta;
+  int32_t split_k;                        /* 0: the library's choice */
+} fiode_gemm_desc;
+FIODE_API int32_t fiode_gemm_splits(const fiode_gemm_desc* d);
+FIODE_API size_t fiode_gemm_counter_bytes(const fiode_gemm_desc* d);
+FIODE_API size_t fiode_gemm_workspace_bytes(const fiode_gemm_desc* d);
+FIODE_API int fiode_gemm(void* stream, const fiode_gemm_desc* d, const float* A, const float* B, const float* bias,
+                         float* C, void* workspace, size_t workspace_bytes);
 
 /* ---- spectral convolution transforms on spatial-major activations [n][n][C][B] (CayleyConv
  * forward_hwcb; fiode_amd/cayley.py).  Spectrum layout [f][C][B] complex64, f = ka (n/2+1) + kb. */

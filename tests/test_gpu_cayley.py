@@ -634,41 +634,72 @@ def test_dense_fused_inverse_equals_staged(shape):
     assert float((Qt.mT @ Qt - eye).abs().max()) < 5e-5
 
 
-@pytest.mark.parametrize("out_kernel", [True, False])
-def test_linear_head_side_stream_wgrad_matches_autograd(out_kernel):
-    """KWLargeConcat's head as one node (_LinearHeadFn: weight / bias gradients on a side stream)
-    against the module-by-module autograd chain (F.linear + GroupSort) on the same inputs.  With the
-    output layer on the library (out_kernel False): the output and the input gradient bit for bit
-    (same kernels, same stream order); with fiode_head_out / _backward_gs (the product path) within
-    float32 rounding.  Weight gradients within float32 rounding either way."""
+@pytest.mark.parametrize("out_kernel,out_dim", [(True, 10), (False, 10), (True, 128)])
+def test_linear_head_side_stream_wgrad_matches_autograd(out_kernel, out_dim):
+    """KWLargeConcat's head as one node (_LinearHeadFn: fiode_gemm products, weight / bias gradients
+    on a side stream) against the module-by-module autograd chain (F.linear + GroupSort) on the same
+    inputs: output, input gradient and weight gradients within float32 rounding.  out_dim = 128
+    (make_ortho_KWLarge_Concat's and ExpConfig's default; more than fiode_head_out's 16 outputs)
+    takes fiode_gemm for the output layer too (it used to raise ESHAPE)."""
     from fiode_amd import cayley as cy
     from fiode_amd.models import KWLargeConcat
     dev = _dev()
     torch.manual_seed(0)
-    net = KWLargeConcat().to(dev).train()
+    net = KWLargeConcat(out_dim=out_dim).to(dev).train()
     mods = list(net.model)[-5:]
     h0 = torch.randn(128, 4096, device=dev)
-    gout = torch.randn(128, 10, device=dev)
+    gout = torch.randn(128, out_dim, device=dev)
     res = {}
     cy.HEAD_OUT_KERNEL = out_kernel
-    for fused in (False, True):
-        cy.HEAD_WGRAD_SIDE = fused
-        for m in mods:
-            if isinstance(m, cy.CayleyLinear):
-                m.zero_grad(set_to_none=True)
-        h = h0.clone().requires_grad_(True)
-        out = cy.linear_head(mods, h)
-        out.backward(gout)
-        torch.cuda.synchronize()
-        res[fused] = (out.detach().clone(), h.grad.clone(),
-                      [p.grad.clone() for m in mods if isinstance(m, cy.CayleyLinear) for p in (m.weight, m.alpha, m.bias)])
-    cy.HEAD_WGRAD_SIDE = True
-    cy.HEAD_OUT_KERNEL = True
-    if out_kernel:
-        assert torch.allclose(res[False][0], res[True][0], rtol=1e-5, atol=1e-5)
-        assert torch.allclose(res[False][1], res[True][1], rtol=1e-5, atol=1e-6)
-    else:
-        assert torch.equal(res[False][0], res[True][0])
-        assert torch.equal(res[False][1], res[True][1])
+    try:
+        for fused in (False, True):
+            cy.HEAD_WGRAD_SIDE = fused
+            for m in mods:
+                if isinstance(m, cy.CayleyLinear):
+                    m.zero_grad(set_to_none=True)
+            h = h0.clone().requires_grad_(True)
+            out = cy.linear_head(mods, h)
+            out.backward(gout)
+            torch.cuda.synchronize()
+            res[fused] = (out.detach().clone(), h.grad.clone(),
+                          [p.grad.clone() for m in mods if isinstance(m, cy.CayleyLinear)
+                           for p in (m.weight, m.alpha, m.bias)])
+    finally:
+        cy.HEAD_WGRAD_SIDE = True
+        cy.HEAD_OUT_KERNEL = True
+    assert torch.allclose(res[False][0], res[True][0], rtol=1e-5, atol=1e-5)
+    assert torch.allclose(res[False][1], res[True][1], rtol=1e-5, atol=1e-6)
     for a, b in zip(res[False][2], res[True][2]):     # the input gradients above differ in rounding
         assert float((a - b).abs().max()) <= 1e-4 * (float(b.abs().max()) + 1e-6), float((a - b).abs().max())
+
+
+def test_block_inverse_timeout_poisons_instead_of_finite_wrong():
+    """k_pinv's polls are bounded; with the bound lowered to one retry most polls time out.  A
+    timed-out chain workgroup publishes its pivot inverse as NaN and a timed-out tile workgroup
+    poisons the tiles it hands on, so every output entry is either NaN or exactly the
+    healthy launch's value -- never a finite value built from stale workspace tiles."""
+    import ctypes as ct
+    from fiode_amd import _lib as L
+    from fiode_amd.cayley import _block_inverse
+    dev = _dev()
+    lib = L.lib()
+    fn = lib.fiode_debug_set_pinv_spin_limit
+    fn.restype, fn.argtypes = ct.c_uint, [ct.c_uint]
+    g = torch.Generator(device="cpu").manual_seed(31)
+    n = 512
+    A = torch.randn(n, n, generator=g) / n ** 0.5
+    M = (torch.eye(n) + A - A.t()).to(dev)
+    ref = _block_inverse(M)
+    torch.cuda.synchronize()
+    fn(1)
+    try:
+        out = _block_inverse(M)
+        torch.cuda.synchronize()
+    finally:
+        fn(0)
+    fin = torch.isfinite(out)
+    assert not bool(fin.all())                      # something timed out at this bound
+    assert torch.equal(out[fin], ref[fin])
+    again = _block_inverse(M)                       # the default bound is back
+    torch.cuda.synchronize()
+    assert torch.equal(again, ref)

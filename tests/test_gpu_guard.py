@@ -24,7 +24,7 @@ def _state(mod, opt):
     return ps, st
 
 
-@pytest.mark.parametrize("kind", ["rk4_exchange_timeout", "dopri5_capacity"])
+@pytest.mark.parametrize("kind", ["rk4_exchange_timeout", "dopri5_exchange_timeout", "dopri5_capacity"])
 def test_poisoned_solve_leaves_parameters_and_moments(kind, monkeypatch):
     import bench
     from fiode_amd.graph_step import GraphTrainStep
@@ -37,6 +37,13 @@ def test_poisoned_solve_leaves_parameters_and_moments(kind, monkeypatch):
         # it were not resident; the others time out (~0.5 s), report status 4 and poison y_hat
         monkeypatch.setenv("FIODE_DEBUG_DROP_PUBLISH", "1")
         mod = bench.build_module(dev, seed=0, train_ode=True, solver="rk4")
+    elif kind == "dopri5_exchange_timeout":
+        # the same hook under the adaptive solve: its float64 batch sums (error ratios) are gathered
+        # by every wave for itself, and the poison decision after a timeout must be the same in all
+        # waves of a workgroup, or the controller's loop would diverge across the evals'
+        # barriers -- the solve has to come back poisoned (status 4), not hang
+        monkeypatch.setenv("FIODE_DEBUG_DROP_PUBLISH", "1")
+        mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5")
     else:
         mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5")
         mod.train_ode_max_attempts = 1           # the solve needs ~10: capacity exhausted, status 2
@@ -54,7 +61,7 @@ def test_poisoned_solve_leaves_parameters_and_moments(kind, monkeypatch):
         for k in sa:
             assert torch.equal(sa[k], sb[k]), k
     assert gs.skipped_steps() == 2
-    assert mod.device_status() == (4 if kind == "rk4_exchange_timeout" else 2)
+    assert mod.device_status() == (2 if kind == "dopri5_capacity" else 4)
     with pytest.raises(RuntimeError, match="skipped by the step guard"):
         gs.check_status()
 
