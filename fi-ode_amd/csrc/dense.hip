@@ -536,3 +536,4 @@ extern "C" int fiode_dense_gemm(void* stream, int32_t batch, int32_t n, int32_t 
   else hipLaunchKernelGGL((k_dense_gemm<false, false>), grid, dim3(256), 0, st, n, A, B, C);
   DENSE_RET();
 }
+

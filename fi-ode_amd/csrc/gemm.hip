@@ -297,19 +297,27 @@ __global__ void __launch_bounds__(NT) k_gemm(GArgs a) {
 // by (row >> 1) & 7 on the SOURCE address (the DMA destination is lane-linear), so a ds_read_b128 of
 // 16 rows hits 16 distinct bank quads; a row-contiguous operand is [32 k][64 rows] as it lies in
 // memory, read with ds_read_b32 (lanes on consecutive rows: conflict-free).
-constexpr int DKC = 32, DIMG = 64 * DKC;                  // chunk k, floats per operand image
+constexpr int DKC = 32;                                   // the default chunk k (plan_of's unit)
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glob_void;
 
-template <bool KC_>
+// k-quad swizzle of a k-contiguous image row: 32-float rows (two rows per 64-bank line) by
+// (row >> 1) & 7, 64-float rows by row & 15 -- either way the 16 rows of a ds_read_b128 lane group
+// land on 16 distinct bank quads
+template <int KCH>
+__device__ __forceinline__ int qswz(int row) { return KCH == 32 ? ((row >> 1) & 7) : (row & 15); }
+
+template <bool KC_, int KCH>
 __device__ __forceinline__ void dma_chunk(float* img, const float* P, int64_t ld, int r0, int k0, int w, int lane) {
+  constexpr int NI = 64 * KCH / 256;                       // wave instructions per operand chunk
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int q = w + 4 * u;                               // wave instruction 0..7 of the chunk
+  for (int u = 0; u < NI / 4; ++u) {
+    const int q = w + 4 * u;
     const float* src;
-    if (KC_) {                                             // rows 8 q .. 8 q + 7, quads 0..7 each
-      const int r = 8 * q + (lane >> 3), p = lane & 7;
-      src = P + (int64_t)(r0 + r) * ld + k0 + 4 * (p ^ ((r >> 1) & 7));
+    if (KC_) {                                             // 1 KiB = 256 / KCH rows of KCH floats
+      constexpr int RPI = 256 / KCH, QPR = KCH / 4;
+      const int r = RPI * q + lane / QPR, p = lane % QPR;
+      src = P + (int64_t)(r0 + r) * ld + k0 + 4 * (p ^ qswz<KCH>(r));
     } else {                                               // k rows 4 q .. 4 q + 3, 16 quads each
       src = P + (int64_t)(k0 + 4 * q + (lane >> 4)) * ld + r0 + 4 * (lane & 15);
     }
@@ -317,10 +325,12 @@ __device__ __forceinline__ void dma_chunk(float* img, const float* P, int64_t ld
   }
 }
 
-template <bool AK, bool BK, int NSG, bool PREF>
+template <bool AK, bool BK, int NSG, int KCH>
 __global__ void __launch_bounds__(NT) k_gemm_dma(GArgs a) {
-  __shared__ __attribute__((aligned(16))) float sm[NSG * 2 * DIMG + 4];
-  int* lastp = reinterpret_cast<int*>(&sm[NSG * 2 * DIMG]);
+  constexpr int IMG = 64 * KCH;                             // floats per operand image
+  constexpr int PER_CHUNK = 2 * (64 * KCH / 256) / 4;       // glds per wave per chunk
+  __shared__ __attribute__((aligned(16))) float sm[NSG * 2 * IMG + 4];
+  int* lastp = reinterpret_cast<int*>(&sm[NSG * 2 * IMG]);
   const int u = (blockIdx.x & 7) * a.per + (blockIdx.x >> 3);       // XCD-aware, as k_gemm
   if (u >= a.units || a.dbg == 4) return;
   const int tm_ = u % a.tiles_m, rest = u / a.tiles_m;
@@ -333,65 +343,55 @@ __global__ void __launch_bounds__(NT) k_gemm_dma(GArgs a) {
   const int m0 = tm_ * BM, n0 = tn_ * BN;
   const float* A = a.A + (int64_t)z * a.sa;
   const float* B = a.B + (int64_t)z * a.sb;
-  const int c0 = s * a.cps, c1 = min(a.nch, c0 + a.cps), cl = max(c0, c1 - 1);
+  // chunks of KCH k (a.cps / a.nch count DKC-chunks: KCH / DKC of them per chunk here)
+  constexpr int R = KCH / DKC;
+  const int c0 = s * a.cps / R, c1 = (min(a.nch, s * a.cps + a.cps) + R - 1) / R, cl = max(c0, c1 - 1);
   auto slot_of = [&](int c) { return NSG == 4 ? ((c - c0) & 3) : ((c - c0) % NSG); };
   auto issue = [&](int c) {              // chunk min(c, cl) into ring slot (c - c0) % NSG
     const int slot = slot_of(c), cc = min(c, cl);
-    dma_chunk<AK>(&sm[(slot * 2 + 0) * DIMG], A, a.lda, m0, cc * DKC, w, lane);
-    dma_chunk<BK>(&sm[(slot * 2 + 1) * DIMG], B, a.ldb, n0, cc * DKC, w, lane);
+    dma_chunk<AK, KCH>(&sm[(slot * 2 + 0) * IMG], A, a.lda, m0, cc * KCH, w, lane);
+    dma_chunk<BK, KCH>(&sm[(slot * 2 + 1) * IMG], B, a.ldb, n0, cc * KCH, w, lane);
   };
   const int ra = 32 * wm + j, rb = 32 * wn + j;
   auto rd = [&](const float* ia, const float* ib, int t, f32x4& av, f32x4& bv) {
     const int qd = 2 * t + h;                              // k quad of this lane half
-    if (AK) av = *reinterpret_cast<const f32x4*>(ia + ra * DKC + 4 * (qd ^ ((ra >> 1) & 7)));
+    if (AK) av = *reinterpret_cast<const f32x4*>(ia + ra * KCH + 4 * (qd ^ qswz<KCH>(ra)));
     else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) av[e] = ia[(4 * qd + e) * 64 + ra];
     }
-    if (BK) bv = *reinterpret_cast<const f32x4*>(ib + rb * DKC + 4 * (qd ^ ((rb >> 1) & 7)));
+    if (BK) bv = *reinterpret_cast<const f32x4*>(ib + rb * KCH + 4 * (qd ^ qswz<KCH>(rb)));
     else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[e] = ib[(4 * qd + e) * 64 + rb];
     }
   };
-  // two accumulators, the k-steps alternating between them: one dependent 32x32x2 chain issues at
-  // about half the MFMA rate (each MFMA waits for the previous one's result), two interleaved
-  // chains keep the pipe full; summed once at the end
+  // two accumulators, the k-steps alternating between them (summed once at the end)
   f32x16 acc = f16_zero(), acc1 = f16_zero();
   if (c0 < c1 && a.dbg != 5) {
 #pragma unroll
     for (int i = 0; i < NSG - 1; ++i) issue(c0 + i);
     for (int c = c0; c < c1; ++c) {
-      // this wave's loads of chunk c are in LDS (its NSG - 2 newer chunks' 4 each stay in flight)
-      if (NSG == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (NSG == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      // this wave's loads of chunk c are in LDS (its NSG - 2 newer chunks' loads stay in flight)
+      if constexpr ((NSG - 2) * PER_CHUNK == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if constexpr ((NSG - 2) * PER_CHUNK == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr ((NSG - 2) * PER_CHUNK == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (and its reads of chunk c - 1 retired)
       __builtin_amdgcn_s_barrier();                       // ... and every other wave's
       if (a.dbg != 7) issue(c + NSG - 1);                 // into the slot chunk c - 1 used
-      const float* ia = &sm[(slot_of(c) * 2 + 0) * DIMG];
-      const float* ib = &sm[(slot_of(c) * 2 + 1) * DIMG];
+      const float* ia = &sm[(slot_of(c) * 2 + 0) * IMG];
+      const float* ib = &sm[(slot_of(c) * 2 + 1) * IMG];
       if (a.dbg == 6) {
         const float xa = __int_as_float(threadIdx.x), xb = __int_as_float(c);
 #pragma unroll
-        for (int t = 0; t < DKC / 4; ++t) {
+        for (int t = 0; t < KCH / 4; ++t) {
           acc = mfma32(xa, xb, acc);
           acc1 = mfma32(xa, xb, acc1);
         }
-      } else if (PREF) {                                   // every operand of the chunk first
-        f32x4 av[DKC / 8], bv[DKC / 8];
-#pragma unroll
-        for (int t = 0; t < DKC / 8; ++t) rd(ia, ib, t, av[t], bv[t]);
-#pragma unroll
-        for (int t = 0; t < DKC / 8; ++t)
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            acc = mfma32(av[t][e], bv[t][e], acc);
-            acc1 = mfma32(av[t][e + 1], bv[t][e + 1], acc1);
-          }
       } else {
 #pragma unroll
-        for (int t = 0; t < DKC / 8; ++t) {
+        for (int t = 0; t < KCH / 8; ++t) {
           f32x4 av, bv;
           rd(ia, ib, t, av, bv);
 #pragma unroll
@@ -505,17 +505,20 @@ extern "C" FIODE_API int fiode_gemm(void* stream, const fiode_gemm_desc* d, cons
   hipStream_t st = (hipStream_t)stream;
   if (dma) {
     const int v = gemm_variant();
-#define FIODE_DMA(NS_, PF_)                                                                                 \
+#define FIODE_DMA(NS_, KC2_)                                                                                \
   do {                                                                                                      \
-    if (ak && bk) hipLaunchKernelGGL((k_gemm_dma<true, true, NS_, PF_>), grid, dim3(NT), 0, st, a);          \
-    else if (ak) hipLaunchKernelGGL((k_gemm_dma<true, false, NS_, PF_>), grid, dim3(NT), 0, st, a);          \
-    else if (bk) hipLaunchKernelGGL((k_gemm_dma<false, true, NS_, PF_>), grid, dim3(NT), 0, st, a);          \
-    else hipLaunchKernelGGL((k_gemm_dma<false, false, NS_, PF_>), grid, dim3(NT), 0, st, a);                 \
+    if (ak && bk) hipLaunchKernelGGL((k_gemm_dma<true, true, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
+    else if (ak) hipLaunchKernelGGL((k_gemm_dma<true, false, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
+    else if (bk) hipLaunchKernelGGL((k_gemm_dma<false, true, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
+    else hipLaunchKernelGGL((k_gemm_dma<false, false, NS_, KC2_>), grid, dim3(NT), 0, st, a);                \
   } while (0)
-    if (v == 1) FIODE_DMA(4, false);
-    else if (v == 2) FIODE_DMA(3, true);
-    else if (v == 3) FIODE_DMA(3, false);
-    else FIODE_DMA(4, true);
+    // 64-k chunks in two stages where every split holds whole ones (measured fastest on the step's
+    // shapes: tools/probes/gemm_probe.py, profiles/r06i), else 32-k chunks in a ring of four
+    const bool k64 = d->K % 64 == 0 && p.cps % 2 == 0;
+    if (v == 1 && k64) FIODE_DMA(3, 64);
+    else if (v == 3) FIODE_DMA(3, 32);
+    else if (v == 2 || (v == 0 && k64)) FIODE_DMA(2, 64);
+    else FIODE_DMA(4, 32);
 #undef FIODE_DMA
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;

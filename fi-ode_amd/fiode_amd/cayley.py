@@ -606,6 +606,7 @@ def linear_head(mods, h: torch.Tensor):
                                l3.forward_weight(), l3.bias)
 
 
+
 class _GroupSortFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cdim: int):

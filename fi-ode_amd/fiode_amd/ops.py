@@ -639,6 +639,11 @@ def _mat_layout(X: torch.Tensor):
     return None
 
 
+# tools/ab_step.py's `lib_gemm` variant routes ops.mm through torch.matmul (hipBLASLt) to measure the
+# step against the library; the product never sets it
+MM_LIBRARY = False
+
+
 def _gemm_ws(dev: torch.device, nbytes: int) -> torch.Tensor:
     # one split-K workspace per stream (its counter words are zero on entry and left zero by every
     # call; calls on one stream are ordered, calls on two streams never share a workspace)
@@ -674,11 +679,24 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
         if beta != 0.0:
             raise ValueError("mm: beta needs out")
         out = torch.empty(oshape, dtype=torch.float32, device=dev)
-    elif tuple(out.shape) != oshape or not out.is_contiguous() or out.dtype != torch.float32 or out.device != dev:
-        raise ValueError(f"mm: out must be a contiguous float32 {oshape} tensor on {dev}")
+    elif (tuple(out.shape) != oshape or out.dtype != torch.float32 or out.device != dev or
+          (out.dim() == 2 and not (out.stride(1) == 1 and out.stride(0) >= N)) or
+          (out.dim() == 3 and not out.is_contiguous())):
+        raise ValueError(f"mm: out must be a float32 {oshape} tensor on {dev} with unit column stride "
+                         "(contiguous when batched)")
+    ldc = out.stride(-2) if out.dim() == 2 else N
     if bias is not None:
         bias = _need(bias.detach(), "bias", (N,), torch.float32, dev)
-    d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], N,
+    if MM_LIBRARY:              # measurement switch of tools/ab_step.py (`lib_gemm`): the library GEMM
+        r = torch.matmul(A, B)
+        r = r * alpha if alpha != 1.0 else r
+        if bias is not None:
+            r = r + bias
+        if beta != 0.0:
+            r = r + beta * out
+        out.copy_(r)
+        return out
+    d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], ldc,
                    A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
                    float(alpha), float(beta), int(split_k))
     lib = L.lib()

@@ -703,3 +703,4 @@ def test_block_inverse_timeout_poisons_instead_of_finite_wrong():
     again = _block_inverse(M)                       # the default bound is back
     torch.cuda.synchronize()
     assert torch.equal(again, ref)
+

@@ -249,6 +249,12 @@ def head_out_lib(m):
     RESTORE.append(lambda: setattr(CY, "HEAD_OUT_KERNEL", True))
 
 
+def lib_gemm(m):
+    from fiode_amd import ops as OPS
+    OPS.MM_LIBRARY = True         # every fiode_gemm product by torch.matmul (hipBLASLt) -- round 5's GEMMs
+    RESTORE.append(lambda: setattr(OPS, "MM_LIBRARY", False))
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -258,7 +264,7 @@ def dyn_wgrad_main(m):
 # variants of paths removed from the product after their A/B (the conv weight gradients on the map
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
-ALL = {"default": default, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+ALL = {"default": default, "lib_gemm": lib_gemm, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
