@@ -22,7 +22,7 @@ FUSED = ("k_static_proj", "k_lyap_prep", "k_lyap_fwd", "k_lyap_bwd", "k_lyap_wgr
          "k_groupsort_bwd", "k_ode", "k_dyn", "k_qp", "k_cert", "k_spec_dft", "k_spec_fwd", "k_spec_bwd",
          "k_spec_taps", "k_spec_gram", "k_spec_inv", "k_spec_qbot", "k_spec_ginv", "k_spec_kk", "k_spec_gv",
          "k_panel_pad", "k_panel_pivot", "k_panel_update", "k_sconv_rfft2", "k_sconv_irfft2", "k_small_cayley", "k_adam",
-         "k_ode_nll", "k_dense", "k_pinv", "k_cgemm")
+         "k_ode_nll", "k_dense", "k_pinv", "k_cgemm", "k_gemm")
 
 
 def short(name: str) -> str:
