@@ -57,6 +57,7 @@ struct GArgs {
   int tiles_m, tiles_n, tiles;  // output tiles per matrix
   int S, cps, nch;            // K splits, chunks per split, chunks
   int units, per;             // work units (batch x S x tiles) and units per XCD
+  int nvb;                    // virtual blocks (8 per)
   float* part;                // [batch][tiles][S][TILE_F]
   unsigned* cnt;              // [batch][tiles]
   int dbg;                    // probe knob (FIODE_GEMM_VARIANT 4: return at once; 5: no K loop; 6: no
@@ -205,16 +206,15 @@ __device__ __forceinline__ void gemm_finish(const GArgs& a, f32x16 acc, int z, i
 }
 
 template <bool AK, bool BK, bool VEC>
-__global__ void __launch_bounds__(NT) k_gemm(GArgs a) {
-  __shared__ __attribute__((aligned(16))) float sA[2][BM][SL];
-  __shared__ __attribute__((aligned(16))) float sB[2][BN][SL];
-  __shared__ int last;
+__device__ __forceinline__ void gemm_unit(const GArgs& a, int vb, float (*sA)[BM][SL], float (*sB)[BN][SL],
+                                          int* lastp) {
   // XCD-aware work mapping: blocks are dealt round-robin over the 8 XCDs (block b on XCD b % 8,
   // MI355X_MICROARCH.md; for speed only), so XCD x takes the contiguous run of work units
   // [x per, (x + 1) per) of the order (batch, split, column tile, row tile): the units of one XCD
   // share their K range (split) and B column block, which its L2 then holds once, instead of every
-  // XCD streaming the whole operand (W2 of the 4096 -> 512 map: 7.3 MB per XCD)
-  const int u = (blockIdx.x & 7) * a.per + (blockIdx.x >> 3);
+  // XCD streaming the whole operand (W2 of the 4096 -> 512 map: 7.3 MB per XCD).  vb: the virtual
+  // block (= blockIdx.x, or one of a capped grid's trips, which keep vb % 8 and so the XCD)
+  const int u = (vb & 7) * a.per + (vb >> 3);
   if (u >= a.units) return;                        // (uniform; no barrier yet)
   const int tm_ = u % a.tiles_m, rest = u / a.tiles_m;
   const int tn_ = rest % a.tiles_n, rest2 = rest / a.tiles_n;
@@ -281,7 +281,20 @@ __global__ void __launch_bounds__(NT) k_gemm(GArgs a) {
     __syncthreads();
   }
 
-  gemm_finish(a, acc + acc1, z, tile, s, m0, n0, &last);
+  gemm_finish(a, acc + acc1, z, tile, s, m0, n0, lastp);
+}
+
+// one workgroup per work unit, or (max_workgroups) a capped grid whose workgroups loop over the
+// virtual blocks b, b + grid, ... -- a narrow launch that leaves the other CUs to concurrent work
+template <bool AK, bool BK, bool VEC>
+__global__ void __launch_bounds__(NT) k_gemm(GArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[2][BM][SL];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN][SL];
+  __shared__ int last;
+  for (int vb = blockIdx.x; vb < a.nvb; vb += gridDim.x) {
+    gemm_unit<AK, BK, VEC>(a, vb, sA, sB, &last);
+    __syncthreads();                               // (uniform) LDS and `last` reused by the next trip
+  }
 }
 
 // ---- the LDS-DMA K loop (aligned shapes: M, N multiples of 64, K of 32, 16-B aligned operands) ----
@@ -325,13 +338,12 @@ __device__ __forceinline__ void dma_chunk(float* img, const float* P, int64_t ld
   }
 }
 
-template <bool AK, bool BK, int NSG, int KCH>
-__global__ void __launch_bounds__(NT) k_gemm_dma(GArgs a) {
+template <bool AK, bool BK, int NSG, int KCH, bool PF>
+__device__ __forceinline__ void gemm_dma_unit(const GArgs& a, int vb, float* sm) {
   constexpr int IMG = 64 * KCH;                             // floats per operand image
   constexpr int PER_CHUNK = 2 * (64 * KCH / 256) / 4;       // glds per wave per chunk
-  __shared__ __attribute__((aligned(16))) float sm[NSG * 2 * IMG + 4];
   int* lastp = reinterpret_cast<int*>(&sm[NSG * 2 * IMG]);
-  const int u = (blockIdx.x & 7) * a.per + (blockIdx.x >> 3);       // XCD-aware, as k_gemm
+  const int u = (vb & 7) * a.per + (vb >> 3);               // XCD-aware, as gemm_unit
   if (u >= a.units || a.dbg == 4) return;
   const int tm_ = u % a.tiles_m, rest = u / a.tiles_m;
   const int tn_ = rest % a.tiles_n, rest2 = rest / a.tiles_n;
@@ -389,6 +401,23 @@ __global__ void __launch_bounds__(NT) k_gemm_dma(GArgs a) {
           acc = mfma32(xa, xb, acc);
           acc1 = mfma32(xa, xb, acc1);
         }
+      } else if (PF) {
+        // the operands of k-group t + 1 read from LDS before group t's MFMAs are issued (two register
+        // sets), so an MFMA never waits on the read that feeds it
+        f32x4 av[2], bv[2];
+        rd(ia, ib, 0, av[0], bv[0]);
+#pragma unroll
+        for (int t = 0; t < KCH / 8; ++t) {
+          if (t + 1 < KCH / 8) rd(ia, ib, t + 1, av[(t + 1) & 1], bv[(t + 1) & 1]);
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            acc = mfma32(av[t & 1][e], bv[t & 1][e], acc);
+            acc1 = mfma32(av[t & 1][e + 1], bv[t & 1][e + 1], acc1);
+          }
+          // keep the schedule in that order: group t + 1's LDS reads, then group t's 4 MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
       } else {
 #pragma unroll
         for (int t = 0; t < KCH / 8; ++t) {
@@ -406,6 +435,30 @@ __global__ void __launch_bounds__(NT) k_gemm_dma(GArgs a) {
     __syncthreads();
   }
   gemm_finish(a, acc + acc1, z, tile, s, m0, n0, lastp);
+}
+
+template <bool AK, bool BK, int NSG, int KCH, bool PF = false>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) k_gemm_dma(GArgs a) {
+  __shared__ __attribute__((aligned(16))) float sm[NSG * 2 * 64 * KCH + 4];
+  for (int vb = blockIdx.x; vb < a.nvb; vb += gridDim.x) {   // (see k_gemm)
+    gemm_dma_unit<AK, BK, NSG, KCH, PF>(a, vb, sm);
+    __syncthreads();
+  }
+}
+
+// A capped (narrow) grid claims each CU's whole LDS: the dispatcher then puts no other LDS-using
+// workgroup on its CUs, so the concurrent kernels it is meant to leave room for land on the other CUs
+// instead of sharing SIMDs with it (measured: a 40-workgroup spectral inverse beside a 64-workgroup
+// capped GEMM ran 2.3x slower when both packed onto the same CUs).
+constexpr size_t LDS_PER_CU = 163840;
+template <typename Kern>
+void launch_gemm(Kern kern, dim3 grid, size_t static_lds, bool excl, hipStream_t st, const GArgs& a) {
+  size_t dyn = 0;
+  if (excl && static_lds + 512 < LDS_PER_CU) {
+    dyn = LDS_PER_CU - static_lds - 512;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(NT), dyn, st, a);
 }
 
 int gemm_variant() {
@@ -498,32 +551,43 @@ extern "C" FIODE_API int fiode_gemm(void* stream, const fiode_gemm_desc* d, cons
   a.S = p.S; a.cps = p.cps; a.nch = p.nch;
   a.units = d->batch * p.S * p.tiles;
   a.per = (a.units + 7) / 8;
+  a.nvb = 8 * a.per;
   a.cnt = p.S > 1 ? (unsigned*)workspace : nullptr;
   a.part = p.S > 1 ? (float*)((char*)workspace + CNT_BYTES) : nullptr;
   a.dbg = gemm_variant();
-  const dim3 grid((unsigned)(8 * a.per));
+  // max_workgroups: a persistent grid (a multiple of 8, so every trip keeps its XCD) that loops
+  int nb = a.nvb;
+  if (d->max_workgroups > 0 && d->max_workgroups < nb) nb = d->max_workgroups < 8 ? 8 : d->max_workgroups & ~7;
+  const dim3 grid((unsigned)nb);
+  const bool excl = nb < a.nvb;
   hipStream_t st = (hipStream_t)stream;
   if (dma) {
     const int v = gemm_variant();
-#define FIODE_DMA(NS_, KC2_)                                                                                \
+#define FIODE_DMA(NS_, KC2_, PF_)                                                                           \
   do {                                                                                                      \
-    if (ak && bk) hipLaunchKernelGGL((k_gemm_dma<true, true, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
-    else if (ak) hipLaunchKernelGGL((k_gemm_dma<true, false, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
-    else if (bk) hipLaunchKernelGGL((k_gemm_dma<false, true, NS_, KC2_>), grid, dim3(NT), 0, st, a);         \
-    else hipLaunchKernelGGL((k_gemm_dma<false, false, NS_, KC2_>), grid, dim3(NT), 0, st, a);                \
+    const size_t sl = (size_t)(NS_ * 2 * 64 * KC2_ + 4) * sizeof(float);                                     \
+    if (ak && bk) launch_gemm(k_gemm_dma<true, true, NS_, KC2_, PF_>, grid, sl, excl, st, a);                \
+    else if (ak) launch_gemm(k_gemm_dma<true, false, NS_, KC2_, PF_>, grid, sl, excl, st, a);                \
+    else if (bk) launch_gemm(k_gemm_dma<false, true, NS_, KC2_, PF_>, grid, sl, excl, st, a);                \
+    else launch_gemm(k_gemm_dma<false, false, NS_, KC2_, PF_>, grid, sl, excl, st, a);                       \
   } while (0)
-    // 64-k chunks in two stages where every split holds whole ones (measured fastest on the step's
-    // shapes: tools/probes/gemm_probe.py, profiles/r06i), else 32-k chunks in a ring of four
+    // 64-k chunks in two stages where every split holds whole ones, the LDS operands read one k-group
+    // ahead (measured fastest on the step's shapes: tools/probes/gemm_probe.py, profiles/r06/
+    // gemm_probe_prefetch.log), else 32-k chunks in a ring of four
     const bool k64 = d->K % 64 == 0 && p.cps % 2 == 0;
-    if (v == 1 && k64) FIODE_DMA(3, 64);
-    else if (v == 3) FIODE_DMA(3, 32);
-    else if (v == 2 || (v == 0 && k64)) FIODE_DMA(2, 64);
-    else FIODE_DMA(4, 32);
+    if (v == 1 && k64) FIODE_DMA(3, 64, false);
+    else if (v == 3) FIODE_DMA(3, 32, false);
+    else if (v == 8 && k64) FIODE_DMA(2, 64, true);
+    else if (v == 9) FIODE_DMA(4, 32, true);
+    else if (v == 2) FIODE_DMA(2, 64, false);
+    else if (v == 0 && k64) FIODE_DMA(2, 64, true);
+    else FIODE_DMA(4, 32, false);
 #undef FIODE_DMA
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
   }
-#define FIODE_GEMM_LAUNCH(AK_, BK_, V_) hipLaunchKernelGGL((k_gemm<AK_, BK_, V_>), grid, dim3(NT), 0, st, a)
+  const size_t sl = (size_t)(2 * 2 * BM * SL + 4) * sizeof(float);
+#define FIODE_GEMM_LAUNCH(AK_, BK_, V_) launch_gemm(k_gemm<AK_, BK_, V_>, grid, sl, excl, st, a)
   if (vec) {
     if (ak && bk) FIODE_GEMM_LAUNCH(true, true, true);
     else if (ak) FIODE_GEMM_LAUNCH(true, false, true);

@@ -82,7 +82,7 @@ class SpectralConfig(ct.Structure):
     _fields_ = [("cout", ct.c_int32), ("cin", ct.c_int32), ("ks", ct.c_int32), ("n", ct.c_int32)]
 
 
-ABI_VERSION = 4            # FIODE_ABI_VERSION (include/fiode.h)
+ABI_VERSION = 5            # FIODE_ABI_VERSION (include/fiode.h)
 FIODE_ODETRAIN_NSAVED = 14  # entries fiode_odetrain_saved_offsets writes
 FIODE_GUARD_MAX_STATUS = 4
 
@@ -115,7 +115,7 @@ class GemmDesc(ct.Structure):
     _fields_ = [("batch", ct.c_int32), ("M", ct.c_int32), ("N", ct.c_int32), ("K", ct.c_int32),
                 ("trans_a", ct.c_int32), ("trans_b", ct.c_int32), ("lda", ct.c_int64), ("ldb", ct.c_int64),
                 ("ldc", ct.c_int64), ("stride_a", ct.c_int64), ("stride_b", ct.c_int64), ("stride_c", ct.c_int64),
-                ("alpha", ct.c_float), ("beta", ct.c_float), ("split_k", ct.c_int32)]
+                ("alpha", ct.c_float), ("beta", ct.c_float), ("split_k", ct.c_int32), ("max_workgroups", ct.c_int32)]
 
 
 class CertifyConfig(ct.Structure):

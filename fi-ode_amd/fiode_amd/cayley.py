@@ -21,6 +21,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .streams import new_stream
+
 
 _BLOCK = 128
 
@@ -522,7 +524,7 @@ _HEAD_STREAMS: dict = {}
 def _head_stream(dev: torch.device) -> torch.cuda.Stream:
     key = dev.index
     if key not in _HEAD_STREAMS:
-        _HEAD_STREAMS[key] = torch.cuda.Stream(dev)
+        _HEAD_STREAMS[key] = new_stream(dev)
     return _HEAD_STREAMS[key]
 
 
@@ -793,7 +795,7 @@ CONV_WGRAD_SIDE = os.environ.get("FIODE_CONV_WGRAD_SIDE", "1") != "0"
 # (Their weight gradients on those streams instead of the head's side stream -- no join: 110-140 us
 # SLOWER in the step, profiles/r05an -- and one stream shared by all layers were measured and removed.)
 def _conv_map_stream(device) -> "torch.cuda.Stream":
-    return torch.cuda.Stream(device)
+    return new_stream(device)
 
 
 class CayleyConv(nn.Conv2d):

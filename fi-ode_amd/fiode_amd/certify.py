@@ -15,6 +15,7 @@ from typing import List, Optional
 import torch
 
 from . import ops
+from .streams import new_stream
 
 
 @dataclass
@@ -62,7 +63,7 @@ def certify_lipschitz(module, images: torch.Tensor, labels: torch.Tensor, T: int
     # status read (odeint: one host read per solve, as torchdiffeq raises) waits for that stream only,
     # and every result is read once after the loop -- no host round trip between images.
     main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
-    side = torch.cuda.Stream(dev) if main is not None else None
+    side = new_stream(dev) if main is not None else None
     pending = []
     with torch.no_grad():
         w = {k: v.detach().float().contiguous() for k, v in dyn.effective_weights().items()}

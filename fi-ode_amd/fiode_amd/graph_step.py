@@ -39,6 +39,8 @@ from typing import Optional
 
 import torch
 
+from .streams import distinct, new_stream
+
 # priority of the stream the step is captured on (its nodes' hardware queue; tools/ab_step.py cap_hi)
 CAPTURE_PRIORITY = 0
 
@@ -85,7 +87,7 @@ class GraphTrainStep:
         if comm not in ("graph", "eager"):
             raise ValueError(f"comm must be 'graph' or 'eager', got {comm!r}")
         self.comm = comm if multi else "none"
-        self.comm_stream = torch.cuda.Stream(dev) if self.comm == "graph" else None
+        self.comm_stream = new_stream(dev) if self.comm == "graph" else None
         dyn = module.dyn_fun
         if module.rng_counter is None:
             module.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -114,7 +116,7 @@ class GraphTrainStep:
         # parameters, the optimizer state and the Philox counter are restored afterwards (in place:
         # the captured graph must see the tensors the warm-up created).
         snap = self._snapshot()
-        side = torch.cuda.Stream(dev)
+        side = new_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for it in range(warmup):
@@ -133,8 +135,9 @@ class GraphTrainStep:
 
         if maps_ahead:
             self._maps_ahead_on()
-        if CAPTURE_PRIORITY:
-            self.capture_stream = torch.cuda.Stream(dev, priority=CAPTURE_PRIORITY)
+        # every capture (the first one included) on fresh dedicated streams made in the same order, so
+        # the placement trials compare like with like
+        self._fresh_streams()
         self.comm_fallback = None
         try:
             self._capture()
@@ -184,11 +187,17 @@ class GraphTrainStep:
                 self._between(warmup=False)
                 self.g_opt.replay()
 
-        def clock():
+        def clock(warm=0):
             # every trial replays from the same state (the adaptive solve's NFE follows the state)
             self._restore(snap)
             m.global_step = gstep
             self.refresh_maps()
+            for _ in range(warm):
+                replay()
+            if warm:
+                self._restore(snap)
+                m.global_step = gstep
+                self.refresh_maps()
             best = float("inf")
             for _ in range(2):
                 for _ in range(2):
@@ -213,11 +222,13 @@ class GraphTrainStep:
                 st["stream"] = cs
 
         dev = self.static_x.device
-        trials_t = [(clock(), streams())]
+        # the first trial's clock starts after ~0.1 s of replays: timed from a cold start it read
+        # ~9 % slow in every bench run (the GPU's clocks ramping), the later trials within 1 %
+        trials_t = [(clock(warm=80), streams())]
         for _ in range(trials - 1):
             # fresh pool streams for the maps' prefetch, the ODE solve, the conv maps computed ahead
             # and the capture itself
-            use((None, None, [torch.cuda.Stream(dev) for _ in stores], torch.cuda.Stream(dev, priority=CAPTURE_PRIORITY)))
+            self._fresh_streams()
             self._capture()
             trials_t.append((clock(), streams()))
         times = [t for t, _ in trials_t]
@@ -242,7 +253,36 @@ class GraphTrainStep:
         self.placement_ms = [round(t * 1e3, 4) for t in times]
         self.placement_pick = best
 
+    def _fresh_streams(self) -> None:
+        """New dedicated streams (fiode_amd.streams) for the module's map prefetch and ODE solve
+        (made at their first use in the capture), the conv maps computed ahead and the capture."""
+        m, dev = self.module, self.static_x.device
+        m._side_streams = m._ode_stream = None
+        for c in self.piped:
+            if getattr(c, "_store", None) is not None:
+                c._store["stream"] = new_stream(dev)
+        self.capture_stream = new_stream(dev, priority=CAPTURE_PRIORITY)
+
+    def role_streams(self) -> list:
+        """Every stream a capture of this step forks work to: the capture stream, the module's map
+        prefetch / ODE / weight-tap streams, the conv maps' streams, the comm stream and the
+        module-level head stream."""
+        from . import cayley as CY
+        m = self.module
+        out = [getattr(self, "capture_stream", None), getattr(self, "comm_stream", None),
+               getattr(m, "_ode_stream", None), getattr(m, "_wtap_stream", None)]
+        out += list(getattr(m, "_side_streams", None) or [])
+        out += [c._store["stream"] for c in self.piped if getattr(c, "_store", None) is not None]
+        out += list(CY._HEAD_STREAMS.values())
+        return out
+
     def _capture(self):
+        # two roles on one HIP stream can make a stream that joined the capture wait on an event it
+        # recorded itself, which this ROCm runtime answers with a host SIGSEGV in hipStreamEndCapture
+        # (streams.py); the product's streams are dedicated, so this only trips on a caller's own
+        if not distinct(self.role_streams()):
+            raise RuntimeError("GraphTrainStep: two roles of the captured step share one HIP stream "
+                               "(use fiode_amd.streams.new_stream for side streams, not the torch pool)")
         self.one_graph = self.single or self.comm == "graph"
         # capture_error_mode "thread_local": the process group's watchdog thread polls its events
         # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it

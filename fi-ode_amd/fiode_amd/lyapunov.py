@@ -28,6 +28,7 @@ from .models import IVP, DefaultOutputFun
 from .odeint import make_solver_params
 from .optim import FiodeAdam, FiodeAdamW
 from .sampling import CompositeSampler, CompositeSamplerScheduler, TrajectorySampler
+from .streams import new_stream
 
 
 class LyapunovLossFn(torch.autograd.Function):
@@ -551,10 +552,10 @@ class LyapunovLearning(nn.Module):
 
             late = getattr(self, "_prefetch_late_at", None)   # the maps after the first: after this conv layer
 
+            last = max(x for x in (at, late) if x is not None)
+
             def hook(i, _t=target, _at=at):
                 if i == _at or (late is not None and i == late):
-                    if late is None or i == late:
-                        _t.after_conv_hook = None
                     self._in_input_hook = True
                     self._prefetch_part = None if late is None else ("first" if i == _at else "rest")
                     try:
@@ -562,10 +563,12 @@ class LyapunovLearning(nn.Module):
                     finally:
                         self._in_input_hook = False
                         self._prefetch_part = None
+                if i >= last:
+                    _t.after_conv_hook = None
             target.after_conv_hook = hook
             return
         if self._side_streams is None:
-            self._side_streams = [torch.cuda.Stream(device) for _ in range(4)]
+            self._side_streams = [new_stream(device) for _ in range(4)]
         s = self._side_streams
         convs, lins = [], []
         for m in self.init_coordinates.modules():
@@ -706,7 +709,7 @@ class LyapunovLearning(nn.Module):
         if static_state.is_cuda and self.parallel_cayley and getattr(self, "ode_side_stream", True):
             from .cayley import _prefetch
             if getattr(self, "_ode_stream", None) is None:
-                self._ode_stream = torch.cuda.Stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
+                self._ode_stream = new_stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
             return _prefetch(self._ode_stream, lambda: ODETrainFn.apply(*args))
         return ODETrainFn.apply(*args)
 
@@ -723,14 +726,14 @@ class LyapunovLearning(nn.Module):
         stream = None
         if self.parallel_cayley and getattr(self, "ode_side_stream", True):
             if getattr(self, "_ode_stream", None) is None:
-                self._ode_stream = torch.cuda.Stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
+                self._ode_stream = new_stream(static_state.device, priority=getattr(self, "_ode_prio", -1))
             stream = self._ode_stream
         p = min(0.98, (self.current_epoch - self.train_ode_epoch) / 50.0)
         keys = ("Q1", "b1", "Qx", "bx", "Q2", "b2", "Q3", "b3")
         if DYN_WGRAD_SIDE and static_state.is_cuda and torch.is_grad_enabled():
             box = {}
             if getattr(self, "_wtap_stream", None) is None:
-                self._wtap_stream = torch.cuda.Stream(static_state.device)
+                self._wtap_stream = new_stream(static_state.device)
             side, main = self._wtap_stream, torch.cuda.current_stream(static_state.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):

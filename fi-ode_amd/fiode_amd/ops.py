@@ -651,11 +651,13 @@ def _gemm_ws(dev: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
-       bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0) -> torch.Tensor:
+       bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0,
+       max_workgroups: int = 0) -> torch.Tensor:
     """fiode_gemm: out = alpha A @ B + beta out + bias, float32, A [(b,) M, K], B [(b,) K, N] (a 2-D
     operand is shared by every batch entry), bias [N].  Either operand may be a transposed view of
     row-major memory (``W.t()``, ``X.mT``, a column slice): the kernel reads it in place.  The hand-
-    written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip)."""
+    written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip).
+    ``max_workgroups``: a capped, persistent grid (a narrow launch beside other work; 0 = none)."""
     dev = B.device
     if A.dtype != torch.float32 or B.dtype != torch.float32 or A.device != dev or dev.type != "cuda":
         raise ValueError(f"mm: float32 ROCm operands, got {A.dtype} on {A.device}, {B.dtype} on {B.device}")
@@ -698,7 +700,7 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
         return out
     d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], ldc,
                    A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
-                   float(alpha), float(beta), int(split_k))
+                   float(alpha), float(beta), int(split_k), int(max_workgroups))
     lib = L.lib()
     nb = lib.fiode_gemm_workspace_bytes(ct.byref(d))
     ws = _gemm_ws(dev, nb) if nb else None

@@ -24,8 +24,10 @@ extern "C" {
 #endif
 
 /* ABI 4 (round 6): fiode_sconv_config gained `nchw` (20 bytes, was 16), the one-launch block inverse
-   (n = 128 .. 512) needs a larger workspace (fiode_block_inverse_workspace_bytes), fiode_gemm added. */
-#define FIODE_ABI_VERSION 4
+   (n = 128 .. 512) needs a larger workspace (fiode_block_inverse_workspace_bytes), fiode_gemm added.
+   ABI 5: fiode_gemm_desc gained `max_workgroups` (in what was its tail padding; the size is unchanged,
+   so a caller built against ABI 4 would pass an undefined value there). */
+#define FIODE_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define FIODE_API __attribute__((visibility("default")))
@@ -428,6 +430,10 @@ typedef struct fiode_gemm_desc {
   int64_t stride_a, stride_b, stride_c;   /* elements between batch entries */
   float alpha, beta;
   int32_t split_k;                        /* 0: the library's choice */
+  int32_t max_workgroups;                 /* 0: one workgroup per 64 x 64 tile (x split); else at most
+                                             this many (rounded down to a multiple of 8, >= 8), each
+                                             looping over tiles: a narrow launch that leaves the other
+                                             CUs to concurrent work (ABI 5) */
 } fiode_gemm_desc;
 FIODE_API int32_t fiode_gemm_splits(const fiode_gemm_desc* d);
 FIODE_API size_t fiode_gemm_counter_bytes(const fiode_gemm_desc* d);

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from fiode_amd import _lib
     lib = _lib.lib()
-    assert lib.fiode_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.fiode_abi_version() == _lib.ABI_VERSION == 5
     hdr = (pathlib.Path(__file__).resolve().parents[1] / "include" / "fiode.h").read_text()
     for name in ("FIODE_ABI_VERSION", "FIODE_ODETRAIN_NSAVED"):
         val = int(re.search(r"#define %s (\d+)" % name, hdr).group(1))

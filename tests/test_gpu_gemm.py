@@ -156,3 +156,20 @@ def test_calls_of_different_shapes_share_the_workspace():
         _check(C1, A1, B1)
         _check(C2, A2, B2)
         _check(C3, A1, B1)
+
+
+@pytest.mark.parametrize("M,K,N,cap", [(512, 3584, 512, 64), (512, 512, 3584, 64), (512, 512, 3584, 8),
+                                       (130, 70, 90, 8), (128, 4096, 512, 16)])
+def test_capped_grid_equals_full_grid(M, K, N, cap):
+    """max_workgroups (a persistent grid looping over the tiles, split-K included) computes the same
+    bits as one workgroup per tile: the same tiles, the same k order, the same split order."""
+    from fiode_amd import ops
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(M + K + N)
+    A = torch.randn(M, K, generator=g).to(dev)
+    B = torch.randn(K, N, generator=g).to(dev)
+    full = ops.mm(A, B)
+    capped = ops.mm(A, B, max_workgroups=cap)
+    torch.cuda.synchronize()
+    assert torch.equal(full, capped)
+    _check(capped, A, B)

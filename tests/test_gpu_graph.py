@@ -253,3 +253,27 @@ def test_placement_trials_keep_results_bit_identical():
     assert len(out[3][0]) == 3 and out[1][0] == out[3][0]
     for a, b in zip(out[1][1], out[3][1]):
         assert torch.equal(a, b)
+
+
+def test_placement_trials_use_distinct_dedicated_streams():
+    """The placement trials' fresh side streams are streams of their own (fiode_amd.streams), never
+    torch pool streams that could alias another role's stream: after the trials every role stream of
+    the kept capture is a distinct HIP stream, and the capture-time check refuses an aliased one."""
+    import bench
+    from fiode_amd import cayley as CY, streams
+    from fiode_amd.graph_step import GraphTrainStep
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
+    y = torch.randint(0, 10, (32,), generator=g).to(dev)
+    mod = bench.build_module(dev, seed=0, train_ode=True)
+    opt = mod.configure_optimizers(capturable=True)[0][0]
+    gs = GraphTrainStep(mod, opt, x, y, warmup=2, placement_trials=4)
+    roles = [s for s in gs.role_streams() if s is not None]
+    assert len(roles) >= 8 and streams.distinct(roles)
+    gs.step()
+    torch.cuda.synchronize()
+    mod._wtap_stream = CY._head_stream(dev)          # two roles on one stream: refused before capturing
+    with pytest.raises(RuntimeError, match="share one HIP stream"):
+        gs._capture()
+    gs.close()

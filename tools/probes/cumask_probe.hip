@@ -97,5 +97,19 @@ int main() {
   hipStreamSynchronize(plain);
   hipMemcpy(h, d, 2 * n * sizeof(unsigned), hipMemcpyDeviceToHost);
   report("fork to masked inside a plain capture", h, n);
+  // how mask bits map to XCDs: every 8th bit (i % 8 == 0), and its complement
+  for (int pat = 0; pat < 3; ++pat) {
+    std::vector<uint32_t> m(8, 0u);
+    for (int i = 0; i < 256; ++i) {
+      const bool on = pat == 0 ? (i % 8 == 0) : pat == 1 ? (i % 8 != 0) : (i / 32 != 0);
+      if (on) m[i / 32] |= 1u << (i % 32);
+    }
+    hipStream_t s;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()) != hipSuccess) {
+      printf("mask pattern %d refused\n", pat);
+      continue;
+    }
+    run(s, pat == 0 ? "mask bits i%8==0 (eager)" : pat == 1 ? "mask bits i%8!=0 (eager)" : "mask bits 32..255 (eager)");
+  }
   return 0;
 }

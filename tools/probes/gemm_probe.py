@@ -83,7 +83,7 @@ def main():
             if s > (K + 31) // 32:
                 continue
             sweep[s] = round(timeit(lambda: ops.mm(A, B, out=out, split_k=s), reps), 2)
-        for v in (1, 2, 3, 5):
+        for v in [int(t) for t in os.environ.get("GEMM_PROBE_VARIANTS", "1,2,3,5").split(",")]:
             os.environ["FIODE_GEMM_VARIANT"] = str(v)
             sweep[f"v{v}"] = round(timeit(lambda: ops.mm(A, B, out=out), reps), 2)
             os.environ["FIODE_GEMM_VARIANT"] = "0"
