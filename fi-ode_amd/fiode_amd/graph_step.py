@@ -187,17 +187,11 @@ class GraphTrainStep:
                 self._between(warmup=False)
                 self.g_opt.replay()
 
-        def clock(warm=0):
+        def clock():
             # every trial replays from the same state (the adaptive solve's NFE follows the state)
             self._restore(snap)
             m.global_step = gstep
             self.refresh_maps()
-            for _ in range(warm):
-                replay()
-            if warm:
-                self._restore(snap)
-                m.global_step = gstep
-                self.refresh_maps()
             best = float("inf")
             for _ in range(2):
                 for _ in range(2):
@@ -222,9 +216,7 @@ class GraphTrainStep:
                 st["stream"] = cs
 
         dev = self.static_x.device
-        # the first trial's clock starts after ~0.1 s of replays: timed from a cold start it read
-        # ~9 % slow in every bench run (the GPU's clocks ramping), the later trials within 1 %
-        trials_t = [(clock(warm=80), streams())]
+        trials_t = [(clock(), streams())]
         for _ in range(trials - 1):
             # fresh pool streams for the maps' prefetch, the ODE solve, the conv maps computed ahead
             # and the capture itself
