@@ -461,6 +461,22 @@ void launch_gemm(Kern kern, dim3 grid, size_t static_lds, bool excl, hipStream_t
   hipLaunchKernelGGL(kern, grid, dim3(NT), dyn, st, a);
 }
 
+// Two independent products in ONE launch (fiode_gemm_pair): virtual blocks [0, a0.nvb) are problem
+// 0's, the rest problem 1's (a0.nvb is a multiple of 8, so every block keeps its XCD's share of
+// either problem).  Each tile is computed exactly as fiode_gemm computes it (same k order, same
+// split order): the pair is bit-identical to the two calls.  The 64-k, two-stage, prefetching K loop
+// only; other shapes take two launches.
+template <bool AK0, bool BK0, bool AK1, bool BK1>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 2))) k_gemm_dma_pair(GArgs a0, GArgs a1) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * 2 * 64 * 64 + 4];
+  const int n0 = a0.nvb, n = n0 + a1.nvb;
+  for (int vb = blockIdx.x; vb < n; vb += gridDim.x) {
+    if (vb < n0) gemm_dma_unit<AK0, BK0, 2, 64, true>(a0, vb, sm);
+    else gemm_dma_unit<AK1, BK1, 2, 64, true>(a1, vb - n0, sm);
+    __syncthreads();
+  }
+}
+
 int gemm_variant() {
   const char* e = getenv("FIODE_GEMM_VARIANT");           // probe knob: 0 = default
   return e && *e ? atoi(e) : 0;
@@ -602,4 +618,87 @@ extern "C" FIODE_API int fiode_gemm(void* stream, const fiode_gemm_desc* d, cons
 #undef FIODE_GEMM_LAUNCH
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
+}
+
+namespace {
+// The checks and kernel arguments of one fiode_gemm product; cnt / part: its counter words and
+// partial-tile region.  ok_pair: the product takes the 64-k prefetching DMA loop (the pair kernel's).
+int gemm_prepare(const fiode_gemm_desc* d, const float* A, const float* B, const float* bias, float* C, unsigned* cnt,
+                 float* part, GArgs& a, bool& ok_pair, bool& ak, bool& bk) {
+  Plan p;
+  if (!plan_of(d, p)) return FIODE_EINVAL;
+  if (!C || (d->K > 0 && (!A || !B))) return FIODE_EINVAL;
+  const bool ta = d->trans_a != 0, tb = d->trans_b != 0;
+  if (d->ldc < d->N || d->lda < (ta ? d->M : d->K) || d->ldb < (tb ? d->K : d->N)) return FIODE_ESHAPE;
+  ak = !ta;
+  bk = tb;
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const bool k64 = d->K % 64 == 0 && p.cps % 2 == 0;
+  ok_pair = p.dma && al16(A) && al16(B) && k64 && gemm_variant() == 0 && d->max_workgroups == 0 && d->M > 0 &&
+            d->N > 0;
+  a.M = d->M; a.N = d->N; a.K = d->K;
+  a.A = A; a.B = B; a.C = C; a.bias = bias;
+  a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+  a.sa = d->stride_a; a.sb = d->stride_b; a.sc = d->stride_c;
+  a.alpha = d->alpha; a.beta = d->beta;
+  a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n; a.tiles = p.tiles;
+  a.S = p.S; a.cps = p.cps; a.nch = p.nch;
+  a.units = d->batch * p.S * p.tiles;
+  a.per = (a.units + 7) / 8;
+  a.nvb = 8 * a.per;
+  a.cnt = p.S > 1 ? cnt : nullptr;
+  a.part = p.S > 1 ? part : nullptr;
+  a.dbg = 0;
+  return FIODE_OK;
+}
+}  // namespace
+
+extern "C" FIODE_API size_t fiode_gemm_pair_workspace_bytes(const fiode_gemm_desc* d0, const fiode_gemm_desc* d1) {
+  const size_t w0 = fiode_gemm_workspace_bytes(d0), w1 = fiode_gemm_workspace_bytes(d1);
+  if (!w0 && !w1) return 0;
+  return CNT_BYTES + (w0 ? w0 - CNT_BYTES : 0) + (w1 ? w1 - CNT_BYTES : 0);
+}
+
+extern "C" FIODE_API int fiode_gemm_pair(void* stream, const fiode_gemm_desc* d0, const float* A0, const float* B0,
+                                         const float* bias0, float* C0, const fiode_gemm_desc* d1, const float* A1,
+                                         const float* B1, const float* bias1, float* C1, void* workspace,
+                                         size_t workspace_bytes) {
+  if (!d0 || !d1) return FIODE_EINVAL;
+  const size_t need = fiode_gemm_pair_workspace_bytes(d0, d1);
+  if (need && (!workspace || workspace_bytes < need)) return FIODE_EWORKSPACE;
+  const size_t w0 = fiode_gemm_workspace_bytes(d0);
+  Plan p0;
+  if (!plan_of(d0, p0)) return FIODE_EINVAL;
+  unsigned* cnt = reinterpret_cast<unsigned*>(workspace);
+  float* part = workspace ? reinterpret_cast<float*>(static_cast<char*>(workspace) + CNT_BYTES) : nullptr;
+  // problem 1's counters follow problem 0's tiles in the fixed block; its partials follow problem 0's
+  const int64_t c1 = (int64_t)d0->batch * p0.tiles;
+  GArgs a0, a1;
+  bool ok0, ok1, ak0, bk0, ak1, bk1;
+  int rc = gemm_prepare(d0, A0, B0, bias0, C0, cnt, part, a0, ok0, ak0, bk0);
+  if (rc != FIODE_OK) return rc;
+  rc = gemm_prepare(d1, A1, B1, bias1, C1, cnt ? cnt + c1 : nullptr,
+                    part ? part + (w0 ? (w0 - CNT_BYTES) / sizeof(float) : 0) : nullptr, a1, ok1, ak1, bk1);
+  if (rc != FIODE_OK) return rc;
+  Plan p1;
+  plan_of(d1, p1);
+  const bool fits = c1 + (int64_t)d1->batch * p1.tiles <= CNT_WORDS;
+  hipStream_t st = (hipStream_t)stream;
+  if (ok0 && ok1 && fits) {
+    const dim3 grid((unsigned)(a0.nvb + a1.nvb));
+#define FIODE_PAIR(X0, Y0, X1, Y1)                                                                     \
+    if (ak0 == X0 && bk0 == Y0 && ak1 == X1 && bk1 == Y1) {                                         \
+      hipLaunchKernelGGL((k_gemm_dma_pair<X0, Y0, X1, Y1>), grid, dim3(NT), 0, st, a0, a1);        \
+      const hipError_t e = hipGetLastError();                                                        \
+      return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;                                       \
+    }
+    // the dense maps' backward pair A = V'^T Gb with P2 = inv Gb^T (wide maps; tall: the mirror)
+    FIODE_PAIR(true, true, true, false)
+    FIODE_PAIR(false, false, true, true)
+#undef FIODE_PAIR
+  }
+  // any other pair: the two products one after the other (the same results)
+  rc = fiode_gemm(stream, d0, A0, B0, bias0, C0, workspace, workspace_bytes);
+  if (rc != FIODE_OK) return rc;
+  return fiode_gemm(stream, d1, A1, B1, bias1, C1, workspace, workspace_bytes);
 }

@@ -200,6 +200,9 @@ def _load():
         "fiode_gemm_counter_bytes": (ct.c_size_t, [ct.POINTER(GemmDesc)]),
         "fiode_gemm_workspace_bytes": (ct.c_size_t, [ct.POINTER(GemmDesc)]),
         "fiode_gemm": (ct.c_int, [_vp, ct.POINTER(GemmDesc), _vp, _vp, _vp, _vp, _vp, ct.c_size_t]),
+        "fiode_gemm_pair_workspace_bytes": (ct.c_size_t, [ct.POINTER(GemmDesc), ct.POINTER(GemmDesc)]),
+        "fiode_gemm_pair": (ct.c_int, [_vp, ct.POINTER(GemmDesc), _vp, _vp, _vp, _vp, ct.POINTER(GemmDesc), _vp, _vp,
+                                       _vp, _vp, _vp, ct.c_size_t]),
         "fiode_sconv_rfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),
         "fiode_sconv_irfft2": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, ct.c_int32, _vp, _vp]),
         "fiode_sconv_rfft2_nchw": (ct.c_int, [_vp, ct.POINTER(SconvConfig), _vp, _vp, _vp, _vp]),

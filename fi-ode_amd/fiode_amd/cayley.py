@@ -204,11 +204,13 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     gQb = gQ.reshape(b, cout, cin).contiguous()
     cfg = L.DenseConfig(b, cout, cin)
     lib, st = L.lib(), ops._stream(Wb.device)
-    Vp = Gb = A = None
+    Vp = Gb = A = P2 = None
     if R > k:
         Vp = Wb[:, :, k:].mT if wide else Wb[:, k:, :]
         Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
-        A = ops.mm(Vp.mT, Gb)
+        # A = V'^T Gb and P2 = Gb inv^T (W layout; wide: inv gQ[:, k:]) need only the inputs: one launch
+        # for both (fiode_gemm_pair), so P2 leaves the A -> Ginv -> GMn -> H -> P1 chain
+        A, P2 = ops.mm_pair(Vp.mT, Gb, inv, gQb[:, :, k:]) if wide else ops.mm_pair(Vp.mT, Gb, Gb, inv.mT)
     Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
                                         ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
@@ -226,14 +228,9 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
     H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
             "fiode_dense_cayley_h")
-    P1 = P2 = None                  # V' H and Gb inv^T in W's layout (wide: H^T W[:, k:], inv gQ[:, k:])
+    P1 = None                       # V' H in W's layout (wide: H^T W[:, k:])
     if R > k:
-        if wide:
-            P1 = ops.mm(H.mT, Wb[:, :, k:])
-            P2 = ops.mm(inv, gQb[:, :, k:])
-        else:
-            P1 = ops.mm(Vp, H)
-            P2 = ops.mm(Gb, ih)
+        P1 = ops.mm(H.mT, Wb[:, :, k:]) if wide else ops.mm(Vp, H)
     gW = torch.empty_like(Wb)
     ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
     ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,

@@ -642,6 +642,8 @@ def _mat_layout(X: torch.Tensor):
 # tools/ab_step.py's `lib_gemm` variant routes ops.mm through torch.matmul (hipBLASLt) to measure the
 # step against the library; the product never sets it
 MM_LIBRARY = False
+# the dense maps' backward pair (A, P2) in one fiode_gemm_pair launch (tools/ab_step.py `no_pair`: two launches)
+MM_PAIR = True
 
 
 def _gemm_ws(dev: torch.device, nbytes: int) -> torch.Tensor:
@@ -650,14 +652,10 @@ def _gemm_ws(dev: torch.device, nbytes: int) -> torch.Tensor:
     return _Workspace.get(dev, nbytes, f"gemm{torch.cuda.current_stream(dev).cuda_stream}", zero=True)
 
 
-def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
-       bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0,
-       max_workgroups: int = 0) -> torch.Tensor:
-    """fiode_gemm: out = alpha A @ B + beta out + bias, float32, A [(b,) M, K], B [(b,) K, N] (a 2-D
-    operand is shared by every batch entry), bias [N].  Either operand may be a transposed view of
-    row-major memory (``W.t()``, ``X.mT``, a column slice): the kernel reads it in place.  The hand-
-    written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip).
-    ``max_workgroups``: a capped, persistent grid (a narrow launch beside other work; 0 = none)."""
+def _gemm_operands(A: torch.Tensor, B: torch.Tensor, alpha: float, beta: float, bias, out, split_k: int,
+                   max_workgroups: int):
+    """The fiode_gemm_desc of out = alpha A @ B + beta out + bias, with the operands as the kernel reads
+    them (a view it cannot read in place copied) and the output allocated when not given."""
     dev = B.device
     if A.dtype != torch.float32 or B.dtype != torch.float32 or A.device != dev or dev.type != "cuda":
         raise ValueError(f"mm: float32 ROCm operands, got {A.dtype} on {A.device}, {B.dtype} on {B.device}")
@@ -689,6 +687,22 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
     ldc = out.stride(-2) if out.dim() == 2 else N
     if bias is not None:
         bias = _need(bias.detach(), "bias", (N,), torch.float32, dev)
+    d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], ldc,
+                   A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
+                   float(alpha), float(beta), int(split_k), int(max_workgroups))
+    return d, A, B, bias, out
+
+
+def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
+       bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0,
+       max_workgroups: int = 0) -> torch.Tensor:
+    """fiode_gemm: out = alpha A @ B + beta out + bias, float32, A [(b,) M, K], B [(b,) K, N] (a 2-D
+    operand is shared by every batch entry), bias [N].  Either operand may be a transposed view of
+    row-major memory (``W.t()``, ``X.mT``, a column slice): the kernel reads it in place.  The hand-
+    written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip).
+    ``max_workgroups``: a capped, persistent grid (a narrow launch beside other work; 0 = none)."""
+    dev = B.device
+    d, A, B, bias, out = _gemm_operands(A, B, alpha, beta, bias, out, split_k, max_workgroups)
     if MM_LIBRARY:              # measurement switch of tools/ab_step.py (`lib_gemm`): the library GEMM
         r = torch.matmul(A, B)
         r = r * alpha if alpha != 1.0 else r
@@ -698,6 +712,29 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
             r = r + beta * out
         out.copy_(r)
         return out
+    lib = L.lib()
+    nb = lib.fiode_gemm_workspace_bytes(ct.byref(d))
+    ws = _gemm_ws(dev, nb) if nb else None
+    L.check(lib.fiode_gemm(_stream(dev), ct.byref(d), A.data_ptr(), B.data_ptr(), _ptr(bias), out.data_ptr(),
+                           _ptr(ws), ws.numel() if ws is not None else 0), "fiode_gemm")
+    return out
+
+
+def mm_pair(A0: torch.Tensor, B0: torch.Tensor, A1: torch.Tensor, B1: torch.Tensor):
+    """fiode_gemm_pair: (A0 @ B0, A1 @ B1) -- two independent products in one launch, each the same
+    bits as ``mm`` computes it."""
+    if MM_LIBRARY or not MM_PAIR:
+        return mm(A0, B0), mm(A1, B1)
+    dev = B0.device
+    d0, A0, B0, _, C0 = _gemm_operands(A0, B0, 1.0, 0.0, None, None, 0, 0)
+    d1, A1, B1, _, C1 = _gemm_operands(A1, B1, 1.0, 0.0, None, None, 0, 0)
+    lib = L.lib()
+    nb = lib.fiode_gemm_pair_workspace_bytes(ct.byref(d0), ct.byref(d1))
+    ws = _gemm_ws(dev, nb) if nb else None
+    L.check(lib.fiode_gemm_pair(_stream(dev), ct.byref(d0), A0.data_ptr(), B0.data_ptr(), None, C0.data_ptr(),
+                                ct.byref(d1), A1.data_ptr(), B1.data_ptr(), None, C1.data_ptr(), _ptr(ws),
+                                ws.numel() if ws is not None else 0), "fiode_gemm_pair")
+    return C0, C1
     d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], ldc,
                    A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
                    float(alpha), float(beta), int(split_k), int(max_workgroups))

@@ -440,6 +440,14 @@ FIODE_API size_t fiode_gemm_counter_bytes(const fiode_gemm_desc* d);
 FIODE_API size_t fiode_gemm_workspace_bytes(const fiode_gemm_desc* d);
 FIODE_API int fiode_gemm(void* stream, const fiode_gemm_desc* d, const float* A, const float* B, const float* bias,
                          float* C, void* workspace, size_t workspace_bytes);
+/* Two independent products in one launch (the dense maps' backward A = V'^T Gb beside P2 = Gb inv^T),
+ * each bit-identical to its own fiode_gemm call; shapes the one-launch kernel does not take run as
+ * two launches.  Workspace: fiode_gemm_pair_workspace_bytes (counters zero before the first call). */
+FIODE_API size_t fiode_gemm_pair_workspace_bytes(const fiode_gemm_desc* d0, const fiode_gemm_desc* d1);
+FIODE_API int fiode_gemm_pair(void* stream, const fiode_gemm_desc* d0, const float* A0, const float* B0,
+                              const float* bias0, float* C0, const fiode_gemm_desc* d1, const float* A1,
+                              const float* B1, const float* bias1, float* C1, void* workspace,
+                              size_t workspace_bytes);
 
 /* ---- spectral convolution transforms on spatial-major activations [n][n][C][B] (CayleyConv
  * forward_hwcb; fiode_amd/cayley.py).  Spectrum layout [f][C][B] complex64, f = ka (n/2+1) + kb. */

@@ -173,3 +173,33 @@ def test_capped_grid_equals_full_grid(M, K, N, cap):
     torch.cuda.synchronize()
     assert torch.equal(full, capped)
     _check(capped, A, B)
+
+
+@pytest.mark.parametrize("wide", [True, False])
+def test_pair_equals_two_calls(wide):
+    """fiode_gemm_pair (two products in one launch: the dense maps' backward A = V'^T Gb beside
+    P2 = Gb inv^T) gives the same bits as the two fiode_gemm calls, for the wide map's operand views
+    and the tall mirror, and shapes the one-launch kernel does not take fall back to two launches."""
+    from fiode_amd import ops
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(17 + wide)
+    k, R = 512, 4096
+    W = torch.randn(1, k, R, generator=g).to(dev) if wide else torch.randn(1, R, k, generator=g).to(dev)
+    gQ = torch.randn_like(W)
+    inv = torch.randn(1, k, k, generator=g).to(dev)
+    if wide:
+        Vp, Gb = W[:, :, k:].mT, gQ[:, :, k:].mT
+        ops_ = (Vp.mT, Gb, inv, gQ[:, :, k:])
+    else:
+        Vp, Gb = W[:, k:, :], gQ[:, k:, :]
+        ops_ = (Vp.mT, Gb, Gb, inv.mT)
+    A0, P0 = ops.mm(ops_[0], ops_[1]), ops.mm(ops_[2], ops_[3])
+    A1, P1 = ops.mm_pair(*ops_)
+    torch.cuda.synchronize()
+    assert torch.equal(A0, A1) and torch.equal(P0, P1)
+    _check(A1[0], ops_[0][0], ops_[1][0])
+    # a ragged pair (register K loop): two launches, same bits
+    X, Y = torch.randn(70, 33, generator=g).to(dev), torch.randn(33, 50, generator=g).to(dev)
+    r0, r1 = ops.mm_pair(X, Y, Y.t(), X.t())
+    torch.cuda.synchronize()
+    assert torch.equal(r0, ops.mm(X, Y)) and torch.equal(r1, ops.mm(Y.t(), X.t()))

@@ -25,11 +25,11 @@ for B, sn in ((128, False), (128, True), (1024, False)):
     lib.fiode_odetrain_saved_offsets(ct.byref(cfg), ct.cast(offs, ct.c_void_p))
     al = lambda v: (v + 255) & ~255
     xs = offs[7] + al(B * E * 10 * 4)
-    prof = ws[xs + (2 * E * nt * 16 + 8) * 8: xs + (2 * E * nt * 16 + 8 + 16 + E) * 8].view(torch.int64).cpu().numpy()
+    prof = ws[xs + (4 * 2 * nt * 16 + 8) * 8: xs + (2 * E * nt * 16 + 8 + 16 + E) * 8].view(torch.int64).cpu().numpy()
     # the backward's VJP phases (prof[10..15], accumulated over its E VJPs on top of the forward's)
     b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     b0.record(); ops.odetrain_backward(torch.ones_like(y), x, w, dyn, cfg, ws); b1.record(); torch.cuda.synchronize()
-    pb = ws[xs + (2 * E * nt * 16 + 8) * 8: xs + (2 * E * nt * 16 + 8 + 16) * 8].view(torch.int64).cpu().numpy()
+    pb = ws[xs + (4 * 2 * nt * 16 + 8) * 8: xs + (2 * E * nt * 16 + 8 + 16) * 8].view(torch.int64).cpu().numpy()
     vj = (pb[10:16] - prof[10:16]) / E * 0.01
     print(f"  backward total {b0.elapsed_time(b1)*1e3:.0f} us, per VJP (us): row math {vj[0]:.2f} g_a2 {vj[1]:.2f} "
           f"g_a1 {vj[2]:.2f} g_h partial {vj[3]:.2f} barrier {vj[4]:.2f} sum {vj[5]:.2f}", flush=True)
