@@ -379,7 +379,6 @@ struct PlainSrc {
   int64_t stride;
   int n;
   __device__ void bind(int m, float*) { in += (int64_t)m * stride; }
-  __device__ void extra(int64_t, float) const {}
   __device__ float at(int r, int c) const { return in[(int64_t)r * n + c]; }
   __device__ f4v row4(int r, int c4) const { return *reinterpret_cast<const f4v*>(in + (int64_t)r * n + c4); }
 };
@@ -391,11 +390,9 @@ struct DenseSrc {
   float* nrm_out;        // [b]
   int cout, cin, k, wide;
   float s;
-  float* rm;             // [b][k][k] or null: -2 s inv (the lazy wide map's second head block)
   __device__ void bind(int m, float* slot) {
     W += (int64_t)m * cout * cin;
     if (G) G += (int64_t)m * k * k;
-    if (rm) rm += (int64_t)m * k * k;
     if (threadIdx.x < 64) {               // dense.hip dense_norm: the same fixed order
       const float* pb = part + m * 256 + 4 * threadIdx.x;
       float v = (pb[0] + pb[1]) + (pb[2] + pb[3]);
@@ -416,9 +413,6 @@ struct DenseSrc {
     return v;
   }
   __device__ f4v row4(int r, int c4) const { return f4v{at(r, c4), at(r, c4 + 1), at(r, c4 + 2), at(r, c4 + 3)}; }
-  __device__ void extra(int64_t idx, float v) const {
-    if (rm) rm[idx] = -2.0f * s * v;
-  }
 };
 // a 64 x 64 block of a row-major matrix (row stride ld) -> LDS, row-major or transposed
 template <class Src>
@@ -679,7 +673,6 @@ __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out
           if (gi == gj) qv -= 1.0f;
           qout[(int64_t)gi * n + gj] = qv;
         }
-        src.extra((int64_t)gi * n + gj, v);
       }
   }
 }
@@ -852,8 +845,7 @@ extern "C" FIODE_API int fiode_dense_cayley_inverse(void* stream, const fiode_de
     return FIODE_EINVAL;
   const size_t per = fiode_block_inverse_workspace_bytes(k);
   if (workspace_bytes < (size_t)cfg->batch * per) return FIODE_EWORKSPACE;
-  DenseSrc src{W, R > k ? G : nullptr, alpha, part, nrm_out, cfg->cout, cfg->cin, k, cfg->cin > cfg->cout ? 1 : 0, 0.f,
-               nullptr};
+  DenseSrc src{W, R > k ? G : nullptr, alpha, part, nrm_out, cfg->cout, cfg->cin, k, cfg->cin > cfg->cout ? 1 : 0, 0.f};
   hipStream_t st = (hipStream_t)stream;
   float* ws = (float*)workspace;
   const int64_t wstride = (int64_t)(per / sizeof(float));
@@ -866,39 +858,6 @@ extern "C" FIODE_API int fiode_dense_cayley_inverse(void* stream, const fiode_de
     case 6: rc = launch_pinv_src<6>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
     case 7: rc = launch_pinv_src<7>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
     default: rc = launch_pinv_src<8>(st, cfg->batch, src, inv_out, q_out, ws, wstride, nullptr, false); break;
-  }
-  if (rc) return rc;
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? FIODE_OK : FIODE_EHIP + (int)e;
-}
-
-// fiode_dense_cayley_inverse_lazy: the same inverse for a tall / wide map, with the map's Q left
-// unformed: its k x k blocks Qt = 2 inv - I -> qt_out and Rm = -2 s inv -> rm_out (in the inverse's
-// own layout), from which the consumer forms x Q^T = x_top Qt + (x_bot V'^T-side) Rm itself (the
-// KWLarge head's first layer, cayley.py _LinearHeadFn) -- no P = V' inv GEMM, no finish launch.
-extern "C" FIODE_API int fiode_dense_cayley_inverse_lazy(void* stream, const fiode_dense_config* cfg, const float* W,
-                                                         const float* alpha, const float* part, const float* G,
-                                                         float* nrm_out, float* inv_out, float* qt_out, float* rm_out,
-                                                         void* workspace, size_t workspace_bytes) {
-  if (!cfg || cfg->batch < 1 || cfg->batch > 65535 || cfg->cout < 1 || cfg->cin < 1) return FIODE_EINVAL;
-  const int k = cfg->cout < cfg->cin ? cfg->cout : cfg->cin, R = cfg->cout < cfg->cin ? cfg->cin : cfg->cout;
-  if (!pinv_shape(k) || R == k) return FIODE_ESHAPE;
-  if (!W || !alpha || !part || !nrm_out || !inv_out || !workspace || !G || !qt_out || !rm_out) return FIODE_EINVAL;
-  const size_t per = fiode_block_inverse_workspace_bytes(k);
-  if (workspace_bytes < (size_t)cfg->batch * per) return FIODE_EWORKSPACE;
-  DenseSrc src{W, G, alpha, part, nrm_out, cfg->cout, cfg->cin, k, cfg->cin > cfg->cout ? 1 : 0, 0.f, rm_out};
-  hipStream_t st = (hipStream_t)stream;
-  float* ws = (float*)workspace;
-  const int64_t wstride = (int64_t)(per / sizeof(float));
-  int rc = FIODE_OK;
-  switch (k / PB) {
-    case 2: rc = launch_pinv_src<2>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    case 3: rc = launch_pinv_src<3>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    case 4: rc = launch_pinv_src<4>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    case 5: rc = launch_pinv_src<5>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    case 6: rc = launch_pinv_src<6>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    case 7: rc = launch_pinv_src<7>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
-    default: rc = launch_pinv_src<8>(st, cfg->batch, src, inv_out, qt_out, ws, wstride, nullptr, false); break;
   }
   if (rc) return rc;
   const hipError_t e = hipGetLastError();

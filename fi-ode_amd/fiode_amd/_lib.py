@@ -189,8 +189,6 @@ def _load():
         "fiode_dense_inverse_flag_bytes": (ct.c_size_t, [ct.c_int32]),
         "fiode_dense_cayley_inverse": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                   _vp, ct.c_size_t]),
-        "fiode_dense_cayley_inverse_lazy": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp, _vp,
-                                                       _vp, _vp, _vp, ct.c_size_t]),
         "fiode_dense_cayley_finish": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_ginv": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp, _vp, _vp]),
         "fiode_dense_cayley_h": (ct.c_int, [_vp, ct.POINTER(DenseConfig), _vp, _vp, _vp]),

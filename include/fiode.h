@@ -396,14 +396,6 @@ FIODE_API size_t fiode_dense_inverse_flag_bytes(int32_t k);
 FIODE_API int fiode_dense_cayley_inverse(void* stream, const fiode_dense_config* cfg, const float* W,
                                          const float* alpha, const float* part, const float* G, float* nrm_out,
                                          float* inv_out, float* q_out, void* workspace, size_t workspace_bytes);
-/* The same inverse of a tall / wide map with its Q left unformed: the k x k blocks Qt = 2 inv - I ->
- * qt_out and Rm = -2 s inv -> rm_out, from which a consumer of y = x Q^T forms it as
- * x_top Qt + (x_bot W[:, k:]^T) Rm (wide; the KWLarge head's first CayleyLinear) -- the map's
- * P = V' inv GEMM and finish launch drop out of the forward. */
-FIODE_API int fiode_dense_cayley_inverse_lazy(void* stream, const fiode_dense_config* cfg, const float* W,
-                                              const float* alpha, const float* part, const float* G,
-                                              float* nrm_out, float* inv_out, float* qt_out, float* rm_out,
-                                              void* workspace, size_t workspace_bytes);
 FIODE_API int fiode_dense_cayley_finish(void* stream, const fiode_dense_config* cfg, const float* alpha,
                                         const float* nrm, const float* inv, const float* P, float* Q);
 FIODE_API int fiode_dense_cayley_ginv(void* stream, const fiode_dense_config* cfg, const float* alpha,
