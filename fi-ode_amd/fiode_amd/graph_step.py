@@ -43,6 +43,8 @@ from .streams import distinct, new_stream
 
 # priority of the stream the step is captured on (its nodes' hardware queue; tools/ab_step.py cap_hi)
 CAPTURE_PRIORITY = 0
+# zeroed GEMM workspace slots reserved per capture (streams made in it that run split-K GEMMs)
+CAPTURE_WS_SLOTS = 24
 
 
 
@@ -276,6 +278,10 @@ class GraphTrainStep:
             raise RuntimeError("GraphTrainStep: two roles of the captured step share one HIP stream "
                                "(use fiode_amd.streams.new_stream for side streams, not the torch pool)")
         self.one_graph = self.single or self.comm == "graph"
+        # zeroed split-K counter words for the GEMMs of streams this capture makes (ops._Workspace:
+        # taken from an arena zeroed here, not filled by the replay on the step's chain)
+        from . import ops
+        ops._Workspace.reserve(self.static_x.device, CAPTURE_WS_SLOTS)
         # capture_error_mode "thread_local": the process group's watchdog thread polls its events
         # during our capture; in the default "global" mode such a call from ANOTHER thread aborts it
         # ("operation not permitted when stream is capturing" -> the watchdog terminates the process)

@@ -57,20 +57,56 @@ def _need(t: torch.Tensor, name: str, shape, dtype, dev) -> torch.Tensor:
     return t.contiguous()
 
 
+# tools/ab_step.py `ws_fill`: zeroed workspaces made inside a capture by a captured fill (before r06)
+WS_FILL_IN_CAPTURE = False
+
+
 class _Workspace:
     _cache: Dict[tuple, torch.Tensor] = {}
+    _arena: Dict[int, list] = {}          # device -> [buffer, slot bytes, next slot]
+    _zero_max: Dict[int, int] = {}        # device -> largest zeroed workspace asked for so far
+    fills_in_capture = 0                  # zeroed workspaces a capture had to fill itself
+    _retired: list = []                   # buffers a larger one replaced (a captured graph may hold them)
 
     @classmethod
     def get(cls, dev: torch.device, nbytes: int, tag: str, zero: bool = False) -> torch.Tensor:
         """A cached device buffer of at least ``nbytes`` per (device, tag); ``zero``: a new buffer
-        starts zeroed (for kernels whose flag words must be zero on first use)."""
+        starts zeroed (for kernels whose flag words must be zero on first use and are left zero by
+        every call).
+
+        A zeroed buffer first asked for inside a hipGraph capture is a slot of the arena that
+        ``reserve`` zeroed before the capture: memory the capture's own pool would hand out can be
+        an earlier temporary of the same replay (written before this call on every replay), so a
+        buffer from it would need a captured fill on the step's chain.  Without a free slot large
+        enough, the capture fills (``fills_in_capture`` counts it)."""
         key = (dev.index, tag)
         buf = cls._cache.get(key)
+        if zero:
+            cls._zero_max[dev.index] = max(cls._zero_max.get(dev.index, 0), int(nbytes))
         if buf is None or buf.numel() < nbytes:
-            alloc = torch.zeros if zero else torch.empty
-            buf = alloc(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            if buf is not None:
+                # never freed: a graph captured with it replays into its address
+                cls._retired.append(buf)
+            n = max(int(nbytes), 256)
+            ar = cls._arena.get(dev.index)
+            if (zero and not WS_FILL_IN_CAPTURE and ar is not None and ar[1] >= n and
+                    (ar[2] + 1) * ar[1] <= ar[0].numel() and torch.cuda.is_current_stream_capturing()):
+                buf = ar[0][ar[2] * ar[1]:(ar[2] + 1) * ar[1]]
+                ar[2] += 1
+            else:
+                if zero and torch.cuda.is_current_stream_capturing():
+                    cls.fills_in_capture += 1
+                buf = (torch.zeros if zero else torch.empty)(n, dtype=torch.uint8, device=dev)
             cls._cache[key] = buf
         return buf
+
+    @classmethod
+    def reserve(cls, dev: torch.device, slots: int) -> None:
+        """Before a capture (outside it): a zeroed arena of ``slots`` slots, each as large as the
+        largest zeroed workspace asked for so far (the eager warm-up's), for the streams the
+        capture makes.  Slots handed out earlier stay with their streams (kernels leave them zero)."""
+        nb = (max(cls._zero_max.get(dev.index, 0), 256) + 255) // 256 * 256
+        cls._arena[dev.index] = [torch.zeros(slots * nb, dtype=torch.uint8, device=dev), nb, 0]
 
 
 def _weights_c(w: Dict[str, torch.Tensor], dev) -> tuple:
@@ -735,15 +771,6 @@ def mm_pair(A0: torch.Tensor, B0: torch.Tensor, A1: torch.Tensor, B1: torch.Tens
                                 ct.byref(d1), A1.data_ptr(), B1.data_ptr(), None, C1.data_ptr(), _ptr(ws),
                                 ws.numel() if ws is not None else 0), "fiode_gemm_pair")
     return C0, C1
-    d = L.GemmDesc(batch, M, N, K, la[0], lb[0], la[1], lb[1], ldc,
-                   A.stride(0) if A.dim() == 3 else 0, B.stride(0) if B.dim() == 3 else 0, M * N,
-                   float(alpha), float(beta), int(split_k), int(max_workgroups))
-    lib = L.lib()
-    nb = lib.fiode_gemm_workspace_bytes(ct.byref(d))
-    ws = _gemm_ws(dev, nb) if nb else None
-    L.check(lib.fiode_gemm(_stream(dev), ct.byref(d), A.data_ptr(), B.data_ptr(), _ptr(bias), out.data_ptr(),
-                           _ptr(ws), ws.numel() if ws is not None else 0), "fiode_gemm")
-    return out
 
 
 def spectral_config(weight_shape, n: int) -> L.SpectralConfig:

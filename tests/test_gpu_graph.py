@@ -268,9 +268,13 @@ def test_placement_trials_use_distinct_dedicated_streams():
     y = torch.randint(0, 10, (32,), generator=g).to(dev)
     mod = bench.build_module(dev, seed=0, train_ode=True)
     opt = mod.configure_optimizers(capturable=True)[0][0]
+    from fiode_amd import ops
+    fills = ops._Workspace.fills_in_capture
     gs = GraphTrainStep(mod, opt, x, y, warmup=2, placement_trials=4)
     roles = [s for s in gs.role_streams() if s is not None]
     assert len(roles) >= 8 and streams.distinct(roles)
+    # every zeroed GEMM workspace of the 5 captures came from a reserved arena (no captured fill)
+    assert ops._Workspace.fills_in_capture == fills
     gs.step()
     torch.cuda.synchronize()
     mod._wtap_stream = CY._head_stream(dev)          # two roles on one stream: refused before capturing

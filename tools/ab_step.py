@@ -261,6 +261,12 @@ def dyn_wgrad_main(m):
     RESTORE.append(lambda: setattr(LY, "DYN_WGRAD_SIDE", True))
 
 
+def ws_fill(m):
+    from fiode_amd import ops as OPS
+    OPS.WS_FILL_IN_CAPTURE = True     # GEMM workspaces made in the capture zeroed by a captured fill
+    RESTORE.append(lambda: setattr(OPS, "WS_FILL_IN_CAPTURE", False))
+
+
 def no_pair(m):
     from fiode_amd import ops as OPS
     OPS.MM_PAIR = False           # the dense maps' backward A and P2 as two launches (before r06)
@@ -270,7 +276,7 @@ def no_pair(m):
 # variants of paths removed from the product after their A/B (the conv weight gradients on the map
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
-ALL = {"default": default, "no_pair": no_pair, "lib_gemm": lib_gemm, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
