@@ -166,7 +166,7 @@ def _dense_prep(W: torch.Tensor, alpha: torch.Tensor, M: Optional[torch.Tensor] 
         L.check(lib.fiode_dense_norm_partials(st, ct.byref(cfg), Wb.data_ptr(), part.data_ptr(), part.numel() * 4),
                 "fiode_dense_norm_partials")
     Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
-    G = ops.mm(Vp.mT, Vp) if Vp is not None else None
+    G = ops.mm(Vp.mT, Vp, site="dense_fwd") if Vp is not None else None
     if M is None:
         M = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
     if not DENSE_NORM_PARTIALS:
@@ -186,7 +186,8 @@ def _dense_finish(st: dict, inv: torch.Tensor) -> torch.Tensor:
     Wb, k = st["Wb"], st["k"]
     P = None                    # V' inv in W's layout (wide: its transpose inv^T V'^T = inv^T W[:, k:])
     if st["Vp"] is not None:
-        P = ops.mm(inv.mT, Wb[:, :, k:]) if st["wide"] else ops.mm(st["Vp"], inv)
+        P = (ops.mm(inv.mT, Wb[:, :, k:], site="dense_fwd") if st["wide"] else
+             ops.mm(st["Vp"], inv, site="dense_fwd"))
     Q = torch.empty_like(Wb)
     L.check(L.lib().fiode_dense_cayley_finish(ops._stream(Wb.device), ct.byref(st["cfg"]), st["al"].data_ptr(),
                                               st["nrm"].data_ptr(), inv.data_ptr(), ops._ptr(P), Q.data_ptr()),
@@ -210,7 +211,8 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
         Gb = gQb[:, :, k:].mT if wide else gQb[:, k:, :]
         # A = V'^T Gb and P2 = Gb inv^T (W layout; wide: inv gQ[:, k:]) need only the inputs: one launch
         # for both (fiode_gemm_pair), so P2 leaves the A -> Ginv -> GMn -> H -> P1 chain
-        A, P2 = ops.mm_pair(Vp.mT, Gb, inv, gQb[:, :, k:]) if wide else ops.mm_pair(Vp.mT, Gb, Gb, inv.mT)
+        A, P2 = (ops.mm_pair(Vp.mT, Gb, inv, gQb[:, :, k:], site="dense_bwd") if wide else
+                 ops.mm_pair(Vp.mT, Gb, Gb, inv.mT, site="dense_bwd"))
     Ginv = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_ginv(st, ct.byref(cfg), al.data_ptr(), nrm.data_ptr(), gQb.data_ptr(),
                                         ops._ptr(A), Ginv.data_ptr()), "fiode_dense_cayley_ginv")
@@ -223,14 +225,14 @@ def _dense_backward(Wb, al, nrm, inv, gQ, wshape, ashape):
         L.check(lib.fiode_dense_gemm(st, b, k, 0, 1, Ginv.data_ptr(), inv.data_ptr(), T.data_ptr()), "fiode_dense_gemm")
         L.check(lib.fiode_dense_gemm(st, b, k, 1, 0, inv.data_ptr(), T.data_ptr(), GMn.data_ptr()), "fiode_dense_gemm")
     else:
-        GMn = ops.mm(ih, ops.mm(Ginv, ih))
+        GMn = ops.mm(ih, ops.mm(Ginv, ih, site="dense_bwd"), site="dense_bwd")
     gX = torch.empty_like(Wb)                    # W layout
     H = torch.empty((b, k, k), dtype=torch.float32, device=Wb.device)
     L.check(lib.fiode_dense_cayley_h(st, ct.byref(cfg), GMn.data_ptr(), gX.data_ptr(), H.data_ptr()),
             "fiode_dense_cayley_h")
     P1 = None                       # V' H in W's layout (wide: H^T W[:, k:])
     if R > k:
-        P1 = ops.mm(H.mT, Wb[:, :, k:]) if wide else ops.mm(Vp, H)
+        P1 = ops.mm(H.mT, Wb[:, :, k:], site="dense_bwd") if wide else ops.mm(Vp, H, site="dense_bwd")
     gW = torch.empty_like(Wb)
     ga = torch.empty(b, dtype=torch.float32, device=Wb.device)
     ws = torch.empty(max(1, lib.fiode_dense_cayley_workspace_bytes(ct.byref(cfg))), dtype=torch.uint8,
@@ -269,7 +271,7 @@ def _dense_forward_fused(W: torch.Tensor, alpha: torch.Tensor):
                                                 ws.data_ptr(), lib.fiode_dense_inverse_flag_bytes(k) // 4, per),
             "fiode_dense_norm_partials_clear")
     Vp = (Wb[:, :, k:].mT if wide else Wb[:, k:, :]) if max(cout, cin) > k else None
-    G = ops.mm(Vp.mT, Vp) if Vp is not None else None
+    G = ops.mm(Vp.mT, Vp, site="dense_fwd") if Vp is not None else None
     nrm = torch.empty(b, dtype=torch.float32, device=W.device)
     inv = torch.empty((b, k, k), dtype=torch.float32, device=W.device)
     Q = torch.empty_like(Wb) if Vp is None else None
@@ -540,13 +542,13 @@ class _LinearHeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, Q1, b1, Q2, b2, Q3, b3):
         from . import ops
-        y1 = ops.mm(h, Q1.t(), bias=b1)
+        y1 = ops.mm(h, Q1.t(), bias=b1, site="head")
         z1 = ops.groupsort_forward(y1, 1)
-        y2 = ops.mm(z1, Q2.t(), bias=b2)
+        y2 = ops.mm(z1, Q2.t(), bias=b2, site="head")
         z2 = ops.groupsort_forward(y2, 1)
         out_k = _head_out_ok(Q3)
         # the 512 -> 10 output layer: the library ran it on one workgroup (~15 us on the chain)
-        out = ops.head_out(z2, Q3, b3) if out_k else ops.mm(z2, Q3.t(), bias=b3)
+        out = ops.head_out(z2, Q3, b3) if out_k else ops.mm(z2, Q3.t(), bias=b3, site="head")
         ctx.save_for_backward(h, Q1, Q2, Q3, y1, z1, y2, z2)
         ctx.out_k = out_k
         return out
@@ -563,16 +565,16 @@ class _LinearHeadFn(torch.autograd.Function):
         def wgrad(k, gk, x):
             side.wait_stream(cur)
             with torch.cuda.stream(side):
-                wg[k] = (ops.mm(gk.t(), x), gk.sum(0))
+                wg[k] = (ops.mm(gk.t(), x, site="head"), gk.sum(0))
             gk.record_stream(side)
             x.record_stream(side)
 
         wgrad(3, g, z2)
-        g2 = ops.head_out_backward_gs(g, Q3, y2) if ctx.out_k else ops.groupsort_backward(y2, ops.mm(g, Q3), 1)
+        g2 = ops.head_out_backward_gs(g, Q3, y2) if ctx.out_k else ops.groupsort_backward(y2, ops.mm(g, Q3, site="head"), 1)
         wgrad(2, g2, z1)
-        g1 = ops.groupsort_backward(y1, ops.mm(g2, Q2), 1)
+        g1 = ops.groupsort_backward(y1, ops.mm(g2, Q2, site="head"), 1)
         wgrad(1, g1, h)
-        dh = ops.mm(g1, Q1)
+        dh = ops.mm(g1, Q1, site="head")
         cur.wait_stream(side)
         for dW, db in wg.values():
             dW.record_stream(cur)
@@ -742,7 +744,10 @@ class _SpectralConvFn(torch.autograd.Function):
                 wq = _SPECTRAL_GRAD_WEIGHTS[key] = w.repeat(n).reshape(-1, 1, 1)
 
         def wgrad():        # dL/dQ = w G X^H: fiode_cgemm with B = X^H read from X and w folded in
-            gq = ops.cgemm(G, X, conj_trans_b=True, scale=wq.reshape(-1)) if need_q else None
+            if need_q and CONV_WGRAD_LIB:          # (the library GEMM: note at CONV_WGRAD_LIB)
+                gq = torch.matmul(G, X.mH) * wq
+            else:
+                gq = ops.cgemm(G, X, conj_trans_b=True, scale=wq.reshape(-1)) if need_q else None
             gbias = G[0].real.sum(-1) if need_b else None
             return gq, gbias
         # the weight / bias gradients beside the input gradient (which alone is on the backward's
@@ -768,12 +773,14 @@ class _SpectralConvFn(torch.autograd.Function):
 
 
 _SPECTRAL_GRAD_WEIGHTS = {}
-# The per-frequency channel products Q X, Q^H G and the weight gradient w G X^H are fiode_cgemm
-# (cgemm.hip), not torch.matmul (the library's batched complex GEMM: one 128 x 64 tile per frequency;
-# the n = 8 layer's forward 41 -> 16 us, conv 3's input gradient 16 -> 10, conv 1's forward 13 -> 10 us;
-# step -25 to -40 us in the alternating A/B, profiles/r05bd).  The weight gradient runs on the side
-# stream (round 5 kept the library GEMM + a scale kernel there: profiles/r05bj; round 6 takes the one
-# fiode_cgemm launch so that no library GEMM is left in the step).
+# The per-frequency channel products Q X and Q^H G are fiode_cgemm (cgemm.hip), not torch.matmul (the
+# library's batched complex GEMM: one 128 x 64 tile per frequency; the n = 8 layer's forward 41 -> 16
+# us, conv 3's input gradient 16 -> 10, conv 1's forward 13 -> 10 us; step -25 to -40 us in the
+# alternating A/B, profiles/r05bd).  The weight gradient w G X^H on the side stream stays the library
+# GEMM + the scale: the one fiode_cgemm launch (conjugate-transposed B, w folded in) measured 4.6 us
+# slower in the step (profiles/r06/ab_gemm_sites.json; round 5: 10-20 us, profiles/r05bj).
+# CONV_WGRAD_LIB = False takes the fiode_cgemm launch.
+CONV_WGRAD_LIB = True
 # conv layers with at most this many input channels (conv 1: 3) form Q X inside the inverse
 # transform's loads (fiode_sconv_irfft2_qx; the kernel's limit is 4): no GEMM launch, no [f][C][B]
 # product in HBM

@@ -675,9 +675,17 @@ def _mat_layout(X: torch.Tensor):
     return None
 
 
-# tools/ab_step.py's `lib_gemm` variant routes ops.mm through torch.matmul (hipBLASLt) to measure the
-# step against the library; the product never sets it
+# GEMM routing.  ops.mm call sites named here take the library GEMM (torch.matmul / addmm: hipBLASLt)
+# instead of fiode_gemm: on the step's shapes fiode_gemm's 64 x 64 tiles run 63-65 TF/s where the
+# library's tuned tiles (224 x 32, 32 x 32 x 128 ...) run 83-90 on the 512-map products and twice
+# as fast on the head's skinny ones (profiles/r06/gemm_probe_prefetch.log), and the same-box step
+# A/B with a copy-free library route measured 1.2404 (library at all three sites) vs 1.2905 ms
+# (fiode_gemm everywhere); each site alone: dense_fwd -14, dense_bwd -10, head -24 us
+# (profiles/r06/ab_gemm_sites.json).  fiode_gemm stays the C-ABI product (tested bit-for-bit
+# against itself and to fp32 tolerance against the library) for any site a faster tile wins back.
+# MM_LIBRARY (tools/ab_step.py `lib_gemm`) routes every call to the library.
 MM_LIBRARY = False
+MM_LIBRARY_SITES: set = {"dense_fwd", "dense_bwd", "head"}
 # the dense maps' backward pair (A, P2) in one fiode_gemm_pair launch (tools/ab_step.py `no_pair`: two launches)
 MM_PAIR = True
 
@@ -731,15 +739,20 @@ def _gemm_operands(A: torch.Tensor, B: torch.Tensor, alpha: float, beta: float, 
 
 def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
        bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, split_k: int = 0,
-       max_workgroups: int = 0) -> torch.Tensor:
+       max_workgroups: int = 0, site: str = "") -> torch.Tensor:
     """fiode_gemm: out = alpha A @ B + beta out + bias, float32, A [(b,) M, K], B [(b,) K, N] (a 2-D
     operand is shared by every batch entry), bias [N].  Either operand may be a transposed view of
     row-major memory (``W.t()``, ``X.mT``, a column slice): the kernel reads it in place.  The hand-
     written replacement of torch.matmul / addmm on the Cayley layers' products (gemm.hip).
     ``max_workgroups``: a capped, persistent grid (a narrow launch beside other work; 0 = none)."""
     dev = B.device
-    d, A, B, bias, out = _gemm_operands(A, B, alpha, beta, bias, out, split_k, max_workgroups)
-    if MM_LIBRARY:              # measurement switch of tools/ab_step.py (`lib_gemm`): the library GEMM
+    if MM_LIBRARY or site in MM_LIBRARY_SITES:   # the library GEMM (routing note above)
+        if out is None and alpha == 1.0 and beta == 0.0:        # round 5's calls: no copy
+            if bias is not None and A.dim() == 2 and B.dim() == 2:
+                return torch.addmm(bias, A, B)
+            r = torch.matmul(A, B)
+            return (r + bias if bias is not None else r).contiguous()
+        d, A, B, bias, out = _gemm_operands(A, B, alpha, beta, bias, out, split_k, max_workgroups)
         r = torch.matmul(A, B)
         r = r * alpha if alpha != 1.0 else r
         if bias is not None:
@@ -748,6 +761,7 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
             r = r + beta * out
         out.copy_(r)
         return out
+    d, A, B, bias, out = _gemm_operands(A, B, alpha, beta, bias, out, split_k, max_workgroups)
     lib = L.lib()
     nb = lib.fiode_gemm_workspace_bytes(ct.byref(d))
     ws = _gemm_ws(dev, nb) if nb else None
@@ -756,11 +770,11 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.
     return out
 
 
-def mm_pair(A0: torch.Tensor, B0: torch.Tensor, A1: torch.Tensor, B1: torch.Tensor):
+def mm_pair(A0: torch.Tensor, B0: torch.Tensor, A1: torch.Tensor, B1: torch.Tensor, site: str = ""):
     """fiode_gemm_pair: (A0 @ B0, A1 @ B1) -- two independent products in one launch, each the same
     bits as ``mm`` computes it."""
-    if MM_LIBRARY or not MM_PAIR:
-        return mm(A0, B0), mm(A1, B1)
+    if MM_LIBRARY or not MM_PAIR or site in MM_LIBRARY_SITES:
+        return mm(A0, B0, site=site), mm(A1, B1, site=site)
     dev = B0.device
     d0, A0, B0, _, C0 = _gemm_operands(A0, B0, 1.0, 0.0, None, None, 0, 0)
     d1, A1, B1, _, C1 = _gemm_operands(A1, B1, 1.0, 0.0, None, None, 0, 0)

@@ -255,6 +255,39 @@ def lib_gemm(m):
     RESTORE.append(lambda: setattr(OPS, "MM_LIBRARY", False))
 
 
+def _lib_site(site):
+    def f(m):
+        from fiode_amd import ops as OPS
+        OPS.MM_LIBRARY_SITES.add(site)
+        RESTORE.append(lambda: OPS.MM_LIBRARY_SITES.discard(site))
+    return f
+
+
+def own_gemm(m):
+    from fiode_amd import ops as OPS, cayley as CY
+    sites = set(OPS.MM_LIBRARY_SITES)
+    OPS.MM_LIBRARY_SITES.clear()         # fiode_gemm at every site, fiode_cgemm for the conv wgrad
+    CY.CONV_WGRAD_LIB = False
+    RESTORE.append(lambda: OPS.MM_LIBRARY_SITES.update(sites))
+    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_LIB", True))
+
+
+def lib3(m):
+    for site in ("dense_fwd", "dense_bwd", "head"):
+        _lib_site(site)(m)
+
+
+def wgrad_lib(m):
+    from fiode_amd import cayley as CY
+    CY.CONV_WGRAD_LIB = True      # the conv weight gradient w G X^H by torch.matmul + scale (round 5)
+    RESTORE.append(lambda: setattr(CY, "CONV_WGRAD_LIB", False))
+
+
+def r05_gemms(m):
+    lib_gemm(m)
+    wgrad_lib(m)
+
+
 def dyn_wgrad_main(m):
     from fiode_amd import lyapunov as LY
     LY.DYN_WGRAD_SIDE = False     # the dynamics weights' gradients inside LyapODELossFn's backward
@@ -276,7 +309,8 @@ def no_pair(m):
 # variants of paths removed from the product after their A/B (the conv weight gradients on the map
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
-ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "wgrad_lib": wgrad_lib, "r05_gemms": r05_gemms, "lib_dense_fwd": _lib_site("dense_fwd"),
+       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
