@@ -496,6 +496,17 @@ class CayleyLinear(nn.Linear):
         the layers before it); the next training forward joins it."""
         self._pre = _prefetch(stream, self.effective_weight)
 
+    def forward_weight_unjoined(self):
+        """(Q, done event or None): forward_weight, but a pending prefetched map is handed out
+        WITHOUT making the current stream wait for it -- the caller waits on the event right before
+        its first use of Q (the stream-order bookkeeping of _take is done here)."""
+        if self._pre is not None and self.training:
+            (Q, ev), self._pre = self._pre, None
+            Q.record_stream(torch.cuda.current_stream(Q.device))
+            self._Q = Q.detach()
+            return Q, ev
+        return self.forward_weight(), None
+
     def forward_weight(self) -> torch.Tensor:
         """The effective weight this forward uses (the prefetched map when one is pending)."""
         if self._pre is not None and self.training:
@@ -534,18 +545,26 @@ class _LinearHeadFn(torch.autograd.Function):
     gradient it does not need (the head's backward is on the step's critical path).  Here the
     weight / bias gradients (the same GEMM g^T x and column sum) of every layer run on a side
     stream forked as soon as that layer's output gradient exists, beside the input-gradient chain,
-    and join the step's stream once at the end.  Every product is fiode_gemm (gemm.hip; the bias
-    added in its epilogue), the output layer fiode_head_out / _backward_gs when it has <= 16 outputs
-    (KWLargeConcat's 10 classes; a wider out_dim, e.g. make_ortho_KWLarge_Concat's default 128,
-    takes fiode_gemm + the GroupSort kernel)."""
+    and join the step's stream once at the end.  The products go through ops.mm (the library GEMM
+    at this site: ops.MM_LIBRARY_SITES), the output layer fiode_head_out / _backward_gs when it has
+    <= 16 outputs (KWLargeConcat's 10 classes; a wider out_dim, e.g. make_ortho_KWLarge_Concat's
+    default 128, takes ops.mm + the GroupSort kernel)."""
 
     @staticmethod
-    def forward(ctx, h, Q1, b1, Q2, b2, Q3, b3):
+    def forward(ctx, h, Q1, b1, Q2, b2, Q3, b3, joins=None):
         from . import ops
+        # joins: the done events of Q2 / Q3 still being computed on their prefetch streams, waited
+        # for right before the layer that reads them (the first layer runs meanwhile)
+        j2, j3 = joins if joins is not None else (None, None)
+        cur = torch.cuda.current_stream(h.device)
         y1 = ops.mm(h, Q1.t(), bias=b1, site="head")
         z1 = ops.groupsort_forward(y1, 1)
+        if j2 is not None:
+            cur.wait_event(j2)
         y2 = ops.mm(z1, Q2.t(), bias=b2, site="head")
         z2 = ops.groupsort_forward(y2, 1)
+        if j3 is not None:
+            cur.wait_event(j3)
         out_k = _head_out_ok(Q3)
         # the 512 -> 10 output layer: the library ran it on one workgroup (~15 us on the chain)
         out = ops.head_out(z2, Q3, b3) if out_k else ops.mm(z2, Q3.t(), bias=b3, site="head")
@@ -579,7 +598,7 @@ class _LinearHeadFn(torch.autograd.Function):
         for dW, db in wg.values():
             dW.record_stream(cur)
             db.record_stream(cur)
-        return dh, wg[1][0], wg[1][1], wg[2][0], wg[2][1], wg[3][0], wg[3][1]
+        return dh, wg[1][0], wg[1][1], wg[2][0], wg[2][1], wg[3][0], wg[3][1], None
 
 
 # the head's output layer and its GroupSort input gradient by fiode_head_out / _backward_gs (<= 16
@@ -603,8 +622,17 @@ def linear_head(mods, h: torch.Tensor):
             h = m(h)
         return h
     l1, l2, l3 = mods[0::2]
-    return _LinearHeadFn.apply(h.contiguous(), l1.forward_weight(), l1.bias, l2.forward_weight(), l2.bias,
+    Q1 = l1.forward_weight()
+    if HEAD_LATE_JOIN:
+        (Q2, j2), (Q3, j3) = l2.forward_weight_unjoined(), l3.forward_weight_unjoined()
+        return _LinearHeadFn.apply(h.contiguous(), Q1, l1.bias, Q2, l2.bias, Q3, l3.bias, (j2, j3))
+    return _LinearHeadFn.apply(h.contiguous(), Q1, l1.bias, l2.forward_weight(), l2.bias,
                                l3.forward_weight(), l3.bias)
+
+
+# the head joins the 512 -> 512 and 512 -> 10 maps' prefetch right before the layer that reads them,
+# not before its first layer (tools/ab_step.py `head_join_early`)
+HEAD_LATE_JOIN = True
 
 
 
