@@ -34,6 +34,9 @@ class _KeepGraph(torch.cuda.CUDAGraph):
 GS.torch.cuda.CUDAGraph = _KeepGraph           # graph_step's captures keep their hipGraph_t
 dev = torch.device("cuda:0")
 mod = bench.build_module(dev, train_ode=True)
+if os.environ.get("FIODE_PROBE_LATE_AT") is not None:     # the map-prefetch split point (None: all first)
+    v = os.environ["FIODE_PROBE_LATE_AT"]
+    mod._prefetch_late_at = None if v == "none" else int(v)
 opt = mod.configure_optimizers(capturable=True)[0][0]
 g = torch.Generator(device="cpu").manual_seed(1234)
 x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
