@@ -478,8 +478,9 @@ __device__ __forceinline__ void mfma_settle(f4v (&acc)[2]) {
 template <int NB, class Src>
 __global__ void __launch_bounds__(PI_NT) k_pinv(Src src, float* __restrict__ out, float* __restrict__ qout,
                                                 float* ws_all, int64_t wstride, const int32_t* __restrict__ skip,
-                                                int acq, unsigned long long* prof, unsigned spin_limit) {
+                                                int acq, unsigned long long* prof, unsigned spin_limit, int prio) {
   if (skip && *skip) return;                  // (uniform)
+  fiode_wave_prio(prio);
   constexpr int n = NB * PB;
   __shared__ __attribute__((aligned(16))) float lds[4][PB][LDTS];
   __shared__ int dead;
@@ -696,7 +697,7 @@ int launch_pinv_src(hipStream_t st, int batch, Src src, float* out, float* qout,
     FIODE_HIP_CHECK(hipMemset2DAsync(ws, (size_t)wstride * sizeof(float), 0, PinvWs::flag_floats(NB) * sizeof(float),
                                      (size_t)batch, st));
   hipLaunchKernelGGL((k_pinv<NB, Src>), dim3(1 + NB * NB, batch), dim3(PI_NT), 0, st, src, out, qout, ws, wstride, skip,
-                     pinv_acquire_knob(), prof, g_pinv_spin_limit);
+                     pinv_acquire_knob(), prof, g_pinv_spin_limit, (int)((g_fiode_prio_mask >> 3) & 1));
   return FIODE_OK;
 }
 
@@ -802,6 +803,17 @@ extern "C" int fiode_block_inverse_batched(void* stream, int32_t batch, int32_t 
 extern "C" int fiode_block_inverse(void* stream, int32_t n, const float* in, float* out, void* workspace,
                                    size_t workspace_bytes) {
   return fiode_block_inverse_batched(stream, 1, n, in, out, workspace, workspace_bytes);
+}
+
+// Diagnostic (not in fiode.h): the wave-priority mask of common.h (g_fiode_prio_mask); returns the
+// previous mask.  Default: the rk4 train solve's two latency chains (k_ot_fwd4, k_ot_bwd4) raised over
+// the fan-out kernels sharing their CUs -- interleaved step A/B 1.2344 -> 1.2297 ms (mask 3; 1 alone
+// 1.2320; the small maps / k_pinv no gain: profiles/r06/ab_wave_prio.json).  tools/ab_step.py `prio_*`.
+unsigned g_fiode_prio_mask = 3;
+extern "C" FIODE_API unsigned fiode_debug_set_prio_mask(unsigned mask) {
+  const unsigned prev = g_fiode_prio_mask;
+  g_fiode_prio_mask = mask;
+  return prev;
 }
 
 // Diagnostic (not in fiode.h): the spin bound of k_pinv's polls (0 restores the default); returns the

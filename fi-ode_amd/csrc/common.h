@@ -7,6 +7,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Wave-priority mask (default 3; fiode_debug_set_prio_mask, not in fiode.h): bit 0 k_ot_fwd4, bit 1
+// k_ot_bwd4, bit 2 k_small_cayley_*, bit 3 k_pinv -- the kernel's waves raise their issue priority
+// (s_setprio) over co-resident waves of other kernels.  Read at launch, so a captured graph keeps it.
+extern unsigned g_fiode_prio_mask;
+__device__ __forceinline__ void fiode_wave_prio(bool on) {
+  if (on) __builtin_amdgcn_s_setprio(2);
+}
+
 #define FIODE_C 10
 #define FIODE_M 128
 #define FIODE_X 10

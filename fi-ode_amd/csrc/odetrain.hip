@@ -43,6 +43,7 @@ constexpr int OT_XRING = 4;
 constexpr int FIODE_OT_KW_PRE = 256;      // dopri5: evals whose keep words k_ot_masks draws ahead
 
 struct OTArgs {
+  int prio;                 // g_fiode_prio_mask at launch (common.h)
   int B, E, niters;
   int nslots;               // u64 words of xslots zeroed by k_ot_masks before the forward
   int kw_lazy;              // dopri5, Philox p = 0.5: the forward draws the keep words of evals >= kw_pre
@@ -421,6 +422,7 @@ __device__ void ot_eval4(const OTArgs& a, const T4W& w, OtShared4& sh, int e, in
 }
 
 __global__ __launch_bounds__(256) void k_ot_fwd4(OTArgs a) {
+  fiode_wave_prio(a.prio & 1);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   OtShared4& sh = *reinterpret_cast<OtShared4*>(smem);
   if (threadIdx.x == 0) {
@@ -912,6 +914,7 @@ __device__ void ot_vjp4(const OTArgs& a, const VjpW4& wv, OtBwdShared4& sh, int 
 
 template <bool SN>
 __global__ __launch_bounds__(256) void k_ot_bwd4(OTArgs a) {
+  fiode_wave_prio(a.prio & 2);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   OtBwdShared4& sh = *reinterpret_cast<OtBwdShared4*>(smem);
   const int lane = threadIdx.x & 63, j = lane & 3;
@@ -2071,6 +2074,7 @@ extern "C" int fiode_odetrain_forward(void* stream, const fiode_odetrain_config*
                                       const uint8_t* masks, const uint64_t* offset_dev, float* y_out, int32_t* stats,
                                       void* workspace, size_t workspace_bytes) {
   OTArgs a{};
+  a.prio = (int)g_fiode_prio_mask;
   int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
   if (!h0 || !y_out || !stats) return FIODE_EINVAL;
@@ -2139,6 +2143,7 @@ extern "C" int fiode_odetrain_backward_x(void* stream, const fiode_odetrain_conf
                                          float* gx, const float* gx_add, const float* gx_add_scale, float* dbg_gft,
                                          void* workspace, size_t workspace_bytes) {
   OTArgs a{};
+  a.prio = (int)g_fiode_prio_mask;
   int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
   if (!g_y || !gx || (gx_add && !gx_add_scale)) return FIODE_EINVAL;
@@ -2156,6 +2161,7 @@ extern "C" int fiode_odetrain_backward_weights(void* stream, const fiode_odetrai
                                                const float* x_feat, fiode_lyap_grads* grads, void* workspace,
                                                size_t workspace_bytes) {
   OTArgs a{};
+  a.prio = (int)g_fiode_prio_mask;
   int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
   if (!grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 || !grads->Q3 ||
@@ -2180,6 +2186,7 @@ extern "C" int fiode_odetrain_backward(void* stream, const fiode_odetrain_config
   // the per-image g_u it reduces): one launch fewer than _x + _weights (k_ot_gx), so the x-gradient
   // may differ from fiode_odetrain_backward_x's in the last bits (summation order of g_u)
   OTArgs a{};
+  a.prio = (int)g_fiode_prio_mask;
   int rc = fill_args(a, cfg, dyn, w, x_feat, workspace, workspace_bytes);
   if (rc) return rc;
   if (!g_y || !grads || !grads->Q1 || !grads->b1 || !grads->Qx || !grads->bx || !grads->Q2 || !grads->b2 ||

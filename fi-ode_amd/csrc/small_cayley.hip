@@ -26,6 +26,7 @@ constexpr int NT = 256;
 constexpr int KM = FIODE_SMALL_CAYLEY_MAX_K;      // 16
 
 struct SCArgs {
+  int prio;             // g_fiode_prio_mask bit 2 at launch
   int cout, cin, k, R, wide;
   const float* W;       // [b][cout][cin]
   const float* alpha;   // [b]
@@ -156,6 +157,7 @@ __device__ __forceinline__ void rows_gram(const float* X, const float* Y, int k,
 
 // LDS: X tall [R][k] | red [256] | m [16][17]
 __global__ void __launch_bounds__(NT) k_small_cayley_fwd(SCArgs a) {
+  fiode_wave_prio(a.prio);
   extern __shared__ float smem[];
   const int b = blockIdx.x, k = a.k, R = a.R, tid = threadIdx.x;
   float* X = smem;
@@ -200,6 +202,7 @@ __global__ void __launch_bounds__(NT) k_small_cayley_fwd(SCArgs a) {
 // LDS: X tall [R][k] | G tall [R][k] | gX tall [R][k] | W tall [R][k] | red [256] |
 //      inv, Ginv, P1, GM [16][17] each
 __global__ void __launch_bounds__(NT) k_small_cayley_bwd(SCArgs a) {
+  fiode_wave_prio(a.prio);
   extern __shared__ float smem[];
   const int b = blockIdx.x, k = a.k, R = a.R, tid = threadIdx.x;
   float* X = smem;
@@ -287,6 +290,7 @@ int check(int32_t batch, int32_t cout, int32_t cin) {
 
 SCArgs make_args(int32_t cout, int32_t cin, const float* W, const float* alpha) {
   SCArgs a{};
+  a.prio = (g_fiode_prio_mask >> 2) & 1;
   a.cout = cout; a.cin = cin;
   a.wide = cin > cout;
   a.k = a.wide ? cout : cin;

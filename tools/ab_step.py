@@ -274,6 +274,17 @@ def all_first_side(m):
     dense_bwd_side(m)             # ... and each dense map's backward on its own prefetch stream
 
 
+def _prio(mask):
+    def v(m):
+        import ctypes
+        from fiode_amd import _lib as L
+        f = L.lib().fiode_debug_set_prio_mask
+        f.argtypes, f.restype = [ctypes.c_uint], ctypes.c_uint
+        f(mask)                   # launch-time knob: this variant's capture keeps it
+        RESTORE.append(lambda: f(3))     # (the library's default mask)
+    return v
+
+
 def own_gemm(m):
     from fiode_amd import ops as OPS, cayley as CY
     sites = set(OPS.MM_LIBRARY_SITES)
@@ -321,7 +332,9 @@ def no_pair(m):
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
 ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "wgrad_lib": wgrad_lib, "r05_gemms": r05_gemms, "lib_dense_fwd": _lib_site("dense_fwd"),
-       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "all_first_side": all_first_side, "head_join_early": head_join_early, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
+       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "prio_otf": _prio(1), "prio_otb": _prio(2), "prio_small": _prio(4),
+       "prio_pinv": _prio(8), "prio_all": _prio(15), "prio_ot": _prio(3),
+       "prio_none": _prio(0), "all_first_side": all_first_side, "head_join_early": head_join_early, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
        "late2_first_ab": late2_first_ab, "late0": late0, "late1": late1, "late2": late2, "late3": late3, "late3b": late3,
        "default_b": default, "ms_213": ms_213, "ms_321": ms_321, "ms_3222": ms_3222, "ms_0": ms_0, "torch_norm": torch_norm, "late_scale": late_scale, "after_ode": after_ode, "no_ahead": no_ahead, "torch_adam": torch_adam,
