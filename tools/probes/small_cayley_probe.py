@@ -1,6 +1,7 @@
 """Isolated timing of the small Cayley map kernels (k_small_cayley_fwd / _bwd) at the step's shapes:
 the head's 512 -> 10 map (W [10][512], one workgroup) and the dynamics' three 128 x 10 maps (batch
-3).  Compare with their in-step durations (rocprofv3) to see how much of those is the kernel itself.
+3).  Run under rocprofv3 --kernel-trace for the kernels' own durations (the event times here include the
+host's launch and autograd overhead).
 (tools; not a test)
 
 usage: python tools/probes/small_cayley_probe.py
@@ -16,15 +17,8 @@ sys.path.insert(0, os.path.join(ROOT, "fi-ode_amd"))
 from fiode_amd.cayley import _SmallCayleyFn  # noqa: E402
 
 dev = torch.device("cuda:0")
-from fiode_amd import _lib as L  # noqa: E402
-import ctypes  # noqa: E402
-setnt = L.lib().fiode_debug_set_small_cayley_threads
-setnt.argtypes, setnt.restype = [ctypes.c_int], ctypes.c_int
 out = {}
-for nt, name, shape in [(nt, n, sh) for nt in (256, 512, 1024)
-                        for n, sh in (("head_512x10", (1, 10, 512)), ("dyn_3x128x10", (3, 128, 10)))]:
-    setnt(nt)
-    name = f"{name}_nt{nt}"
+for name, shape in (("head_512x10", (1, 10, 512)), ("dyn_3x128x10", (3, 128, 10))):
     g = torch.Generator(device="cpu").manual_seed(0)
     W = torch.randn(*shape, generator=g).to(dev).requires_grad_(True)
     a = torch.rand(shape[0], generator=g).add(0.5).to(dev).requires_grad_(True)
