@@ -8,6 +8,7 @@ orders / stream layouts, warm-started inverses) were measured here and removed f
 (DESIGN.md section 4 keeps their numbers); the variants left are the ones the product still has.
 """
 import json
+import os
 import pathlib
 import statistics
 import sys
@@ -25,7 +26,8 @@ torch.cuda.set_device(dev)
 
 
 def make(setup):
-    mod = bench.build_module(dev, train_ode=True)
+    # FIODE_AB_SOLVER=dopri5: the configs[2] step (train_ode dopri5, tol 1e-3) instead of rk4
+    mod = bench.build_module(dev, train_ode=True, solver=os.environ.get("FIODE_AB_SOLVER", "rk4"))
     setup(mod)
     opt = mod.configure_optimizers(capturable=True)[0][0]
     if getattr(mod, "_torch_adam", False):
@@ -35,7 +37,6 @@ def make(setup):
     g = torch.Generator(device="cpu").manual_seed(1234)
     x = torch.rand(128, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (128,), generator=g).to(dev)
-    import os
     return GraphTrainStep(mod, opt, x, y, maps_ahead=not getattr(mod, "_no_ahead", False),
                           placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "1")))
 
