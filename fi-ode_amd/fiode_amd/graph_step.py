@@ -37,6 +37,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 
 from .streams import distinct, new_stream
@@ -70,7 +72,7 @@ class GraphTrainStep:
     def __init__(self, module, optimizer, x: torch.Tensor, y: torch.Tensor, *, reducer=None, world: int = 1,
                  warmup: int = 3, act: str = "relu", check_every: int = 200, maps_ahead: bool = True,
                  comm: Optional[str] = None, bucket_bytes: int = 4 << 20, force_comm: bool = False,
-                 guard: bool = True, placement_trials: int = 1):
+                 guard: bool = True, placement_trials: int = 1, warm_capture: bool = True):
         _check_runtime_queues()
         dev = x.device
         if dev.type != "cuda":
@@ -138,20 +140,35 @@ class GraphTrainStep:
         if maps_ahead:
             self._maps_ahead_on()
         # every capture (the first one included) on fresh dedicated streams made in the same order, so
-        # the placement trials compare like with like
-        self._fresh_streams()
+        # the placement trials compare like with like.  warm_capture: the first capture in a process
+        # replays ~10 % slower than any later capture of the same step (same kernels, same launch
+        # shapes -- profiles/r06/warm_capture.json: placement trials 1.349 / 1.226 / 1.236 / 1.228 ms
+        # without, 1.243 / 1.241 / 1.244 / 1.242 with one discarded capture ahead), so one capture is
+        # made and dropped first (no kernel runs in a capture: parameters, optimizer state and
+        # counters are untouched; every rank does the same, so captured collectives stay paired).
         self.comm_fallback = None
-        try:
-            self._capture()
-        except Exception as exc:                   # noqa: BLE001 - rethrown unless it is the comm capture
-            if self.comm != "graph":
-                raise
-            # the collectives could not be captured by this runtime: eager bucket all-reduces
-            # between two graphs instead (the reason is kept in comm_fallback)
-            if self.reducer is not None:
-                self.reducer._armed = None
-            self.comm, self.comm_fallback = "eager", repr(exc)
-            self._capture()
+        for keep in ([False, True] if warm_capture else [True]):
+            self._fresh_streams()
+            try:
+                self._capture()
+            except Exception as exc:               # noqa: BLE001 - rethrown unless it is the comm capture
+                if self.comm != "graph":
+                    raise
+                # the collectives could not be captured by this runtime: eager bucket all-reduces
+                # between two graphs instead (the reason is kept in comm_fallback)
+                if self.reducer is not None:
+                    self.reducer._armed = None
+                self.comm, self.comm_fallback = "eager", repr(exc)
+                self._capture()
+            if not keep:
+                # The dropped capture's autograd graph stays referenced (self.loss), so the
+                # parameters' AccumulateGrad nodes made in it -- bound to its capture stream -- serve
+                # the kept captures too; that binding is what makes them replay faster: freeing the
+                # graph first brings the slow first-capture time back (1.348 vs 1.239 ms,
+                # profiles/r06/warm_capture.json).  torch warns about the stream mismatch it causes
+                # (an extra event join per parameter inside the graph): silenced, it is deliberate.
+                self.g_fb = self.g_opt = None
+                torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
         self.placement_ms = None
         if placement_trials > 1 and self.comm != "eager":
             self._select_placement(int(placement_trials))

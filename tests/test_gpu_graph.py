@@ -23,7 +23,9 @@ def test_graph_replay_matches_eager_step(train_ode):
     x = torch.rand(32, 3, 32, 32, generator=g).to(dev)
     y = torch.randint(0, 10, (32,), generator=g).to(dev)
     opt = mod.configure_optimizers(capturable=True)[0][0]
-    gs = GraphTrainStep(mod, opt, x, y, warmup=2)
+    # one capture, so that the AccumulateGrad-stream check above holds (the default warm capture
+    # binds the parameters' accumulators to its own stream on purpose: graph_step.py)
+    gs = GraphTrainStep(mod, opt, x, y, warmup=2, warm_capture=False)
     twin = bench.build_module(dev, seed=1, train_ode=train_ode)          # same parameters / counter as before the replay
     twin.load_state_dict(mod.state_dict())
     twin.rng_counter = mod.rng_counter.clone()
