@@ -289,6 +289,7 @@ def main():
             gstep = GraphTrainStep(mod, opt, x, y, reducer=reducer, world=world, comm=os.environ.get("FIODE_COMM"),
                                    placement_trials=int(os.environ.get("FIODE_PLACEMENT_TRIALS", "4")))
             last["placement_ms"] = gstep.placement_ms
+            last["recaptures"] = getattr(gstep, "placement_recaptures", 0)
             last["comm"] = gstep.comm if world > 1 else None
 
             def step():
@@ -330,6 +331,7 @@ def main():
         health["comm"] = last.get("comm")
         if last.get("placement_ms") is not None:
             health["placement_ms"] = last["placement_ms"]     # per trial capture; the fastest is kept
+            health["placement_recaptures"] = last.get("recaptures", 0)
         return float(dt.item()), mod, x, y, health
 
     def certify_companion(n_img: int = 2):
