@@ -287,17 +287,6 @@ def _prio(mask):
     return v
 
 
-def _sc_threads(nt):
-    def v(m):
-        import ctypes
-        from fiode_amd import _lib as L
-        f = L.lib().fiode_debug_set_small_cayley_threads
-        f.argtypes, f.restype = [ctypes.c_int], ctypes.c_int
-        prev = f(nt)              # launch-time knob: this variant's capture keeps it
-        RESTORE.append(lambda: f(prev))
-    return v
-
-
 def no_warm(m):
     m._no_warm = True
 
@@ -349,7 +338,7 @@ def no_pair(m):
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
 ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "wgrad_lib": wgrad_lib, "r05_gemms": r05_gemms, "lib_dense_fwd": _lib_site("dense_fwd"),
-       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "no_warm": no_warm, "sc256": _sc_threads(256), "sc512": _sc_threads(512), "sc1024": _sc_threads(1024), "prio_otf": _prio(1), "prio_otb": _prio(2), "prio_small": _prio(4),
+       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "no_warm": no_warm, "prio_otf": _prio(1), "prio_otb": _prio(2), "prio_small": _prio(4),
        "prio_pinv": _prio(8), "prio_all": _prio(15), "prio_ot": _prio(3),
        "prio_none": _prio(0), "all_first_side": all_first_side, "head_join_early": head_join_early, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
