@@ -36,7 +36,7 @@ def short(n):
 def main(dot, trace):
     txt = open(dot).read()
     nodes = {}
-    for m in re.finditer(r'"graph_0_node_(\d+)"\[style="\w+"shape="record"label="\{\n(\w+)\n(.*?)\}"\];', txt, re.S):
+    for m in re.finditer(r'"graph_\d+_node_(\d+)"\[style="\w+"shape="record"label="\{\n(\w+)\n(.*?)\}"\];', txt, re.S):
         nid, kind, body = int(m.group(1)), m.group(2), m.group(3)
         name, grid, block = None, None, None
         k = re.search(r"\{ID \| \d+ \| (.*?)\\<\\<\\<\((\d+),(\d+),(\d+)\),\((\d+),(\d+),(\d+)\)", body)
@@ -45,7 +45,7 @@ def main(dot, trace):
             grid = tuple(int(k.group(i)) for i in (2, 3, 4))
             block = tuple(int(k.group(i)) for i in (5, 6, 7))
         nodes[nid] = {"kind": kind, "name": name, "grid": grid, "block": block}
-    edges = [(int(a), int(b)) for a, b in re.findall(r'"graph_0_node_(\d+)" -> "graph_0_node_(\d+)"', txt)]
+    edges = [(int(a), int(b)) for a, b in re.findall(r'"graph_\d+_node_(\d+)" -> "graph_\d+_node_(\d+)"', txt)]
     kn = [i for i in sorted(nodes) if nodes[i]["name"]]
     dem = demangle([nodes[i]["name"] for i in kn])
     for i, d in zip(kn, dem):

@@ -8,11 +8,11 @@ import re, csv
 dot, trace = sys.argv[1], sys.argv[2]
 txt=open(dot).read()
 nodes={}
-for m in re.finditer(r'"graph_0_node_(\d+)"\[style="\w+"shape="record"label="\{\n(\w+)\n(.*?)\}"\];', txt, re.S):
+for m in re.finditer(r'"graph_\d+_node_(\d+)"\[style="\w+"shape="record"label="\{\n(\w+)\n(.*?)\}"\];', txt, re.S):
     nid, kind, body = int(m.group(1)), m.group(2), m.group(3)
     k = re.search(r"\{ID \| \d+ \| (.*?)\\<\\<\\<\((\d+),(\d+),(\d+)\),\((\d+),(\d+),(\d+)\)", body)
     nodes[nid]={"kind":kind,"name":k.group(1) if k else kind,"grid":tuple(int(k.group(i)) for i in (2,3,4)) if k else None,"block":tuple(int(k.group(i)) for i in (5,6,7)) if k else None}
-edges=[(int(a),int(b)) for a,b in re.findall(r'"graph_0_node_(\d+)" -> "graph_0_node_(\d+)"', txt)]
+edges=[(int(a),int(b)) for a,b in re.findall(r'"graph_\d+_node_(\d+)" -> "graph_\d+_node_(\d+)"', txt)]
 names=[nodes[i]["name"] for i in sorted(nodes)]
 dem=D.demangle(names)
 for i,d in zip(sorted(nodes),dem): nodes[i]["d"]=D.short(d)
