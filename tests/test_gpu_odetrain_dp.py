@@ -228,25 +228,32 @@ def test_nan_state_reproduced_by_oracle(B, S):
     from fiode_amd.graph_step import GraphTrainStep
     from tests.test_gpu_sampler import masks_from_keep_words
     dev = _dev()
-    mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5", h_sample=S)
-    mod.seed = 1000
-    opt = mod.configure_optimizers(capturable=True)[0][0]
-    g = torch.Generator(device="cpu").manual_seed(1234)
-    x = torch.rand(B, 3, 32, 32, generator=g).to(dev)
-    y = torch.randint(0, 10, (B,), generator=g).to(dev)
-    gs = GraphTrainStep(mod, opt, x, y, check_every=0)
+    # configs[4]'s NaN steps come at the third replay; configs[2]'s are rarer (3 of 25 bench replays
+    # in round 4) and move with the last bits of the backbone's arithmetic, so at B = 128 several
+    # synthetic batches are searched (the first NaN replay found is the state checked)
+    batch_seeds, reps = ([1234], 30) if B == 1024 else ([1234, 1, 2, 3, 4, 5, 6, 7], 60)
     nan_step = None
-    for i in range(30):
-        loss = gs.step()
-        torch.cuda.synchronize()
-        if not bool(torch.isfinite(loss).all()):
-            nan_step = i
+    for bseed in batch_seeds:
+        mod = bench.build_module(dev, seed=0, train_ode=True, solver="dopri5", h_sample=S)
+        mod.seed = 1000
+        opt = mod.configure_optimizers(capturable=True)[0][0]
+        g = torch.Generator(device="cpu").manual_seed(bseed)
+        x = torch.rand(B, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (B,), generator=g).to(dev)
+        gs = GraphTrainStep(mod, opt, x, y, check_every=0)
+        for i in range(reps):
+            loss = gs.step()
+            torch.cuda.synchronize()
+            if not bool(torch.isfinite(loss).all()):
+                nan_step = i
+                break
+        if nan_step is not None:
             break
+        gs.close()
     if nan_step is None and B == 128:
-        # configs[2]'s NaN steps are rarer (3 of 25 bench replays in round 4) and move with the last
-        # bits of the backbone's arithmetic; configs[4]'s come at the third replay
-        pytest.skip("no NaN step in 30 replays at B = 128 with this build's rounding")
-    assert nan_step is not None, "no NaN step in 30 replays"
+        pytest.skip(f"no NaN step in {reps} replays of {len(batch_seeds)} batches at B = 128 with this build's rounding")
+    assert nan_step is not None, f"no NaN step in {reps} replays"
+    print(f"batch seed {bseed}")
     assert gs.skipped_steps() == 1                 # the guard kept the update away
     yh_graph = mod.last_plan["y_hat"].detach().clone()
     counter = int(mod.rng_counter.item()) - 1      # the replay's Philox offset (advanced after it)
