@@ -307,6 +307,10 @@ class DecisionBoundary(nn.Module):
         return torch.log(v) if self.log_mode else v
 
 
+# the solve's h0 kept contiguous between steps (tools/ab_step.py `h0_copy`: copied every step)
+H0_CACHE = True
+
+
 class UniformInitFun(nn.Module):
     """dynamics/init_coordinates.py:38-44: h0 = 1/C, static = param_map(x)."""
 
@@ -697,7 +701,7 @@ class LyapunovLearning(nn.Module):
         self.model(x); the backbone is deterministic (no dropout / batch norm), so static_state is
         reused.  Its persistent kernel occupies B/32 CUs for the whole solve, so on ROCm it is
         launched on a side stream and overlaps the fan-out kernels."""
-        h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
+        h0 = self._h0(static_state.shape[0])
         plan = self.ode_plan(static_state.shape[0], masks)
         # leaf parameters (the biases) enter the side-stream solve through views taken here, on the
         # step stream: their AccumulateGrad nodes then receive every gradient on the step stream
@@ -713,6 +717,21 @@ class LyapunovLearning(nn.Module):
             return _prefetch(self._ode_stream, lambda: ODETrainFn.apply(*args))
         return ODETrainFn.apply(*args)
 
+    def _h0(self, B: int) -> torch.Tensor:
+        """The solve's initial state h0 = 1/C for every row (init_coordinates.py:38-44) as the
+        contiguous [B][C] the kernels read.  Kept from an eager call (the GraphTrainStep warm-up)
+        while the buffer is unchanged, so a captured step holds no copy kernel right before the
+        solve; never made inside a capture (a captured copy would only run at replay)."""
+        h0_0 = self.init_coordinates.h0_0
+        key = (B, h0_0.device, h0_0.data_ptr(), h0_0._version)
+        c = getattr(self, "_h0_cache", None)
+        if H0_CACHE and c is not None and c[0] == key:
+            return c[1]
+        h0 = h0_0[None].expand(B, -1).float().contiguous()
+        if H0_CACHE and not (h0.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self._h0_cache = (key, h0)
+        return h0
+
     def _lyap_ode_loss(self, x, static_state, w, y, plan):
         """The fused configs[1] loss (LyapODELossFn): one autograd node for the Lyapunov step, the
         train_ode solve and the mix (pl_modules.py:444-500)."""
@@ -720,7 +739,7 @@ class LyapunovLearning(nn.Module):
         if not self.ode_reuse_features:
             # reference order: self.model(x, ...) re-runs the backbone (pl_modules.py:491)
             x_ode, _ = self.init_coordinates(x, self.dyn_fun)
-        h0 = self.init_coordinates.h0_0[None].expand(static_state.shape[0], -1).float()
+        h0 = self._h0(static_state.shape[0])
         oplan = self.ode_plan(static_state.shape[0])
         self.last_ode_plan = oplan
         stream = None
