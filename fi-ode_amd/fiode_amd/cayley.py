@@ -531,8 +531,17 @@ HEAD_WGRAD_SIDE = os.environ.get("FIODE_HEAD_WGRAD_SIDE", "1") != "0"
 _HEAD_STREAMS: dict = {}
 
 
-def _head_stream(dev: torch.device) -> torch.cuda.Stream:
-    key = dev.index
+# side streams of the head's weight gradients: 3 = one stream per layer (the step's stream joins
+# them all at the end of the head's backward; layer 3's is also the conv weight gradients' stream).
+# With 1 the three layers' products and bias sums ran in sequence on one stream, and that ~55 us
+# chain, not the input-gradient chain, was the head backward's part of the step's dependency path
+# (profiles/r06/dag_warm/): 3 streams measured 8-23 us faster per step, 2 streams or the bias sums on
+# three more streams slower (profiles/r06/ab_head_wgrad_streams.json)
+HEAD_WGRAD_STREAMS = 3
+
+
+def _head_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
+    key = (dev.index, k % HEAD_WGRAD_STREAMS)
     if key not in _HEAD_STREAMS:
         _HEAD_STREAMS[key] = new_stream(dev)
     return _HEAD_STREAMS[key]
@@ -544,8 +553,8 @@ class _LinearHeadFn(torch.autograd.Function):
     sum in sequence on one stream, so the next layer's input gradient waited for the weight
     gradient it does not need (the head's backward is on the step's critical path).  Here the
     weight / bias gradients (the same GEMM g^T x and column sum) of every layer run on a side
-    stream forked as soon as that layer's output gradient exists, beside the input-gradient chain,
-    and join the step's stream once at the end.  The products go through ops.mm (the library GEMM
+    stream of their own (HEAD_WGRAD_STREAMS) forked as soon as that layer's output gradient exists,
+    beside the input-gradient chain, and join the step's stream once at the end.  The products go through ops.mm (the library GEMM
     at this site: ops.MM_LIBRARY_SITES), the output layer fiode_head_out / _backward_gs when it has
     <= 16 outputs (KWLargeConcat's 10 classes; a wider out_dim, e.g. make_ortho_KWLarge_Concat's
     default 128, takes ops.mm + the GroupSort kernel)."""
@@ -578,10 +587,13 @@ class _LinearHeadFn(torch.autograd.Function):
         h, Q1, Q2, Q3, y1, z1, y2, z2 = ctx.saved_tensors
         g = g.contiguous()
         cur = torch.cuda.current_stream(g.device)
-        side = _head_stream(g.device)
+        sides = []
         wg = {}
 
         def wgrad(k, gk, x):
+            side = _head_stream(g.device, k)
+            if side not in sides:
+                sides.append(side)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 wg[k] = (ops.mm(gk.t(), x, site="head"), gk.sum(0))
@@ -594,7 +606,8 @@ class _LinearHeadFn(torch.autograd.Function):
         g1 = ops.groupsort_backward(y1, ops.mm(g2, Q2, site="head"), 1)
         wgrad(1, g1, h)
         dh = ops.mm(g1, Q1, site="head")
-        cur.wait_stream(side)
+        for side in sides:
+            cur.wait_stream(side)
         for dW, db in wg.values():
             dW.record_stream(cur)
             db.record_stream(cur)

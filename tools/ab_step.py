@@ -291,6 +291,12 @@ def no_warm(m):
     m._no_warm = True
 
 
+def head_wg1(m):
+    from fiode_amd import cayley as CY
+    CY.HEAD_WGRAD_STREAMS = 1     # the head's three weight gradients in sequence on one stream (before r06)
+    RESTORE.append(lambda: setattr(CY, "HEAD_WGRAD_STREAMS", 3))
+
+
 def h0_copy(m):
     from fiode_amd import lyapunov as LY
     LY.H0_CACHE = False
@@ -344,7 +350,7 @@ def no_pair(m):
 # streams, fiode_cgemm for w G X^H, the library for thin / Q^H G products, h0 repeat, the pre-solve
 # zero fill, one shared conv map stream) are kept only as records in DESIGN.md section 11
 ALL = {"default": default, "ws_fill": ws_fill, "no_pair": no_pair, "lib_gemm": lib_gemm, "wgrad_lib": wgrad_lib, "r05_gemms": r05_gemms, "lib_dense_fwd": _lib_site("dense_fwd"),
-       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "h0_copy": h0_copy, "no_warm": no_warm, "prio_otf": _prio(1), "prio_otb": _prio(2), "prio_small": _prio(4),
+       "lib_dense_bwd": _lib_site("dense_bwd"), "lib_head": _lib_site("head"), "lib3": lib3, "own_gemm": own_gemm, "h0_copy": h0_copy, "head_wg1": head_wg1, "no_warm": no_warm, "prio_otf": _prio(1), "prio_otb": _prio(2), "prio_small": _prio(4),
        "prio_pinv": _prio(8), "prio_all": _prio(15), "prio_ot": _prio(3),
        "prio_none": _prio(0), "all_first_side": all_first_side, "head_join_early": head_join_early, "head_autograd": head_autograd, "conv_wgrad_main": conv_wgrad_main,
        "cap_hi": cap_hi, "ode_lo": ode_lo, "norm_unfused": norm_unfused, "nchw_last_off": nchw_last_off, "dyn_wgrad_main": dyn_wgrad_main, "qx_off": qx_off, "head_out_lib": head_out_lib, "all_first": all_first, "first_ab": first_ab, "first_dyn": first_dyn,
