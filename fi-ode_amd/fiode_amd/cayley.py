@@ -537,7 +537,7 @@ _HEAD_STREAMS: dict = {}
 # chain, not the input-gradient chain, was the head backward's part of the step's dependency path
 # (profiles/r06/dag_warm/): 3 streams measured 8-23 us faster per step, 2 streams or the bias sums on
 # three more streams slower (profiles/r06/ab_head_wgrad_streams.json)
-HEAD_WGRAD_STREAMS = 3
+HEAD_WGRAD_STREAMS = int(os.environ.get("FIODE_HEAD_WGRAD_STREAMS", "3"))
 
 
 def _head_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
